@@ -1,0 +1,172 @@
+/*
+ * isim.h — C ABI of the MI355X-native isotope trace simulator ("isim").
+ *
+ * This is the drop-in boundary for ONE hot path of adalrsjr1/istio-isotope:
+ * executing isotope service-graph scripts (isotope/service/pkg/srv) for many
+ * independent request traces, over graphs loaded with isotope's own
+ * service-graph schema (isotope/convert/pkg/graph).  Plain C types only: a Go
+ * host binds it through cgo, Python through ctypes.
+ *
+ * Reference interfaces replaced (file:line relative to the reference repo):
+ *   isim_graph_unmarshal_json  <- (*graph.ServiceGraph).UnmarshalJSON
+ *                                 isotope/convert/pkg/graph/unmarshal.go:30-48
+ *                                 (reached through sigs.k8s.io/yaml.Unmarshal,
+ *                                 isotope/service/pkg/srv/graph.go:82-94; the
+ *                                 host does the YAML->JSON step)
+ *   isim_handler_create        <- srv.HandlerFromServiceGraphYAML(path, name)
+ *                                 isotope/service/pkg/srv/graph.go:34-60
+ *                                 (extractService :97-109, extractServiceTypes :113-120)
+ *   isim_serve / isim_serve_device
+ *                              <- Handler.ServeHTTP  isotope/service/pkg/srv/handler.go:37-79
+ *                                 + execute / executeRequestCommand /
+ *                                 executeConcurrentCommand executable.go:43-179,
+ *                                 run for n_traces independent client requests
+ *                                 in virtual integer-nanosecond time
+ *   stats words                <- prometheus.Record* isotope/service/pkg/srv/prometheus/handler.go:87-106
+ *
+ * Semantics: "isim semantics v1" (SURVEY.md Appendix A).
+ * Errors: every function returns an isim_status; isim_last_error() gives a
+ * thread-local message (the Go error text for graph-load errors).
+ * Thread-safety: distinct handles may be used concurrently; a handle may be
+ * served from several threads onto different devices.
+ */
+#ifndef ISIM_H
+#define ISIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ISIM_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define ISIM_API __attribute__((visibility("default")))
+#else
+#define ISIM_API
+#endif
+
+typedef enum {
+  ISIM_OK = 0,
+  ISIM_EINVAL = 1,   /* bad argument, or no isEntrypoint service */
+  ISIM_ENOMEM = 2,
+  ISIM_EHIP = 3,     /* HIP runtime error */
+  ISIM_EPARSE = 4,   /* graph load error: the Go error text is in isim_last_error() */
+  ISIM_ECYCLE = 5,   /* call cycle reachable from the entry (would recurse forever) */
+  ISIM_EDEPTH = 6,   /* call depth above isim_params.max_depth (<= 64) */
+  ISIM_ERANGE = 7,   /* hop cost / latency bound overflows int64 */
+  ISIM_ENOTFOUND = 8,/* service name not in graph */
+  ISIM_ENODEV = 9    /* no usable gfx950 device */
+} isim_status;
+
+/* Error propagation mode. */
+#define ISIM_MODE_A 0u /* reference: a callee's 500 is swallowed (executable.go:131-143) */
+#define ISIM_MODE_B 1u /* EXT: a callee's 500 fails the calling step and aborts the script */
+
+typedef struct isim_graph isim_graph;
+typedef struct isim_handler isim_handler;
+
+/* Simulation parameters (the hop-cost model replaces the HTTP transport of
+ * isotope/service/pkg/srv/request.go:30-64):
+ *   H(call) = hop_base_ns + floor((size*req_ps_per_byte + responseSize(callee)*resp_ps_per_byte)/1000) */
+typedef struct {
+  uint64_t seed;             /* Philox4x32-10 key = (seed_lo, seed_hi) */
+  uint64_t hop_base_ns;
+  uint64_t req_ps_per_byte;
+  uint64_t resp_ps_per_byte;
+  uint32_t error_mode;       /* ISIM_MODE_A / ISIM_MODE_B */
+  uint32_t max_depth;        /* 0 = 64; at most 64 */
+} isim_params;
+
+/* One 16-byte record per simulated request trace. */
+typedef struct {
+  uint64_t latency_ns;       /* T(entry): virtual duration of the entry's ServeHTTP */
+  uint32_t hops;             /* executed invocations (entry included) */
+  uint32_t status_err;       /* bit31: entry responded 500; bits0-30: invocations that responded 500 */
+} isim_trace_rec;
+
+/* Layout of the u64 stats buffer filled by isim_serve*.  Offsets in words. */
+#define ISIM_ST_N_TRACES 0
+#define ISIM_ST_SUM_LATENCY 1
+#define ISIM_ST_SUM_HOPS 2
+#define ISIM_ST_SUM_ERR_HOPS 3
+#define ISIM_ST_N_500 4
+#define ISIM_ST_NOT_MIN_LATENCY 5 /* ~min latency (so min and max both merge with MAX) */
+#define ISIM_ST_MAX_LATENCY 6
+#define ISIM_ST_PROM 8            /* [2][33] latency histogram, Prometheus duration buckets
+                                     (prometheus/handler.go:26-31), index [status500][bucket] */
+#define ISIM_N_PROM 33
+#define ISIM_ST_LOG2 (ISIM_ST_PROM + 2 * ISIM_N_PROM) /* [2][64] latency histogram by bit length */
+#define ISIM_N_LOG2 64
+#define ISIM_ST_SITES (ISIM_ST_LOG2 + 2 * ISIM_N_LOG2) /* [2][n_slots]: executed calls, then callee 500s,
+                                                          per reachable call site slot */
+
+typedef struct {
+  int32_t n_services;        /* services in the graph */
+  int32_t n_sites;           /* call commands in the graph (document order) */
+  int32_t n_slots;           /* call sites reachable from the entry (stats slots) */
+  int32_t entry;             /* entry service index */
+  int32_t max_depth;         /* deepest call chain from the entry (entry = 1) */
+  int32_t static_walk;       /* 1: every invocation executes in every trace */
+  int32_t time_bits;         /* 32 or 64: per-lane time width of the kernel */
+  int32_t program_len;       /* instructions in the device program */
+  uint64_t max_latency_ns;   /* static upper bound of any trace's latency */
+  uint64_t hops_upper;       /* static upper bound of invocations per trace */
+  uint64_t stats_words;      /* u64 words of the stats buffer */
+} isim_handler_info;
+
+ISIM_API const char *isim_last_error(void);
+ISIM_API int isim_abi_version(void);
+
+/* ---- graph (convert/pkg/graph) ---- */
+ISIM_API int isim_graph_unmarshal_json(const char *json, size_t len, isim_graph **out);
+ISIM_API void isim_graph_free(isim_graph *g);
+ISIM_API int isim_graph_num_services(const isim_graph *g);
+/* Exact implementation-neutral dump of the decoded graph.
+ * Writes at most cap bytes (NUL-terminated when it fits); *len = bytes needed. */
+ISIM_API int isim_graph_canonical_json(const isim_graph *g, char *buf, size_t cap, size_t *len);
+/* extractService: first service with that name (graph.go:97-109); -1 if absent. */
+ISIM_API int isim_graph_service_index(const isim_graph *g, const char *name);
+
+/* ---- units (convert/pkg/graph/size, pct, script/sleep_command.go) ---- */
+ISIM_API int isim_size_from_string(const char *s, uint64_t *out);        /* size.FromString */
+ISIM_API int isim_duration_parse(const char *s, int64_t *out_ns);        /* time.ParseDuration */
+ISIM_API int isim_percentage_from_string(const char *s, double *out);    /* pct.FromString */
+
+/* ---- handler (service/pkg/srv) ---- */
+/* service_name NULL: the first service with isEntrypoint: true. */
+ISIM_API int isim_handler_create(const isim_graph *g, const char *service_name, const isim_params *p,
+                        isim_handler **out);
+ISIM_API void isim_handler_free(isim_handler *h);
+ISIM_API int isim_handler_info_get(const isim_handler *h, isim_handler_info *out);
+/* Map of stats slots to the graph: slot -> call-site id (document order) and
+ * callee service index.  Arrays of info.n_slots entries. */
+ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32_t *slot_callee);
+
+/* Serve n_traces requests (trace ids [trace_begin, trace_begin+n_traces)) on
+ * the current HIP device, asynchronously on `hip_stream` (a hipStream_t, NULL =
+ * default stream).  d_records: device array of n_traces records or NULL.
+ * d_stats: device array of info.stats_words u64; ACCUMULATED into (zero it
+ * first; ~min word starts at 0).  No host synchronisation, no allocation:
+ * graph-capturable after the first call on a device. */
+ISIM_API int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces,
+                      isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
+
+/* Synchronous convenience: host buffers (either may be NULL), device `device`. */
+ISIM_API int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint64_t n_traces,
+               isim_trace_rec *h_records, uint64_t *h_stats);
+
+/* Fold a stats buffer into per-service / per-call-site counters:
+ * svc_calls[n_services] = incoming requests (RecordRequestReceived),
+ * svc_errs[n_services]  = responses with code 500 (RecordResponseSent),
+ * site_calls[n_sites]   = executed calls per call command (RecordRequestSent).
+ * Any output may be NULL. */
+ISIM_API int isim_stats_fold(const isim_handler *h, const uint64_t *stats, uint64_t *svc_calls,
+                    uint64_t *svc_errs, uint64_t *site_calls);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ISIM_H */

@@ -1,0 +1,328 @@
+// C ABI of libisim (include/isim.h): graph load, handler creation, device
+// program upload and the walk launch.  Host code; the kernel is in walk.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "../../include/isim.h"
+#include "gounits.h"
+#include "graph.h"
+#include "kernel_abi.h"
+#include "program.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(ISIM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+struct DevState {
+  isim::Ins *d_prog = nullptr;
+  void *kernel = nullptr;
+  uint32_t threads = 0;
+  uint32_t lds_bytes = 0;
+  uint32_t lds_counters = 0;
+  uint32_t max_blocks = 0;  // resident workgroups for the whole device
+};
+
+}  // namespace
+
+struct isim_graph {
+  isim::ServiceGraph g;
+};
+
+struct isim_handler {
+  isim::Program prog;
+  isim_params params{};
+  std::mutex mu;
+  std::map<int, DevState> dev;
+  ~isim_handler() {
+    for (auto &kv : dev) {
+      int cur = 0;
+      if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
+        (void)hipFree(kv.second.d_prog);
+        (void)hipSetDevice(cur);
+      }
+    }
+  }
+};
+
+namespace {
+
+// LDS layout of the walk kernel for a given workgroup size (walk.hip).
+uint32_t lds_need(const isim::Program &p, uint32_t waves, bool counters) {
+  uint32_t b = isim::kLdsAccBytes + isim::kHistWords * 4u;
+  if (counters) b += 8u * (uint32_t)p.n_slots;
+  b = (b + 15u) & ~15u;
+  if (!p.static_walk) {
+    uint32_t tt = p.time_bits == 32 ? 4u : 8u;
+    b += waves * (uint32_t)p.max_frames * 64u * (2u * tt + 4u);
+  }
+  return b;
+}
+
+int prepare_device(isim_handler *h, int device, DevState *&out) {
+  std::lock_guard<std::mutex> lk(h->mu);
+  auto it = h->dev.find(device);
+  if (it != h->dev.end()) {
+    out = &it->second;
+    return ISIM_OK;
+  }
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(ISIM_ENODEV, std::string("libisim is built for gfx950 only; device is ") + prop.gcnArchName);
+  const isim::Program &p = h->prog;
+  DevState st;
+  const uint32_t lds_max = (uint32_t)prop.sharedMemPerBlock;  // 160 KiB on gfx950
+  // Largest workgroup (waves) whose LDS fits, counters in LDS if possible.
+  bool counters = true;
+  uint32_t waves = 16;
+  while (waves > 1 && lds_need(p, waves, counters) > lds_max) waves >>= 1;
+  if (lds_need(p, waves, counters) > lds_max) {
+    counters = false;
+    waves = 16;
+    while (waves > 1 && lds_need(p, waves, counters) > lds_max) waves >>= 1;
+    if (lds_need(p, waves, counters) > lds_max)
+      return fail(ISIM_EDEPTH, "call stack does not fit in LDS");
+  }
+  st.threads = waves * 64u;
+  st.lds_bytes = lds_need(p, waves, counters);
+  st.lds_counters = counters ? 1u : 0u;
+  st.kernel = isim::walk_kernel(p.static_walk, h->params.error_mode == ISIM_MODE_B, p.time_bits == 64);
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)st.kernel, (int)st.threads,
+                                                      st.lds_bytes));
+  if (per_cu < 1) return fail(ISIM_EHIP, "walk kernel cannot be resident (occupancy 0)");
+  st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
+  HIPCHK(hipMalloc(&st.d_prog, p.code.size() * sizeof(isim::Ins)));
+  HIPCHK(hipMemcpy(st.d_prog, p.code.data(), p.code.size() * sizeof(isim::Ins), hipMemcpyHostToDevice));
+  auto res = h->dev.emplace(device, st);
+  out = &res.first->second;
+  return ISIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *isim_last_error(void) { return g_err.c_str(); }
+int isim_abi_version(void) { return ISIM_ABI_VERSION; }
+
+int isim_graph_unmarshal_json(const char *json, size_t len, isim_graph **out) {
+  if (!json || !out) return fail(ISIM_EINVAL, "null argument");
+  isim_graph *g = new (std::nothrow) isim_graph();
+  if (!g) return fail(ISIM_ENOMEM, "out of memory");
+  std::string err;
+  if (!isim::unmarshal_service_graph(json, len, g->g, err)) {
+    delete g;
+    return fail(ISIM_EPARSE, err);
+  }
+  *out = g;
+  return ISIM_OK;
+}
+
+void isim_graph_free(isim_graph *g) { delete g; }
+
+int isim_graph_num_services(const isim_graph *g) { return g ? (int)g->g.services.size() : -1; }
+
+int isim_graph_canonical_json(const isim_graph *g, char *buf, size_t cap, size_t *len) {
+  if (!g) return fail(ISIM_EINVAL, "null graph");
+  std::string s = isim::canonical_json(g->g);
+  if (len) *len = s.size() + 1;
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return ISIM_OK;
+}
+
+int isim_graph_service_index(const isim_graph *g, const char *name) {
+  if (!g || !name) return -1;
+  return isim::service_index(g->g, name);
+}
+
+int isim_size_from_string(const char *s, uint64_t *out) {
+  if (!s || !out) return fail(ISIM_EINVAL, "null argument");
+  std::string err;
+  if (!isim::size_from_string(s, *out, err)) return fail(ISIM_EPARSE, err);
+  return ISIM_OK;
+}
+
+int isim_duration_parse(const char *s, int64_t *out_ns) {
+  if (!s || !out_ns) return fail(ISIM_EINVAL, "null argument");
+  std::string err;
+  if (!isim::go_parse_duration(s, *out_ns, err)) return fail(ISIM_EPARSE, err);
+  return ISIM_OK;
+}
+
+int isim_percentage_from_string(const char *s, double *out) {
+  if (!s || !out) return fail(ISIM_EINVAL, "null argument");
+  std::string err;
+  if (!isim::pct_from_string(s, *out, err)) return fail(ISIM_EPARSE, err);
+  return ISIM_OK;
+}
+
+int isim_handler_create(const isim_graph *g, const char *service_name, const isim_params *p,
+                        isim_handler **out) {
+  if (!g || !p || !out) return fail(ISIM_EINVAL, "null argument");
+  int32_t entry = -1;
+  if (service_name) {
+    entry = isim::service_index(g->g, service_name);
+    if (entry < 0) return fail(ISIM_ENOTFOUND, std::string("service with name ") + service_name + " does not exist");
+  } else {
+    for (size_t i = 0; i < g->g.services.size(); ++i)
+      if (g->g.services[i].is_entrypoint) {
+        entry = (int32_t)i;
+        break;
+      }
+    if (entry < 0) return fail(ISIM_EINVAL, "no service has isEntrypoint: true");
+  }
+  isim_handler *h = new (std::nothrow) isim_handler();
+  if (!h) return fail(ISIM_ENOMEM, "out of memory");
+  h->params = *p;
+  std::string err;
+  int rc = isim::compile_program(g->g, entry, *p, h->prog, err);
+  if (rc != ISIM_OK) {
+    delete h;
+    return fail(rc, err);
+  }
+  *out = h;
+  return ISIM_OK;
+}
+
+void isim_handler_free(isim_handler *h) { delete h; }
+
+int isim_handler_info_get(const isim_handler *h, isim_handler_info *out) {
+  if (!h || !out) return fail(ISIM_EINVAL, "null argument");
+  const isim::Program &p = h->prog;
+  out->n_services = p.n_services;
+  out->n_sites = p.n_sites;
+  out->n_slots = p.n_slots;
+  out->entry = p.entry;
+  out->max_depth = p.max_depth;
+  out->static_walk = p.static_walk ? 1 : 0;
+  out->time_bits = p.static_walk ? 64 : p.time_bits;
+  out->program_len = (int32_t)p.code.size();
+  out->max_latency_ns = p.max_latency;
+  out->hops_upper = p.hops_upper;
+  out->stats_words = ISIM_ST_SITES + 2ull * (uint64_t)p.n_slots;
+  return ISIM_OK;
+}
+
+int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32_t *slot_callee) {
+  if (!h) return fail(ISIM_EINVAL, "null handler");
+  const isim::Program &p = h->prog;
+  if (slot_site) std::copy(p.slot_site.begin(), p.slot_site.end(), slot_site);
+  if (slot_callee) std::copy(p.slot_callee.begin(), p.slot_callee.end(), slot_callee);
+  return ISIM_OK;
+}
+
+int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, isim_trace_rec *d_records,
+                      uint64_t *d_stats, void *hip_stream) {
+  if (!h || !d_stats) return fail(ISIM_EINVAL, "null argument");
+  if (n_traces == 0) return ISIM_OK;
+  int device = 0;
+  HIPCHK(hipGetDevice(&device));
+  DevState *st = nullptr;
+  int rc = prepare_device(h, device, st);
+  if (rc != ISIM_OK) return rc;
+  isim::KParams kp{};
+  kp.prog = st->d_prog;
+  kp.trace_begin = trace_begin;
+  kp.n_traces = n_traces;
+  kp.records = d_records;
+  kp.stats = d_stats;
+  kp.seed_lo = (uint32_t)h->params.seed;
+  kp.seed_hi = (uint32_t)(h->params.seed >> 32);
+  kp.n_slots = (uint32_t)h->prog.n_slots;
+  kp.max_frames = (uint32_t)h->prog.max_frames;
+  kp.lds_counters = st->lds_counters;
+  const uint64_t batches = (n_traces + 63) / 64;
+  const uint64_t waves = st->threads / 64;
+  const uint64_t want = (batches + waves - 1) / waves;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);
+  void *args[] = {&kp};
+  HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
+                         (hipStream_t)hip_stream));
+  return ISIM_OK;
+}
+
+int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint64_t n_traces, isim_trace_rec *h_records,
+               uint64_t *h_stats) {
+  if (!h) return fail(ISIM_EINVAL, "null handler");
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  HIPCHK(hipSetDevice(device));
+  const uint64_t words = ISIM_ST_SITES + 2ull * (uint64_t)h->prog.n_slots;
+  uint64_t *d_stats = nullptr;
+  isim_trace_rec *d_rec = nullptr;
+  int rc = ISIM_OK;
+  hipStream_t s = nullptr;
+  do {
+    if (hipStreamCreate(&s) != hipSuccess) { rc = fail(ISIM_EHIP, "hipStreamCreate failed"); break; }
+    if (hipMalloc(&d_stats, words * 8) != hipSuccess) { rc = fail(ISIM_EHIP, "hipMalloc(stats) failed"); break; }
+    if (hipMemsetAsync(d_stats, 0, words * 8, s) != hipSuccess) { rc = fail(ISIM_EHIP, "hipMemset failed"); break; }
+    if (h_records && n_traces) {
+      if (hipMalloc(&d_rec, n_traces * sizeof(isim_trace_rec)) != hipSuccess) {
+        rc = fail(ISIM_EHIP, "hipMalloc(records) failed");
+        break;
+      }
+    }
+    rc = isim_serve_device(h, trace_begin, n_traces, d_rec, d_stats, s);
+    if (rc != ISIM_OK) break;
+    if (hipStreamSynchronize(s) != hipSuccess) { rc = fail(ISIM_EHIP, "walk kernel failed"); break; }
+    if (h_stats && hipMemcpy(h_stats, d_stats, words * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "copy stats failed");
+      break;
+    }
+    if (h_records && d_rec &&
+        hipMemcpy(h_records, d_rec, n_traces * sizeof(isim_trace_rec), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "copy records failed");
+      break;
+    }
+  } while (0);
+  if (d_rec) (void)hipFree(d_rec);
+  if (d_stats) (void)hipFree(d_stats);
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int isim_stats_fold(const isim_handler *h, const uint64_t *stats, uint64_t *svc_calls, uint64_t *svc_errs,
+                    uint64_t *site_calls) {
+  if (!h || !stats) return fail(ISIM_EINVAL, "null argument");
+  const isim::Program &p = h->prog;
+  if (svc_calls) std::fill(svc_calls, svc_calls + p.n_services, 0);
+  if (svc_errs) std::fill(svc_errs, svc_errs + p.n_services, 0);
+  if (site_calls) std::fill(site_calls, site_calls + p.n_sites, 0);
+  const uint64_t *calls = stats + ISIM_ST_SITES;
+  const uint64_t *errs = calls + p.n_slots;
+  for (int32_t s = 0; s < p.n_slots; ++s) {
+    if (svc_calls) svc_calls[p.slot_callee[s]] += calls[s];
+    if (svc_errs) svc_errs[p.slot_callee[s]] += errs[s];
+    if (site_calls) site_calls[p.slot_site[s]] += calls[s];
+  }
+  // the client request into the entry is not a call site
+  if (svc_calls) svc_calls[p.entry] += stats[ISIM_ST_N_TRACES];
+  if (svc_errs) svc_errs[p.entry] += stats[ISIM_ST_N_500];
+  return ISIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Shared between the host program compiler and the HIP walk kernel: the
+// device instruction format and the kernel argument block.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/isim.h"
+
+namespace isim {
+
+enum Op : uint32_t {
+  OP_HALT = 0,
+  OP_SLEEP = 1,   // acc += d
+  OP_CBEGIN = 2,  // cmax = 0, cerr = 0
+  OP_CSLEEP = 3,  // cmax = max(cmax, d)
+  OP_CEND = 4,    // acc += cmax; mode B: failed |= cerr
+  OP_CALL = 5,    // invoke a service with a script that makes calls
+  OP_LEAF = 6,    // invoke a service whose script makes no calls
+  OP_RET = 7,     // end of a service body (respond)
+};
+
+enum Flag : uint32_t {
+  F_CONC = 1,        // the call is a sub-command of a concurrent step
+  F_PROB = 2,        // probability 1..99: draw to skip
+  F_ERR_ALWAYS = 4,  // callee errorRate == 1
+  F_ERR_DRAW = 8,    // 0 < callee errorRate < 1: draw against thr
+  F_ROOT = 16,       // the client request into the entry (no call site)
+};
+
+// 32-byte instruction, read by the kernel with one scalar load.
+struct Ins {
+  uint32_t opf;   // op | flags << 8 | probability << 16
+  uint32_t k;     // CALL/LEAF: index of the call command in the caller's script
+  uint32_t thr;   // CALL/LEAF: callee error threshold (F_ERR_DRAW)
+  uint32_t slot;  // CALL/LEAF: stats slot of the call site
+  uint32_t a_lo, a_hi;  // CALL/LEAF: hop cost H; SLEEP/CSLEEP: duration
+  uint32_t b_lo, b_hi;  // CALL: target pc (b_lo); LEAF: callee latency
+};
+static_assert(sizeof(Ins) == 32, "Ins must be 32 bytes");
+
+struct KParams {
+  const Ins *prog;
+  uint64_t trace_begin;
+  uint64_t n_traces;
+  isim_trace_rec *records;  // may be null
+  uint64_t *stats;
+  uint32_t seed_lo, seed_hi;
+  uint32_t n_slots;
+  uint32_t max_frames;
+  uint32_t lds_counters;    // 1: per-site counters in the LDS table
+  uint32_t pad;
+};
+
+constexpr uint32_t kWgThreads = 1024;                 // max workgroup size (launch bound)
+constexpr uint32_t kLdsAccBytes = 64;                 // WgAcc
+constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
+
+// walk.hip: kernel pointer for a walk variant.
+void *walk_kernel(bool is_static, bool modeb, bool time64);
+
+}  // namespace isim

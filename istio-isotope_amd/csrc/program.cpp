@@ -1,0 +1,296 @@
+// Graph -> device program.  See program.h and DESIGN.md §4.
+#include "program.h"
+
+#include <algorithm>
+#include <unordered_map>
+
+#include "gounits.h"
+
+namespace isim {
+namespace {
+
+constexpr uint64_t kTimeCap = 1ull << 63;  // latencies must stay below 2^63 ns
+
+struct Site {
+  int32_t caller, callee;
+  uint64_t size;
+  int64_t prob;
+  uint32_t k;     // index of the call command within the caller's script
+  bool conc;
+  uint64_t hop;   // H
+};
+
+uint64_t sat_add(uint64_t a, uint64_t b) {
+  uint64_t r = a + b;
+  return (r < a || r >= kTimeCap) ? kTimeCap : r;
+}
+
+uint64_t sleep_ns(int64_t d) { return d > 0 ? (uint64_t)d : 0; }
+
+}  // namespace
+
+int32_t service_index(const ServiceGraph &g, const std::string &name) {
+  for (size_t i = 0; i < g.services.size(); ++i)
+    if (g.services[i].name == name) return (int32_t)i;
+  return -1;
+}
+
+int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, Program &out,
+                    std::string &err) {
+  const int32_t n = (int32_t)g.services.size();
+  if (entry < 0 || entry >= n) {
+    err = "entry service out of range";
+    return ISIM_EINVAL;
+  }
+  if (p.error_mode > ISIM_MODE_B) {
+    err = "error_mode must be ISIM_MODE_A or ISIM_MODE_B";
+    return ISIM_EINVAL;
+  }
+  const uint32_t max_depth = p.max_depth == 0 ? 64 : p.max_depth;
+  if (max_depth > 64) {
+    err = "max_depth must be <= 64";
+    return ISIM_EINVAL;
+  }
+  const bool modeb = p.error_mode == ISIM_MODE_B;
+  std::unordered_map<std::string, int32_t> index;
+  for (int32_t i = 0; i < n; ++i) index.emplace(g.services[i].name, i);  // first wins
+
+  // ---- call sites in document order: services, steps, concurrent sub-commands
+  std::vector<Site> sites;
+  std::vector<std::vector<int32_t>> svc_sites(n);
+  std::vector<uint64_t> thr(n);
+  for (int32_t s = 0; s < n; ++s) thr[s] = error_threshold(g.services[s].error_rate);
+  auto add_site = [&](int32_t s, const Command &c, uint32_t k, bool conc) -> bool {
+    Site st;
+    st.caller = s;
+    auto it = index.find(c.service);
+    if (it == index.end()) {  // impossible after validate(); keep the guard
+      err = "cannot call undefined service \"" + c.service + "\"";
+      return false;
+    }
+    st.callee = it->second;
+    st.size = c.size;
+    st.prob = c.probability;
+    st.k = k;
+    st.conc = conc;
+    unsigned __int128 h = (unsigned __int128)p.hop_base_ns +
+                          ((unsigned __int128)c.size * p.req_ps_per_byte +
+                           (unsigned __int128)g.services[st.callee].response_size * p.resp_ps_per_byte) /
+                              1000;
+    st.hop = h >= kTimeCap ? kTimeCap : (uint64_t)h;
+    svc_sites[s].push_back((int32_t)sites.size());
+    sites.push_back(st);
+    return true;
+  };
+  for (int32_t s = 0; s < n; ++s) {
+    uint32_t k = 0;
+    for (const Command &c : g.services[s].script) {
+      if (c.kind == Command::Request) {
+        if (!add_site(s, c, k++, false)) return ISIM_EPARSE;
+      } else if (c.kind == Command::Concurrent) {
+        for (const Command &x : c.commands)
+          if (x.kind == Command::Request && !add_site(s, x, k++, true)) return ISIM_EPARSE;
+      }
+    }
+  }
+
+  // ---- reachability, cycle check (EXT, F12) and post-order from the entry
+  std::vector<int8_t> color(n, 0);  // 0 white, 1 grey, 2 black
+  std::vector<int32_t> post, pre;
+  {
+    std::vector<std::pair<int32_t, size_t>> stack;
+    stack.push_back({entry, 0});
+    color[entry] = 1;
+    pre.push_back(entry);
+    while (!stack.empty()) {
+      auto &top = stack.back();
+      int32_t s = top.first;
+      if (top.second < svc_sites[s].size()) {
+        int32_t c = sites[svc_sites[s][top.second++]].callee;
+        if (color[c] == 1) {
+          err = "call cycle through service \"" + g.services[c].name + "\"";
+          return ISIM_ECYCLE;
+        }
+        if (color[c] == 0) {
+          color[c] = 1;
+          pre.push_back(c);
+          stack.push_back({c, 0});
+        }
+      } else {
+        color[s] = 2;
+        post.push_back(s);
+        stack.pop_back();
+      }
+    }
+  }
+
+  // ---- per-service static facts, children before parents
+  std::vector<uint64_t> tmax(n, 0), hops(n, 0);
+  std::vector<int32_t> depth(n, 0), frames(n, 0);
+  std::vector<char> leaf(n, 1), can_fail(n, 0);
+  bool any_prob = false, nonstatic_abort = false;
+  for (int32_t s : post) {
+    const Service &sv = g.services[s];
+    uint64_t T = 0, H = 1;
+    int32_t d = 1, fr = 0;
+    bool fail = thr[s] > 0;
+    size_t si = 0;  // walks svc_sites[s] in document order
+    const size_t nsteps = sv.script.size();
+    for (size_t step = 0; step < nsteps; ++step) {
+      const Command &c = sv.script[step];
+      bool step_fallible = false;
+      auto visit_call = [&](uint64_t &dt) {
+        const Site &st = sites[svc_sites[s][si++]];
+        leaf[s] = 0;
+        if (st.prob >= 1 && st.prob <= 99) any_prob = true;
+        dt = sat_add(st.hop, tmax[st.callee]);
+        H = std::min<uint64_t>(H + hops[st.callee], kTimeCap);
+        d = std::max(d, 1 + depth[st.callee]);
+        fr = std::max(fr, frames[st.callee]);
+        if (modeb && can_fail[st.callee]) step_fallible = true;
+      };
+      if (c.kind == Command::Sleep) {
+        T = sat_add(T, sleep_ns(c.sleep_ns));
+      } else if (c.kind == Command::Request) {
+        uint64_t dt;
+        visit_call(dt);
+        T = sat_add(T, dt);
+      } else {
+        uint64_t m = 0;
+        for (const Command &x : c.commands) {
+          uint64_t dt = 0;
+          if (x.kind == Command::Request) visit_call(dt);
+          else dt = sleep_ns(x.sleep_ns);
+          m = std::max(m, dt);
+        }
+        T = sat_add(T, m);
+      }
+      if (step_fallible) {
+        fail = true;
+        if (step + 1 < nsteps) nonstatic_abort = true;  // a failure would skip later steps
+      }
+    }
+    tmax[s] = T;
+    hops[s] = H;
+    depth[s] = d;
+    frames[s] = leaf[s] ? 0 : 1 + fr;
+    can_fail[s] = fail;
+  }
+  if (tmax[entry] >= kTimeCap) {
+    err = "latency bound of the entry overflows int64 nanoseconds";
+    return ISIM_ERANGE;
+  }
+  if ((uint32_t)depth[entry] > max_depth) {
+    err = "call depth " + std::to_string(depth[entry]) + " exceeds max_depth " + std::to_string(max_depth);
+    return ISIM_EDEPTH;
+  }
+
+  out = Program();
+  out.entry = entry;
+  out.n_services = n;
+  out.n_sites = (int32_t)sites.size();
+  out.max_depth = depth[entry];
+  out.max_frames = std::max(1, frames[entry]);
+  out.static_walk = !any_prob && !(modeb && nonstatic_abort);
+  out.max_latency = tmax[entry];
+  out.hops_upper = hops[entry];
+  out.time_bits = tmax[entry] < (1ull << 32) ? 32 : 64;
+  out.site_callee.resize(sites.size());
+  out.site_slot.assign(sites.size(), -1);
+  for (size_t i = 0; i < sites.size(); ++i) out.site_callee[i] = sites[i].callee;
+  // stats slots: reachable call sites in document order
+  for (size_t i = 0; i < sites.size(); ++i) {
+    if (color[sites[i].caller] == 2) {
+      out.site_slot[i] = (int32_t)out.slot_site.size();
+      out.slot_site.push_back((int32_t)i);
+      out.slot_callee.push_back(sites[i].callee);
+    }
+  }
+  out.n_slots = (int32_t)out.slot_site.size();
+
+  // ---- emit
+  auto err_flags = [&](int32_t callee) -> uint32_t {
+    if (thr[callee] >= (1ull << 32)) return F_ERR_ALWAYS;
+    return thr[callee] > 0 ? (uint32_t)F_ERR_DRAW : 0u;
+  };
+  auto make_invoke = [&](int32_t callee, uint64_t hop, uint32_t flags, uint32_t prob, uint32_t k,
+                         uint32_t slot) {
+    Ins in{};
+    const bool lf = leaf[callee];
+    flags |= err_flags(callee);
+    in.opf = (uint32_t)(lf ? OP_LEAF : OP_CALL) | (flags << 8) | (prob << 16);
+    in.k = k;
+    in.thr = (uint32_t)thr[callee];
+    in.slot = slot;
+    in.a_lo = (uint32_t)hop;
+    in.a_hi = (uint32_t)(hop >> 32);
+    if (lf) {
+      in.b_lo = (uint32_t)tmax[callee];
+      in.b_hi = (uint32_t)(tmax[callee] >> 32);
+    } else {
+      in.b_lo = (uint32_t)callee;  // patched to the body's pc below
+    }
+    return in;
+  };
+  std::vector<Ins> &code = out.code;
+  code.push_back(make_invoke(entry, 0, F_ROOT, 0, 0, 0));
+  Ins halt{};
+  halt.opf = OP_HALT;
+  code.push_back(halt);
+  std::vector<int32_t> body_pc(n, -1);
+  for (int32_t s : pre) {  // bodies in DFS preorder from the entry (streaming locality)
+    if (leaf[s]) continue;
+    body_pc[s] = (int32_t)code.size();
+    size_t si = 0;
+    for (const Command &c : g.services[s].script) {
+      Ins in{};
+      if (c.kind == Command::Sleep) {
+        uint64_t d = sleep_ns(c.sleep_ns);
+        in.opf = OP_SLEEP;
+        in.a_lo = (uint32_t)d;
+        in.a_hi = (uint32_t)(d >> 32);
+        code.push_back(in);
+      } else if (c.kind == Command::Request) {
+        int32_t sid = svc_sites[s][si++];
+        const Site &st = sites[sid];
+        uint32_t prob = (st.prob >= 1 && st.prob <= 99) ? (uint32_t)st.prob : 0;
+        code.push_back(make_invoke(st.callee, st.hop, prob ? F_PROB : 0, prob, st.k,
+                                   (uint32_t)out.site_slot[sid]));
+      } else {
+        in.opf = OP_CBEGIN;
+        code.push_back(in);
+        for (const Command &x : c.commands) {
+          Ins sub{};
+          if (x.kind == Command::Sleep) {
+            uint64_t d = sleep_ns(x.sleep_ns);
+            sub.opf = OP_CSLEEP;
+            sub.a_lo = (uint32_t)d;
+            sub.a_hi = (uint32_t)(d >> 32);
+            code.push_back(sub);
+          } else {
+            int32_t sid = svc_sites[s][si++];
+            const Site &st = sites[sid];
+            uint32_t prob = (st.prob >= 1 && st.prob <= 99) ? (uint32_t)st.prob : 0;
+            code.push_back(make_invoke(st.callee, st.hop, F_CONC | (prob ? (uint32_t)F_PROB : 0u), prob, st.k,
+                                       (uint32_t)out.site_slot[sid]));
+          }
+        }
+        Ins e{};
+        e.opf = OP_CEND;
+        code.push_back(e);
+      }
+    }
+    Ins r{};
+    r.opf = OP_RET;
+    code.push_back(r);
+  }
+  for (Ins &in : code)
+    if ((in.opf & 0xFF) == OP_CALL) in.b_lo = (uint32_t)body_pc[in.b_lo];
+  if (code.size() >= (1u << 30)) {
+    err = "program too large";
+    return ISIM_EINVAL;
+  }
+  return ISIM_OK;
+}
+
+}  // namespace isim

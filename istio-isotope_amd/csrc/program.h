@@ -1,0 +1,43 @@
+// Flattening of a loaded ServiceGraph into the device program the walk
+// kernel interprets.
+//
+// One code block per reachable non-leaf service (its script, in order),
+// ending in RET; a call is CALL (jump into the callee's block, return to the
+// next instruction) or LEAF (callee without calls: its whole invocation —
+// error draw, counters, fixed latency — in one instruction).  pc 0 invokes
+// the entry (the client request), pc 1 halts.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/isim.h"
+#include "graph.h"
+#include "kernel_abi.h"
+
+namespace isim {
+
+
+
+struct Program {
+  std::vector<Ins> code;
+  int32_t entry = -1;
+  int32_t n_services = 0, n_sites = 0, n_slots = 0;
+  int32_t max_depth = 0;   // deepest call chain from the entry (entry = 1)
+  int32_t max_frames = 0;  // CALL frames the kernel stack needs (client frame included)
+  bool static_walk = false;
+  int32_t time_bits = 64;
+  uint64_t max_latency = 0, hops_upper = 0;
+  std::vector<int32_t> slot_site, slot_callee;  // per slot
+  std::vector<int32_t> site_slot;               // per site (-1: unreachable)
+  std::vector<int32_t> site_callee;             // per site
+};
+
+// Returns an isim_status; on error `err` holds the message.
+int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, Program &out,
+                    std::string &err);
+
+// First service with the name, -1 if absent (extractService, srv/graph.go:97-109).
+int32_t service_index(const ServiceGraph &g, const std::string &name);
+
+}  // namespace isim

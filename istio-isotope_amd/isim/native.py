@@ -1,0 +1,113 @@
+"""ctypes binding of libisim.so (include/isim.h).
+
+The library is built in-tree (``istio-isotope_amd/isim/libisim.so``) by
+``__graft_entry__.build()``.  There is no fallback: if the library is missing
+or fails to load, every entry point raises.
+
+torch is imported (when available) BEFORE the library is loaded: torch ships
+its own ``libamdhip64.so`` (SONAME ``libamdhip64.so.7``); loading it first
+makes libisim's ``libamdhip64.so.7`` dependency resolve to the same runtime
+instead of a second copy from /opt/rocm.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libisim.so")
+
+# isim_status
+OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = range(10)
+STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
+                6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
+MODE_A, MODE_B = 0, 1
+
+# stats layout (isim.h)
+ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
+ST_NOT_MIN_LATENCY, ST_MAX_LATENCY = 5, 6
+N_PROM, N_LOG2 = 33, 64
+ST_PROM = 8
+ST_LOG2 = ST_PROM + 2 * N_PROM
+ST_SITES = ST_LOG2 + 2 * N_LOG2
+
+
+class IsimError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        self.code = code
+        self.status = STATUS_NAMES.get(code, str(code))
+        super().__init__(f"{self.status}: {msg}")
+
+
+class Params(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("hop_base_ns", C.c_uint64),
+                ("req_ps_per_byte", C.c_uint64), ("resp_ps_per_byte", C.c_uint64),
+                ("error_mode", C.c_uint32), ("max_depth", C.c_uint32)]
+
+
+class TraceRec(C.Structure):
+    _fields_ = [("latency_ns", C.c_uint64), ("hops", C.c_uint32), ("status_err", C.c_uint32)]
+
+
+class HandlerInfo(C.Structure):
+    _fields_ = [("n_services", C.c_int32), ("n_sites", C.c_int32), ("n_slots", C.c_int32),
+                ("entry", C.c_int32), ("max_depth", C.c_int32), ("static_walk", C.c_int32),
+                ("time_bits", C.c_int32), ("program_len", C.c_int32),
+                ("max_latency_ns", C.c_uint64), ("hops_upper", C.c_uint64),
+                ("stats_words", C.c_uint64)]
+
+
+# every function declared in include/isim.h: name -> (restype, argtypes)
+_VP = C.c_void_p
+SIGNATURES = {
+    "isim_last_error": (C.c_char_p, []),
+    "isim_abi_version": (C.c_int, []),
+    "isim_graph_unmarshal_json": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_VP)]),
+    "isim_graph_free": (None, [_VP]),
+    "isim_graph_num_services": (C.c_int, [_VP]),
+    "isim_graph_canonical_json": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "isim_graph_service_index": (C.c_int, [_VP, C.c_char_p]),
+    "isim_size_from_string": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
+    "isim_duration_parse": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    "isim_percentage_from_string": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
+    "isim_handler_create": (C.c_int, [_VP, C.c_char_p, C.POINTER(Params), C.POINTER(_VP)]),
+    "isim_handler_free": (None, [_VP]),
+    "isim_handler_info_get": (C.c_int, [_VP, C.POINTER(HandlerInfo)]),
+    "isim_handler_slots": (C.c_int, [_VP, _VP, _VP]),
+    "isim_serve_device": (C.c_int, [_VP, C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
+    "isim_serve": (C.c_int, [_VP, C.c_int, C.c_uint64, C.c_uint64, _VP, _VP]),
+    "isim_stats_fold": (C.c_int, [_VP, _VP, _VP, _VP, _VP]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libisim.so (raises if absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (see module docstring)
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libisim.so not built: {LIB_PATH} (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.isim_abi_version() != 1:
+        raise ImportError("libisim ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().isim_last_error().decode("utf-8", "replace")
+
+
+def check(rc: int) -> None:
+    if rc != OK:
+        raise IsimError(rc, last_error())

@@ -1,0 +1,118 @@
+"""GPU parity: the HIP walk kernel (through the C ABI) against the CPU oracle,
+bit-exact per-trace records and stats, on seeded inputs."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+import isim
+from isim.generators import config2_topology, config3_topology, mesh_topology, realistic_topology, tree_topology
+from isim.yamljson import obj_to_json, yaml_to_json
+
+from conftest import TOPOLOGIES
+from parity import Case, with_defaults
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = sorted(glob.glob(os.path.join(TOPOLOGIES, "*.yaml")))
+
+
+def _fixture_json(path, error_rate=None):
+    j = yaml_to_json(open(path, "rb").read())
+    if error_rate is not None:
+        j = with_defaults(j, errorRate=error_rate)
+    return j
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_reference_topologies(gpu, path, mode):
+    c = Case(_fixture_json(path, error_rate=0.05), None, isim.SimParams(error_mode=mode))
+    c.compare(0, 3000)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4097])
+def test_ragged_batches(gpu, n):
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3))
+    c.compare(777, n)
+
+
+def test_zero_traces(gpu):
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3))
+    recs, stats = c.gpu(0, 0)
+    assert stats.sum() == 0
+
+
+def test_trace_ids_cross_2_32(gpu):
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3))
+    c.compare((1 << 32) - 1000, 2000)
+
+
+def test_error_always_and_never(gpu):
+    j = json.dumps({"services": [
+        {"name": "e", "isEntrypoint": True, "script": [{"call": "a"}, [{"call": "b"}, {"call": "a"}]]},
+        {"name": "a", "errorRate": 1.0},
+        {"name": "b", "errorRate": "0%", "script": [{"call": "a"}, {"sleep": "1ms"}]}]})
+    for mode in (isim.MODE_A, isim.MODE_B):
+        Case(j, None, isim.SimParams(error_mode=mode)).compare(0, 500)
+
+
+def test_probability_and_mode_b_abort(gpu):
+    # sequential calls after fallible calls: mode B aborts change the walk per lane
+    j = json.dumps({"defaults": {"errorRate": 0.2, "requestSize": "1 KB", "responseSize": 300},
+                    "services": [
+        {"name": "e", "isEntrypoint": True, "script": [
+            {"call": {"service": "a", "probability": 50}}, {"sleep": "3ms"},
+            [{"call": "b"}, {"call": {"service": "c", "probability": 70}}, {"sleep": "2ms"}],
+            {"call": "d"}, {"sleep": "1ms"}]},
+        {"name": "a", "script": [{"call": {"service": "c", "probability": 20}}, {"call": "d"}]},
+        {"name": "b", "script": [{"sleep": "500us"}, {"call": "d"}, {"call": "c"}]},
+        {"name": "c", "script": [{"call": {"service": "d", "probability": 99}}, {"sleep": "1.5ms"}]},
+        {"name": "d", "script": [{"sleep": "250us"}]}]})
+    for mode in (isim.MODE_A, isim.MODE_B):
+        c = Case(j, None, isim.SimParams(error_mode=mode, seed=99))
+        assert not c.handler.info.static_walk
+        c.compare(5, 20000)
+
+
+def test_large_latency_u64(gpu):
+    # latency bound above 2^32 ns forces the 64-bit per-lane time kernel
+    j = json.dumps({"services": [
+        {"name": "e", "isEntrypoint": True, "errorRate": 0.5,
+         "script": [{"sleep": "3s"}, {"call": {"service": "a", "probability": 40}}, {"sleep": "2h"}]},
+        {"name": "a", "errorRate": 0.5, "script": [{"sleep": "1h"}, {"call": "b"}]},
+        {"name": "b", "script": [{"sleep": "-5s"}, {"sleep": "100ns"}]}]})
+    c = Case(j)
+    assert c.handler.info.time_bits == 64
+    c.compare(0, 5000)
+
+
+def test_tree_sequential_config2(gpu):
+    j = obj_to_json(config2_topology())
+    c = Case(with_defaults(j, errorRate=0.01))
+    c.compare(0, 2048)
+
+
+def test_realistic_config3(gpu):
+    j = obj_to_json(config3_topology())
+    for mode in (isim.MODE_A, isim.MODE_B):
+        Case(j, None, isim.SimParams(error_mode=mode)).compare(1 << 20, 1024)
+
+
+def test_realistic_sequential_probability(gpu):
+    d = realistic_topology(2000, "multitier", seed=3, concurrent=False, sleep_ms=(1, 5), error_rate=(0, 0.05))
+    for i, s in enumerate(d["services"]):
+        if i % 3 == 0:
+            s["script"] = [({"call": {"service": c["call"], "probability": 60}} if isinstance(c, dict) and "call" in c else c)
+                           for c in s["script"]]
+    j = obj_to_json(d)
+    for mode in (isim.MODE_A, isim.MODE_B):
+        Case(j, None, isim.SimParams(error_mode=mode)).compare(0, 2000)
+
+
+def test_mesh_config4(gpu):
+    j = obj_to_json(mesh_topology(n_services=8000, layers=8, fanout=3, probability=30, seed=11))
+    c = Case(with_defaults(j, errorRate=0.02))
+    c.compare(0, 20000)
