@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: simulated isotope request traces per second (node), 10k-service
+realistic topology (BASELINE.json config 3), MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one launch of the walk kernel (isim_serve_device) over a batch of
+`--batch` traces per rank, trace ids sharded globally (rank r, step s owns
+[(s*N + r)*B, (s*N + r + 1)*B)), per-trace 16-byte records written to HBM,
+per-site counters and latency histograms accumulated on device.  Weak
+scaling: per-GPU work is fixed.  After the K timed steps the per-rank stats
+buffers are merged with one RCCL all-reduce (SUM) plus a 2-word MAX for the
+latency extrema, inside the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` (dominant kernel = isim_walk, algorithmic bytes per launch =
+16 B/trace records + program + stats, live HIP-event timing on the launch
+stream) and `cpu_baseline` (the C oracle, OpenMP, bounded sample, rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "istio-isotope_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_CU = 256
+CLOCK_HZ = 2.4e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--mode", default="A", choices=["A", "B"])
+    ap.add_argument("--no-records", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-traces", type=int, default=0, help="cpu_baseline sample size (0 = auto)")
+    return ap.parse_args()
+
+
+def build_graph(config: str):
+    from isim.generators import config2_topology, config3_topology, mesh_topology
+    from isim.yamljson import obj_to_json
+    if config == "c2":
+        j = obj_to_json(config2_topology())
+        desc = {"workload": "create_tree_topology.py tree depth 4 x fan-out 8, sequential requests (585 services)",
+                "services": 585}
+    elif config == "c4":
+        j = obj_to_json(mesh_topology())
+        desc = {"workload": "100k-service 8-layer mesh, fan-out 3 at probability 30, numReplicas + responseSize",
+                "services": 100000}
+    else:
+        j = obj_to_json(config3_topology())
+        desc = {"workload": "create_realistic_topology.py multitier Barabasi 10k services, concurrent fan-out, "
+                            "sleep U{1..5}ms, errorRate U[0,1%] (restated generator, seed 42)",
+                "services": 10000}
+    return j, desc
+
+
+def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
+    """The C oracle (kind "port": no Go toolchain exists to run the reference)."""
+    from oracle import executor as oc
+    from oracle import graph_ref as gr
+    from oracle.executor_py import SimGraph
+    from oracle.executor_py import SimParams as OParams
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    sg = SimGraph(gr.unmarshal_service_graph(json_text))
+    op = OParams(params.seed, params.hop_base_ns, params.req_ps_per_byte, params.resp_ps_per_byte,
+                 params.error_mode)
+    og = oc.OracleGraph(sg, op)
+    if n_traces <= 0:
+        n_traces = 32768 * threads
+    t0 = time.perf_counter()
+    _, st = oc.run(sg, op, sg.entry(), trace_begin, n_traces, records=False, n_threads=threads, og=og)
+    dt = time.perf_counter() - t0
+    return {"value": n_traces / dt, "unit": "traces/s", "cores": threads, "kind": "port",
+            "sample": f"{n_traces} traces of the same workload (trace ids from {trace_begin}), "
+                      f"C oracle oracle/isim_oracle.c with OpenMP, {dt:.1f} s",
+            "hop_visits_per_s": float(st[2]) / dt}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import isim
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    json_text, desc = build_graph(args.config)
+    params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A)
+    h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
+    info = h.info
+    launch = h.launch_info(torch.cuda.current_device())
+    B = args.batch
+    stats = torch.zeros(info.stats_words, dtype=torch.int64, device=dev)
+    recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step(s):
+        begin = (s * world + rank) * B
+        h.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), sptr)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    stats.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step(args.warmup + i)
+        ev[i][1].record(stream)
+    if world > 1:
+        # one all-reduce of the counters/histograms; extrema words merge with MAX
+        ext = stats[isim.native.ST_NOT_MIN_LATENCY:isim.native.ST_MAX_LATENCY + 1].clone()
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        dist.all_reduce(ext, op=dist.ReduceOp.MAX)
+        stats[isim.native.ST_NOT_MIN_LATENCY:isim.native.ST_MAX_LATENCY + 1] = ext
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    host_stats = stats.cpu().numpy().view(np.uint64)
+    folded = h.fold(host_stats)
+    total = args.steps * B * world
+    assert folded["n_traces"] == total, (folded["n_traces"], total)
+    value = total / elapsed
+    hops_per_trace = folded["sum_hops"] / total
+
+    # algorithmic bytes of one launch: 16 B records per trace + program read + stats written
+    alg_bytes = B * (0 if args.no_records else 16) + info.program_len * 32 + info.stats_words * 8
+    achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("config") == args.config and pmc.get("batch") == B:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    line = {
+        "metric": "simulated request traces/sec (node), 10k-svc topology" if args.config == "c3"
+        else f"simulated request traces/sec (node), config {args.config}",
+        "value": value,
+        "unit": "traces/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": dict(desc, global_batch=B * world, traces_per_rank_per_step=B,
+                       error_mode=args.mode, hop_visits_per_trace=hops_per_trace,
+                       parallelism=f"trace-shard x{world}", records=not args.no_records,
+                       static_walk=bool(info.static_walk), program_len=info.program_len,
+                       launch=launch),
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+        "hop_visits_per_s": value * hops_per_trace,
+        "n_500_frac": folded["n_500"] / total,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(json_text, params, args.cpu_traces, 0)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,7 +78,12 @@ typedef struct {
   uint64_t resp_ps_per_byte;
   uint32_t error_mode;       /* ISIM_MODE_A / ISIM_MODE_B */
   uint32_t max_depth;        /* 0 = 64; at most 64 */
+  uint32_t flags;            /* ISIM_FLAG_* */
+  uint32_t reserved;         /* must be 0 */
 } isim_params;
+
+/* isim_params.flags */
+#define ISIM_FLAG_NO_STREAM 1u /* run static walks on the interpreter kernel instead of the draw stream */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -117,6 +122,16 @@ typedef struct {
   uint64_t stats_words;      /* u64 words of the stats buffer */
 } isim_handler_info;
 
+/* Launch configuration chosen for a device (filled on first use of that device). */
+typedef struct {
+  int32_t wg_threads;        /* workgroup size (multiple of 64) */
+  int32_t lds_bytes;         /* dynamic LDS per workgroup */
+  int32_t lds_counters;      /* 1: per-site counters in LDS; 0: global atomics */
+  int32_t blocks_per_cu;     /* resident workgroups per CU (occupancy query) */
+  int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
+  int32_t kernel_kind;       /* 0/1 static u32/u64 time, 2/3 dynamic u32/u64 */
+} isim_launch_info;
+
 ISIM_API const char *isim_last_error(void);
 ISIM_API int isim_abi_version(void);
 
@@ -141,6 +156,8 @@ ISIM_API int isim_handler_create(const isim_graph *g, const char *service_name, 
                         isim_handler **out);
 ISIM_API void isim_handler_free(isim_handler *h);
 ISIM_API int isim_handler_info_get(const isim_handler *h, isim_handler_info *out);
+/* Prepares `device` (uploads the program) and reports the launch configuration. */
+ISIM_API int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out);
 /* Map of stats slots to the graph: slot -> call-site id (document order) and
  * callee service index.  Arrays of info.n_slots entries. */
 ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32_t *slot_callee);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -32,12 +33,14 @@ int fail(int code, const std::string &msg) {
   } while (0)
 
 struct DevState {
-  isim::Ins *d_prog = nullptr;
+  void *d_prog = nullptr;  // Ins[] (interpreters) or Node[] (draw stream)
   void *kernel = nullptr;
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
   uint32_t lds_counters = 0;
   uint32_t max_blocks = 0;  // resident workgroups for the whole device
+  uint32_t per_cu = 0;
+  uint32_t kind = 0;
 };
 
 }  // namespace
@@ -89,7 +92,9 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
     return fail(ISIM_ENODEV, std::string("libisim is built for gfx950 only; device is ") + prop.gcnArchName);
   const isim::Program &p = h->prog;
   DevState st;
-  const uint32_t lds_max = (uint32_t)prop.sharedMemPerBlock;  // 160 KiB on gfx950
+  // HIP reports 64 KiB per block by default; a gfx950 workgroup may use all
+  // 160 KiB of the CU's LDS once the kernel attribute is raised.
+  const uint32_t lds_max = (uint32_t)std::max<size_t>(prop.sharedMemPerBlock, prop.maxSharedMemoryPerMultiProcessor);
   // Largest workgroup (waves) whose LDS fits, counters in LDS if possible.
   bool counters = true;
   uint32_t waves = 16;
@@ -104,14 +109,21 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   st.threads = waves * 64u;
   st.lds_bytes = lds_need(p, waves, counters);
   st.lds_counters = counters ? 1u : 0u;
-  st.kernel = isim::walk_kernel(p.static_walk, h->params.error_mode == ISIM_MODE_B, p.time_bits == 64);
+  st.kind = p.stream_nodes ? 4u : (p.static_walk ? 0u : 2u) + (p.time_bits == 64 ? 1u : 0u);
+  if ((h->params.flags & ISIM_FLAG_NO_STREAM) && st.kind == 4) st.kind = p.time_bits == 64 ? 1u : 0u;
+  st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B);
+  HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)st.lds_bytes));
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)st.kernel, (int)st.threads,
                                                       st.lds_bytes));
   if (per_cu < 1) return fail(ISIM_EHIP, "walk kernel cannot be resident (occupancy 0)");
+  st.per_cu = (uint32_t)per_cu;
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-  HIPCHK(hipMalloc(&st.d_prog, p.code.size() * sizeof(isim::Ins)));
-  HIPCHK(hipMemcpy(st.d_prog, p.code.data(), p.code.size() * sizeof(isim::Ins), hipMemcpyHostToDevice));
+  const void *src = st.kind == 4 ? (const void *)p.stream.data() : (const void *)p.code.data();
+  const size_t bytes = st.kind == 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
+  HIPCHK(hipMalloc(&st.d_prog, bytes));
+  HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
   auto res = h->dev.emplace(device, st);
   out = &res.first->second;
   return ISIM_OK;
@@ -218,11 +230,29 @@ int isim_handler_info_get(const isim_handler *h, isim_handler_info *out) {
   out->entry = p.entry;
   out->max_depth = p.max_depth;
   out->static_walk = p.static_walk ? 1 : 0;
-  out->time_bits = p.static_walk ? 64 : p.time_bits;
+  out->time_bits = p.time_bits;
   out->program_len = (int32_t)p.code.size();
   out->max_latency_ns = p.max_latency;
   out->hops_upper = p.hops_upper;
   out->stats_words = ISIM_ST_SITES + 2ull * (uint64_t)p.n_slots;
+  return ISIM_OK;
+}
+
+int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out) {
+  if (!h || !out) return fail(ISIM_EINVAL, "null argument");
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  HIPCHK(hipSetDevice(device));
+  DevState *st = nullptr;
+  int rc = prepare_device(h, device, st);
+  (void)hipSetDevice(prev);
+  if (rc != ISIM_OK) return rc;
+  out->wg_threads = (int32_t)st->threads;
+  out->lds_bytes = (int32_t)st->lds_bytes;
+  out->lds_counters = (int32_t)st->lds_counters;
+  out->blocks_per_cu = (int32_t)st->per_cu;
+  out->max_blocks = (int32_t)st->max_blocks;
+  out->kernel_kind = (int32_t)st->kind;
   return ISIM_OK;
 }
 
@@ -244,21 +274,21 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   int rc = prepare_device(h, device, st);
   if (rc != ISIM_OK) return rc;
   isim::KParams kp{};
-  kp.prog = st->d_prog;
   kp.trace_begin = trace_begin;
   kp.n_traces = n_traces;
-  kp.records = d_records;
-  kp.stats = d_stats;
   kp.seed_lo = (uint32_t)h->params.seed;
   kp.seed_hi = (uint32_t)(h->params.seed >> 32);
   kp.n_slots = (uint32_t)h->prog.n_slots;
   kp.max_frames = (uint32_t)h->prog.max_frames;
   kp.lds_counters = st->lds_counters;
+  kp.n_nodes = h->prog.stream_nodes;
+  kp.t_static = h->prog.max_latency;
   const uint64_t batches = (n_traces + 63) / 64;
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);
-  void *args[] = {&kp};
+  const void *prog = st->d_prog;
+  void *args[] = {&prog, &d_records, &d_stats, &kp};
   HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
                          (hipStream_t)hip_stream));
   return ISIM_OK;

@@ -37,17 +37,28 @@ struct Ins {
 };
 static_assert(sizeof(Ins) == 32, "Ins must be 32 bytes");
 
+// STATIC walks also compile to a draw stream: one record per invocation in
+// hop (DFS preorder) order.  meta = slot (bits 0-23) | closes (24-30) | always (31).
+struct Node {
+  uint32_t thr;   // error threshold over the u32 draw (0: never)
+  uint32_t meta;
+};
+static_assert(sizeof(Node) == 8, "Node must be 8 bytes");
+constexpr uint32_t kSlotRoot = 0xFFFFFFu;  // the entry invocation (no call site)
+constexpr uint32_t kSlotPad = 0xFFFFFEu;   // padding to a multiple of 4 records
+constexpr uint32_t kMaxStreamNodes = 1u << 24;
+
+// Scalar kernel arguments (the program, records and stats pointers are
+// separate __restrict__ kernel arguments so program fetches become s_load).
 struct KParams {
-  const Ins *prog;
   uint64_t trace_begin;
   uint64_t n_traces;
-  isim_trace_rec *records;  // may be null
-  uint64_t *stats;
   uint32_t seed_lo, seed_hi;
   uint32_t n_slots;
   uint32_t max_frames;
   uint32_t lds_counters;    // 1: per-site counters in the LDS table
-  uint32_t pad;
+  uint32_t n_nodes;         // stream kernel: invocations per trace
+  uint64_t t_static;        // stream kernel: the (trace-invariant) latency
 };
 
 constexpr uint32_t kWgThreads = 1024;                 // max workgroup size (launch bound)
@@ -55,6 +66,7 @@ constexpr uint32_t kLdsAccBytes = 64;                 // WgAcc
 constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 
 // walk.hip: kernel pointer for a walk variant.
-void *walk_kernel(bool is_static, bool modeb, bool time64);
+// kind: 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream.
+void *walk_kernel(int kind, bool modeb);
 
 }  // namespace isim

@@ -286,6 +286,32 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
   }
   for (Ins &in : code)
     if ((in.opf & 0xFF) == OP_CALL) in.b_lo = (uint32_t)body_pc[in.b_lo];
+
+  // ---- draw stream of a static walk: the unrolled invocation tree in hop order
+  if (out.static_walk && hops[entry] <= kMaxStreamNodes) {
+    auto rec = [&](int32_t callee, uint32_t slot) {
+      Node nd;
+      nd.thr = thr[callee] >= (1ull << 32) ? 0u : (uint32_t)thr[callee];
+      nd.meta = (slot & 0xFFFFFFu) | (thr[callee] >= (1ull << 32) ? 0x80000000u : 0u);
+      out.stream.push_back(nd);
+    };
+    std::vector<std::pair<int32_t, size_t>> stack;
+    rec(entry, kSlotRoot);
+    stack.push_back({entry, 0});
+    while (!stack.empty()) {
+      auto &top = stack.back();
+      if (top.second < svc_sites[top.first].size()) {
+        const int32_t sid = svc_sites[top.first][top.second++];
+        rec(sites[sid].callee, (uint32_t)out.site_slot[sid]);
+        stack.push_back({sites[sid].callee, 0});
+      } else {
+        stack.pop_back();
+        out.stream.back().meta += 1u << 24;  // the subtree ending here closes after this record
+      }
+    }
+    out.stream_nodes = (uint32_t)out.stream.size();
+    while (out.stream.size() % 4) out.stream.push_back(Node{0u, kSlotPad});
+  }
   if (code.size() >= (1u << 30)) {
     err = "program too large";
     return ISIM_EINVAL;

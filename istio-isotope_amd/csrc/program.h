@@ -31,6 +31,9 @@ struct Program {
   std::vector<int32_t> slot_site, slot_callee;  // per slot
   std::vector<int32_t> site_slot;               // per site (-1: unreachable)
   std::vector<int32_t> site_callee;             // per site
+  // draw stream (static walks whose unrolled invocation tree is <= kMaxStreamNodes)
+  std::vector<Node> stream;                     // padded to a multiple of 4
+  uint32_t stream_nodes = 0;                    // invocations per trace (unpadded)
 };
 
 // Returns an isim_status; on error `err` holds the message.

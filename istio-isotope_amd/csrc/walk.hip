@@ -6,48 +6,65 @@
 // integer-nanosecond time.
 //
 // Execution model:
-//  * The program counter, the current instruction (one s_load_dwordx8) and the
-//    call depth are wave-uniform (SGPRs).  Per-lane booleans — "this lane's
-//    trace executes the current invocation", "a step failed", "error in the
-//    current concurrent step", "this invocation's own error draw" — are 64-bit
-//    lane masks held in SGPRs and combined with scalar ALU ops.
+//  * The program counter, the current instruction and the call depth are
+//    wave-uniform (SGPRs).  The next instruction is known before the current
+//    one executes (pc+1, a CALL's target, or the return pc of a RET), so the
+//    loop issues one s_load_dwordx16 of [npc-1, npc] first and consumes it on
+//    the next iteration; for a RET the first half is the CALL record.
+//  * Per-lane booleans — "this lane's trace executes the current invocation",
+//    "a step failed", "error in the current concurrent step", "this
+//    invocation's own error draw" — are 64-bit lane masks in SGPRs.
 //  * STATIC walks (no probabilistic calls, no mode-B abort that could skip a
-//    step) execute the identical invocation sequence in every lane, so
-//    virtual time and hop ids are wave-uniform: they live in SGPRs, and the
-//    only per-lane work is the Philox error draw, the status masks and the
-//    per-trace error count.  Other walks keep time (u32 or u64, chosen from
-//    the program's static latency bound) and hop ids per lane.
-//  * Call frames: uniform parts (return pc, masks, uniform time) are stored
-//    in VGPR lanes (lane d holds frame d: v_writelane / v_readlane); per-lane
-//    time and hop of dynamic walks go to an LDS stack [frame][lane].
-//  * Error draws: word (h&3) of Philox4x32-10((t, h>>2, 0), seed), so one
-//    block serves four consecutive invocations of a lane.
-//  * Per-call-site counters (executed calls, callee 500s) are wave-reduced to
-//    one ds_add per instruction into a workgroup LDS table and flushed to HBM
-//    with global atomics once per workgroup; latency histograms are reduced
-//    per batch with a wave "match" loop.
+//    step) execute the identical invocation sequence in every lane, so virtual
+//    time and hop ids are wave-uniform (SGPRs); the per-lane work is the
+//    Philox error draws, the status masks and the per-trace error count.
+//    Other walks keep time (u32 or u64 by the program's latency bound) and
+//    hop ids per lane.
+//  * Call frames: wave-uniform parts live in VGPR lanes (lane d holds frame
+//    d: v_writelane / v_readlane); per-lane time and hop of dynamic walks go
+//    to an LDS stack [frame][lane].
+//  * Error draws: word (h&3) of Philox4x32-10((t_lo, t_hi, h>>2, 0), seed):
+//    one block serves four consecutive invocations of a lane.
+//  * Per-call-site counters (executed calls, callee 500s) are one ds_add per
+//    instruction per wave into a workgroup LDS table, flushed to HBM with
+//    global atomics once per workgroup; latency histograms are reduced per
+//    64-trace batch with a wave "match" loop.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "kernel_abi.h"
 
 namespace isim {
 namespace dev {
 
+constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
 constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 
-__device__ __forceinline__ void philox10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
-                                         uint32_t k0, uint32_t k1) {
+struct Ins2 {
+  Ins a, b;
+};
+
+__device__ __forceinline__ void round1(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t k0,
+                                       uint32_t k1) {
+  const uint64_t p0 = (uint64_t)M0 * c0;
+  const uint64_t p1 = (uint64_t)M1 * c2;
+  const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+  const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+  c0 = n0;
+  c1 = (uint32_t)p1;
+  c2 = n2;
+  c3 = (uint32_t)p0;
+}
+
+// Philox4x32-10, generic (all counter words per lane).
+__device__ __forceinline__ void philox10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t k0,
+                                         uint32_t k1) {
+  asm volatile("" : "+s"(k0), "+s"(k1));  // do not hoist the key schedule into 20 SGPRs
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    c0 = n0;
-    c1 = (uint32_t)p1;
-    c2 = n2;
-    c3 = (uint32_t)p0;
+    round1(c0, c1, c2, c3, k0, k1);
     k0 += W0;
     k1 += W1;
   }
@@ -62,64 +79,63 @@ __device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__builti
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 // v_writelane_b32: no clang builtin on this toolchain, so bind the LLVM
 // intrinsic directly (value and lane index are wave-uniform).
 __device__ int llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t wrl(uint32_t v, uint32_t l, uint32_t old) {
   return (uint32_t)llvm_writelane((int)v, (int)l, (int)old);
 }
-__device__ __forceinline__ uint32_t uni(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
 
-// A 64-bit wave-uniform value kept in two VGPR-lane stacks.
-struct U64Stack {
+// A wave-uniform value kept in VGPR lanes (lane d = frame d).
+template <typename T>
+struct LaneStack;
+template <>
+struct LaneStack<uint32_t> {
+  uint32_t v = 0;
+  __device__ __forceinline__ void put(uint32_t d, uint32_t x) { v = wrl(x, d, v); }
+  __device__ __forceinline__ uint32_t get(uint32_t d) const { return rdl(v, d); }
+};
+template <>
+struct LaneStack<uint64_t> {
   uint32_t lo = 0, hi = 0;
-  __device__ __forceinline__ void put(uint32_t d, uint64_t v) {
-    lo = wrl((uint32_t)v, d, lo);
-    hi = wrl((uint32_t)(v >> 32), d, hi);
+  __device__ __forceinline__ void put(uint32_t d, uint64_t x) {
+    lo = wrl((uint32_t)x, d, lo);
+    hi = wrl((uint32_t)(x >> 32), d, hi);
   }
-  __device__ __forceinline__ uint64_t get(uint32_t d) const {
-    return (uint64_t)rdl(lo, d) | ((uint64_t)rdl(hi, d) << 32);
-  }
+  __device__ __forceinline__ uint64_t get(uint32_t d) const { return u64of(rdl(lo, d), rdl(hi, d)); }
 };
 
-// LDS counter add of a wave-uniform amount by one lane.
-__device__ __forceinline__ void lds_add(uint32_t *p, uint32_t v) {
-  if (lane_id() == 0) atomicAdd(p, v);
-}
-
-__device__ __forceinline__ void count(const KParams &kp, uint32_t *cnt, uint32_t idx, uint32_t v) {
+// Per-site counter add of a wave-uniform amount by one lane (LDS table, or
+// global atomics when the table does not fit).
+__device__ __forceinline__ void count(uint64_t *__restrict__ gstats, uint32_t *cnt, uint32_t idx, uint32_t v) {
   if (v == 0) return;
-  if (cnt) {
-    lds_add(cnt + idx, v);
-  } else if (lane_id() == 0) {
-    atomicAdd((unsigned long long *)(kp.stats + ISIM_ST_SITES + idx), (unsigned long long)v);
+  if (lane_id() == 0) {
+    if (cnt) atomicAdd(cnt + idx, v);
+    else atomicAdd((unsigned long long *)(gstats + ISIM_ST_SITES + idx), (unsigned long long)v);
   }
 }
 
-__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) {
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
+// service_request_duration_seconds buckets (srv/prometheus/handler.go:26-31):
+// bucket = first i with t <= edge_i ms  <=>  ceil(t / 1ms) <= edge_i.
 __device__ __forceinline__ uint32_t prom_bucket(uint64_t t) {
-  const uint64_t ms = 1000000ull;
-  // service_request_duration_seconds buckets, srv/prometheus/handler.go:26-31
+  if (t > 500000000ull) return 32;
+  const uint32_t c = (uint32_t)((t + 999999ull) / 1000000ull);  // <= 500
   const uint32_t e[32] = {7, 8, 9, 10, 11, 12, 14, 16, 18, 20, 25, 30, 35, 40, 45, 50,
                           60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
-  uint32_t b = 32;
+  uint32_t b = 0;
 #pragma unroll
-  for (int i = 31; i >= 0; --i)
-    if (t <= (uint64_t)e[i] * ms) b = (uint32_t)i;
+  for (int i = 0; i < 32; ++i) b += e[i] < c ? 1u : 0u;
   return b;
 }
 
 // Wave-aggregated LDS histogram add: one ds_add per distinct key.
 __device__ __forceinline__ void hist_add(uint32_t *h, uint32_t key, uint64_t lanes) {
   while (lanes) {
-    uint32_t leader = (uint32_t)__builtin_ctzll(lanes);
-    uint32_t k = rdl(key, leader);
-    uint64_t m = ballot(key == k) & lanes;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(lanes);
+    const uint32_t k = rdl(key, leader);
+    const uint64_t m = ballot(key == k) & lanes;
     if (lane_id() == leader) atomicAdd(h + k, popc(m));
     lanes &= ~m;
   }
@@ -133,7 +149,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
-    uint64_t w = __shfl_xor(v, o, 64);
+    const uint64_t w = __shfl_xor(v, o, 64);
     v = w > v ? w : v;
   }
   return v;
@@ -144,193 +160,339 @@ struct WgAcc {
   unsigned long long sum_latency, sum_hops, sum_err, n500, ntr, notmin, max;
 };
 
-template <bool STATIC, bool MODEB, typename TT>
-__device__ __forceinline__ void walk_batch(const KParams &kp, uint64_t base, uint32_t *cnt,
-                                           uint32_t *hist, WgAcc *acc_lds, TT *lstk,
-                                           uint32_t *hstk) {
+struct Ctx {
+  const Ins *__restrict__ prog;
+  isim_trace_rec *__restrict__ records;
+  uint64_t *__restrict__ gstats;
+  uint32_t *cnt;   // LDS per-site counters or null
+  uint32_t *hist;  // LDS histograms
+  WgAcc *acc;      // LDS accumulators
+  uint32_t n_slots;
+  uint32_t k0, k1;
+};
+
+// Per-batch epilogue: record, histograms, sums.
+__device__ __forceinline__ void finish_batch(const Ctx &c, uint64_t idx, bool valid, uint64_t all, uint64_t lat,
+                                             uint32_t hops, uint64_t root_st, uint32_t errh) {
+  const bool is500 = lane_in(root_st);
+  if (c.records != nullptr && valid) {
+    uint4 r;
+    r.x = (uint32_t)lat;
+    r.y = (uint32_t)(lat >> 32);
+    r.z = hops;
+    r.w = (is500 ? 0x80000000u : 0u) | errh;
+    *reinterpret_cast<uint4 *>(c.records + idx) = r;
+  }
+  hist_add(c.hist, (is500 ? ISIM_N_PROM : 0u) + prom_bucket(lat), all);
+  const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
+  hist_add(c.hist + 2 * ISIM_N_PROM, (is500 ? ISIM_N_LOG2 : 0u) + l2, all);
+  const uint64_t s_lat = wave_sum64(valid ? lat : 0);
+  const uint64_t s_hops = wave_sum64(valid ? (uint64_t)hops : 0);
+  const uint64_t s_err = wave_sum64(valid ? (uint64_t)errh : 0);
+  const uint64_t mx = wave_max64(valid ? lat : 0);
+  const uint64_t nmn = wave_max64(valid ? ~lat : 0);
+  if (lane_id() == 0) {
+    atomicAdd(&c.acc->sum_latency, (unsigned long long)s_lat);
+    atomicAdd(&c.acc->sum_hops, (unsigned long long)s_hops);
+    atomicAdd(&c.acc->sum_err, (unsigned long long)s_err);
+    atomicAdd(&c.acc->n500, (unsigned long long)popc(root_st & all));
+    atomicAdd(&c.acc->ntr, (unsigned long long)popc(all));
+    atomicMax(&c.acc->max, (unsigned long long)mx);
+    atomicMax(&c.acc->notmin, (unsigned long long)nmn);
+  }
+}
+
+// ======================================================================
+// STATIC walk: uniform time (UT = u32 when the latency bound fits) and hops.
+// ======================================================================
+template <bool MODEB, typename UT>
+__device__ __forceinline__ void walk_static(const Ctx &c, uint64_t trace_begin, uint64_t n_traces,
+                                            uint64_t base) {
   const uint32_t lane = lane_id();
   const uint64_t idx = base + lane;
-  const bool valid = idx < kp.n_traces;
-  const uint64_t t = kp.trace_begin + idx;
+  const bool valid = idx < n_traces;
+  const uint64_t t = trace_begin + idx;
   const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32);
+  const uint32_t t_hi_u = rfl(t_hi);
+  const bool hi_uniform = ballot(t_hi != t_hi_u) == 0;  // the batch does not straddle 2^32
   const uint64_t all = ballot(valid);
-  const uint32_t k0 = kp.seed_lo, k1 = kp.seed_hi;
-  const Ins *__restrict__ prog = kp.prog;
+  const Ins *__restrict__ prog = c.prog;
 
-  // ---- wave-uniform state
-  uint32_t pc = 0, depth = 0;
-  uint64_t live = all, failed = 0, cerr = 0, own = 0, root_st = 0;
-  // STATIC: uniform time and hop counter
-  uint64_t uacc = 0, ucmax = 0;
-  uint32_t uhop = 0, ublk = 0xFFFFFFFFu;
-  // ---- per-lane state
-  TT acc = 0, cmax = 0;           // dynamic walks
-  uint32_t myhop = 0, hopn = 0;   // dynamic walks
-  uint32_t cblk = 0xFFFFFFFFu;    // dynamic walks: cached Philox block
-  uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
-  uint32_t errh = 0;
-  // ---- frame stacks in VGPR lanes
-  uint32_t f_ret = 0;
-  U64Stack f_live, f_failed, f_cerr, f_own, f_acc, f_cmax;
+  UT acc = 0, cmax = 0;
+  uint64_t own = 0, failed = 0, cerr = 0, root_st = 0;
+  uint32_t hop = 0, have = 0xFFFFFFFFu, depth = 0, pc = 0;
+  uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, errh = 0;
+  LaneStack<uint32_t> f_ret;
+  LaneStack<uint64_t> f_own, f_cerr;
+  LaneStack<UT> f_acc, f_cmax;
 
-  // error draw for the lanes in `e` invoking a callee with flags/thr
-  auto draw_err = [&](uint32_t flags, uint32_t thr, uint64_t e) -> uint64_t {
-    if (flags & F_ERR_ALWAYS) return e;
-    if (!(flags & F_ERR_DRAW)) return 0;
-    bool hit;
-    if constexpr (STATIC) {
-      const uint32_t blk = uhop >> 2;
-      if (blk != ublk) {  // uniform branch
-        x0 = t_lo; x1 = t_hi; x2 = blk; x3 = 0;
-        philox10(x0, x1, x2, x3, k0, k1);
-        ublk = blk;
-      }
-      const uint32_t w = uhop & 3;
-      uint32_t word;
-      if (w == 0) word = x0;
-      else if (w == 1) word = x1;
-      else if (w == 2) word = x2;
-      else word = x3;
-      hit = word < thr;
-    } else {
-      const uint32_t blk = hopn >> 2;
-      const uint64_t need = ballot(blk != cblk) & e;
-      if (need) {
-        if (lane_in(need)) {
-          uint32_t a = t_lo, b = t_hi, c = blk, d = 0;
-          philox10(a, b, c, d, k0, k1);
-          x0 = a; x1 = b; x2 = c; x3 = d;
-          cblk = blk;
-        }
-      }
-      const uint32_t w = hopn & 3;
-      const uint32_t lo = (w & 1) ? x1 : x0;
-      const uint32_t hi = (w & 1) ? x3 : x2;
-      hit = ((w & 2) ? hi : lo) < thr;
-    }
-    return ballot(hit) & e;
-  };
-
-  // probability skip draw (dynamic walks only): lanes of `a` that skip
-  auto draw_skip = [&](uint32_t k, uint32_t q, uint64_t a) -> uint64_t {
-    bool skip = false;
-    if (lane_in(a)) {
-      uint32_t c0 = t_lo, c1 = t_hi, c2 = myhop, c3 = 1u + (k >> 2);
-      philox10(c0, c1, c2, c3, k0, k1);
-      const uint32_t sel = k & 3;  // uniform
-      const uint32_t word = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
-      skip = (word % 100u) < 100u - q;
-    }
-    return ballot(skip) & a;
-  };
-
-  // fold a finished invocation (duration H + T per lane, status st) into
-  // the caller frame for lanes `e`
-  auto fold = [&](uint32_t flags, uint64_t H, TT T, uint64_t uT, uint64_t e, uint64_t st) {
+  auto fold = [&](uint32_t flags, UT v, uint64_t st) {
     if (flags & F_ROOT) {
       root_st = st;
-      if constexpr (STATIC) uacc = H + uT;
-      else if (lane_in(e)) acc = (TT)H + T;
+      acc = v;
     } else if (flags & F_CONC) {
-      if constexpr (STATIC) {
-        const uint64_t v = H + uT;
-        ucmax = v > ucmax ? v : ucmax;
-      } else if (lane_in(e)) {
+      cmax = v > cmax ? v : cmax;
+      if constexpr (MODEB) cerr |= st;
+    } else {
+      acc += v;
+      if constexpr (MODEB) failed |= st;
+    }
+  };
+
+  Ins cur = prog[0];
+  while (true) {
+    const uint32_t op = cur.opf & 0xFFu;
+    if (op == OP_HALT) break;
+    const uint32_t flags = (cur.opf >> 8) & 0xFFu;
+    uint32_t npc = pc + 1;
+    if (op == OP_CALL) npc = cur.b_lo;
+    if (op == OP_RET) npc = f_ret.get(depth - 1);
+    const Ins2 pre = *reinterpret_cast<const Ins2 *>(prog + (npc - 1));  // [npc-1, npc]
+    switch (op) {
+      case OP_SLEEP:
+        acc += (UT)u64of(cur.a_lo, cur.a_hi);
+        break;
+      case OP_CBEGIN:
+        cmax = 0;
+        cerr = 0;
+        break;
+      case OP_CSLEEP: {
+        const UT d = (UT)u64of(cur.a_lo, cur.a_hi);
+        cmax = d > cmax ? d : cmax;
+        break;
+      }
+      case OP_CEND:
+        acc += cmax;
+        if constexpr (MODEB) failed |= cerr;
+        break;
+      case OP_LEAF:
+      case OP_CALL: {
+        uint64_t st = 0;
+        if (flags & F_ERR_ALWAYS) {
+          st = all;
+        } else if (flags & F_ERR_DRAW) {
+          const uint32_t blk = hop >> 2;
+          if (blk != have) {
+            have = blk;
+            uint32_t a = t_lo, b = t_hi, cc = blk, d = 0;
+            if (hi_uniform) {
+              // rounds 1-2 with the uniform counter words folded into SGPR math
+              // keep the key schedule out of SGPRs between refills (recomputed
+              // with 2 SALU adds per round instead of 20 hoisted registers)
+              uint32_t k0a = c.k0, k1a = c.k1;
+              asm volatile("" : "+s"(k0a), "+s"(k1a));
+              const uint64_t q1 = (uint64_t)M1 * blk;                    // scalar
+              const uint64_t p0 = (uint64_t)M0 * t_lo;                   // per lane
+              const uint32_t u0 = (uint32_t)(q1 >> 32) ^ t_hi_u ^ k0a;   // uniform
+              const uint32_t u1 = (uint32_t)q1;                          // uniform
+              const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;            // per lane
+              const uint32_t v3 = (uint32_t)p0;                          // per lane
+              const uint32_t k0b = k0a + W0, k1b = k1a + W1;
+              const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
+              const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
+              a = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+              b = (uint32_t)p1;
+              cc = (uint32_t)(q0 >> 32) ^ v3 ^ k1b;
+              d = (uint32_t)q0;
+              uint32_t k0 = k0b + W0, k1 = k1b + W1;
+#pragma unroll
+              for (int r = 2; r < 10; ++r) {
+                round1(a, b, cc, d, k0, k1);
+                k0 += W0;
+                k1 += W1;
+              }
+            } else {
+              philox10(a, b, cc, d, c.k0, c.k1);
+            }
+            x0 = a;
+            x1 = b;
+            x2 = cc;
+            x3 = d;
+          }
+          const uint32_t w = hop & 3u;
+          const uint32_t lo = (w & 1u) ? x1 : x0;
+          const uint32_t hi = (w & 1u) ? x3 : x2;
+          st = ballot(((w & 2u) ? hi : lo) < cur.thr) & all;
+        }
+        ++hop;
+        if (!(flags & F_ROOT)) count(c.gstats, c.cnt, cur.slot, popc(all));
+        const UT H = (UT)u64of(cur.a_lo, cur.a_hi);
+        if (op == OP_LEAF) {
+          if (!(flags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cur.slot, popc(st));
+          if (lane_in(st)) ++errh;
+          fold(flags, H + (UT)u64of(cur.b_lo, cur.b_hi), st);
+        } else {
+          f_ret.put(depth, pc + 1);
+          f_own.put(depth, own);
+          f_acc.put(depth, acc);
+          f_cmax.put(depth, cmax);
+          if constexpr (MODEB) f_cerr.put(depth, cerr);
+          ++depth;
+          acc = 0;
+          cmax = 0;
+          cerr = 0;
+          failed = 0;
+          own = st;
+        }
+        break;
+      }
+      case OP_RET: {
+        const uint64_t st = (failed | own) & all;
+        const UT T = acc;
+        --depth;
+        own = f_own.get(depth);
+        acc = f_acc.get(depth);
+        cmax = f_cmax.get(depth);
+        if constexpr (MODEB) cerr = f_cerr.get(depth);
+        failed = 0;  // static walks never call after a failed step
+        const Ins &cin = pre.a;
+        const uint32_t cflags = (cin.opf >> 8) & 0xFFu;
+        if (!(cflags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cin.slot, popc(st));
+        if (lane_in(st)) ++errh;
+        fold(cflags, (UT)u64of(cin.a_lo, cin.a_hi) + T, st);
+        break;
+      }
+      default:
+        __builtin_trap();
+    }
+    cur = pre.b;
+    pc = npc;
+  }
+  finish_batch(c, idx, valid, all, (uint64_t)acc, hop, root_st, errh);
+}
+
+// ======================================================================
+// DYNAMIC walk: per-lane time (TT) and hop ids, LDS frame stack.
+// ======================================================================
+template <bool MODEB, typename TT>
+__device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin, uint64_t n_traces,
+                                             uint64_t base, TT *__restrict__ lstk, uint32_t *__restrict__ hstk) {
+  const uint32_t lane = lane_id();
+  const uint64_t idx = base + lane;
+  const bool valid = idx < n_traces;
+  const uint64_t t = trace_begin + idx;
+  const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32);
+  const uint64_t all = ballot(valid);
+  const Ins *__restrict__ prog = c.prog;
+
+  uint64_t live = all, failed = 0, cerr = 0, own = 0, root_st = 0;
+  uint32_t depth = 0, pc = 0;
+  TT acc = 0, cmax = 0;
+  uint32_t myhop = 0, hopn = 0, cblk = 0xFFFFFFFFu;
+  uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, errh = 0;
+  LaneStack<uint32_t> f_ret;
+  LaneStack<uint64_t> f_live, f_failed, f_cerr, f_own;
+
+  auto fold = [&](uint32_t flags, uint64_t H, TT T, uint64_t e, uint64_t st) {
+    if (flags & F_ROOT) {
+      root_st = st;
+      if (lane_in(e)) acc = (TT)H + T;
+    } else if (flags & F_CONC) {
+      if (lane_in(e)) {
         const TT v = (TT)H + T;
         cmax = v > cmax ? v : cmax;
       }
       if constexpr (MODEB) cerr |= st;
     } else {
-      if constexpr (STATIC) uacc += H + uT;
-      else if (lane_in(e)) acc += (TT)H + T;
+      if (lane_in(e)) acc += (TT)H + T;
       if constexpr (MODEB) failed |= st;
     }
   };
 
+  Ins cur = prog[0];
   while (true) {
-    const Ins in = prog[pc];
-    const uint32_t op = in.opf & 0xFFu;
-    const uint32_t flags = (in.opf >> 8) & 0xFFu;
+    const uint32_t op = cur.opf & 0xFFu;
     if (op == OP_HALT) break;
+    const uint32_t flags = (cur.opf >> 8) & 0xFFu;
+    uint32_t npc = pc + 1;
+    if (op == OP_CALL) npc = cur.b_lo;
+    if (op == OP_RET) npc = f_ret.get(depth - 1);
+    Ins2 pre = *reinterpret_cast<const Ins2 *>(prog + (npc - 1));
+    const uint64_t act = live & ~failed;
     switch (op) {
-      case OP_SLEEP: {
-        const uint64_t d = u64of(in.a_lo, in.a_hi);
-        if constexpr (STATIC) uacc += d;
-        else if (lane_in(live & ~failed)) acc += (TT)d;
-        ++pc;
+      case OP_SLEEP:
+        if (lane_in(act)) acc += (TT)u64of(cur.a_lo, cur.a_hi);
         break;
-      }
-      case OP_CBEGIN: {
-        if constexpr (STATIC) ucmax = 0;
-        else if (lane_in(live & ~failed)) cmax = 0;
+      case OP_CBEGIN:
+        if (lane_in(act)) cmax = 0;
         cerr = 0;
-        ++pc;
         break;
-      }
-      case OP_CSLEEP: {
-        const uint64_t d = u64of(in.a_lo, in.a_hi);
-        if constexpr (STATIC) ucmax = d > ucmax ? d : ucmax;
-        else if (lane_in(live & ~failed)) cmax = (TT)d > cmax ? (TT)d : cmax;
-        ++pc;
+      case OP_CSLEEP:
+        if (lane_in(act)) {
+          const TT d = (TT)u64of(cur.a_lo, cur.a_hi);
+          cmax = d > cmax ? d : cmax;
+        }
         break;
-      }
-      case OP_CEND: {
-        if constexpr (STATIC) uacc += ucmax;
-        else if (lane_in(live & ~failed)) acc += cmax;
+      case OP_CEND:
+        if (lane_in(act)) acc += cmax;
         if constexpr (MODEB) failed |= cerr & live;
-        ++pc;
         break;
-      }
       case OP_LEAF:
       case OP_CALL: {
-        uint64_t e = live & ~failed;
-        if constexpr (!STATIC) {
-          if (flags & F_PROB) e &= ~draw_skip(in.k, in.opf >> 16, e);
-          if (e == 0) {  // no lane makes this call
-            ++pc;
-            break;
+        uint64_t e = act;
+        if (flags & F_PROB) {  // shouldSkipRequest: Intn(100) < 100 - p
+          bool skip = false;
+          if (lane_in(e)) {
+            uint32_t c0 = t_lo, c1 = t_hi, c2 = myhop, c3 = 1u + (cur.k >> 2);
+            philox10(c0, c1, c2, c3, c.k0, c.k1);
+            const uint32_t sel = cur.k & 3u;
+            const uint32_t word = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+            skip = (word % 100u) < 100u - (cur.opf >> 16);
           }
+          e &= ~ballot(skip);
         }
-        const uint64_t st_own = draw_err(flags, in.thr, e);
-        if constexpr (STATIC) ++uhop;
+        if (e == 0) {  // no lane makes this call: fall through to pc+1
+          if (op == OP_CALL) {
+            npc = pc + 1;
+            pre = *reinterpret_cast<const Ins2 *>(prog + (npc - 1));
+          }
+          break;
+        }
+        uint64_t st = 0;
+        if (flags & F_ERR_ALWAYS) {
+          st = e;
+        } else if (flags & F_ERR_DRAW) {
+          const uint32_t blk = hopn >> 2;
+          const uint64_t need = ballot(blk != cblk) & e;
+          if (need && lane_in(need)) {
+            uint32_t a = t_lo, b = t_hi, cc = blk, d = 0;
+            philox10(a, b, cc, d, c.k0, c.k1);
+            x0 = a;
+            x1 = b;
+            x2 = cc;
+            x3 = d;
+            cblk = blk;
+          }
+          const uint32_t w = hopn & 3u;
+          const uint32_t lo = (w & 1u) ? x1 : x0;
+          const uint32_t hi = (w & 1u) ? x3 : x2;
+          st = ballot(((w & 2u) ? hi : lo) < cur.thr) & e;
+        }
         const uint32_t myh = hopn;
-        if constexpr (!STATIC) {
-          if (lane_in(e)) ++hopn;
-        }
-        if (!(flags & F_ROOT)) count(kp, cnt, in.slot, popc(e));
-        const uint64_t H = u64of(in.a_lo, in.a_hi);
+        if (lane_in(e)) ++hopn;
+        if (!(flags & F_ROOT)) count(c.gstats, c.cnt, cur.slot, popc(e));
+        const uint64_t H = u64of(cur.a_lo, cur.a_hi);
         if (op == OP_LEAF) {
-          if (!(flags & F_ROOT)) count(kp, cnt, (uint32_t)kp.n_slots + in.slot, popc(st_own));
-          if (lane_in(st_own)) ++errh;
-          const uint64_t TL = u64of(in.b_lo, in.b_hi);
-          fold(flags, H, (TT)TL, TL, e, st_own);
-          ++pc;
+          if (!(flags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cur.slot, popc(st));
+          if (lane_in(st)) ++errh;
+          fold(flags, H, (TT)u64of(cur.b_lo, cur.b_hi), e, st);
         } else {
-          // push the caller frame
-          f_ret = wrl(pc + 1, depth, f_ret);
+          f_ret.put(depth, pc + 1);
           f_own.put(depth, own);
+          f_live.put(depth, live);
+          f_failed.put(depth, failed);
           if constexpr (MODEB) f_cerr.put(depth, cerr);
-          if constexpr (STATIC) {
-            f_acc.put(depth, uacc);
-            f_cmax.put(depth, ucmax);
-            uacc = 0;
-            ucmax = 0;
-          } else {
-            f_live.put(depth, live);
-            f_failed.put(depth, failed);
-            lstk[2 * depth * 64 + lane] = acc;
-            lstk[(2 * depth + 1) * 64 + lane] = cmax;
-            hstk[depth * 64 + lane] = myhop;
-            acc = 0;
-            cmax = 0;
-            myhop = myh;
-            live = e;
-          }
+          lstk[(2 * depth) * 64 + lane] = acc;
+          lstk[(2 * depth + 1) * 64 + lane] = cmax;
+          hstk[depth * 64 + lane] = myhop;
+          ++depth;
+          acc = 0;
+          cmax = 0;
+          myhop = myh;
+          live = e;
           failed = 0;
           cerr = 0;
-          own = st_own;
-          ++depth;
-          pc = in.b_lo;
+          own = st;
         }
         break;
       }
@@ -338,80 +500,167 @@ __device__ __forceinline__ void walk_batch(const KParams &kp, uint64_t base, uin
         const uint64_t e = live;
         const uint64_t st = (failed | own) & e;
         const TT T = acc;
-        const uint64_t uT = uacc;
         --depth;
-        const uint32_t ret = rdl(f_ret, depth);
         own = f_own.get(depth);
+        live = f_live.get(depth);
+        failed = f_failed.get(depth);
         if constexpr (MODEB) cerr = f_cerr.get(depth);
         else cerr = 0;
-        if constexpr (STATIC) {
-          uacc = f_acc.get(depth);
-          ucmax = f_cmax.get(depth);
-          failed = 0;
-        } else {
-          live = f_live.get(depth);
-          failed = f_failed.get(depth);
-          acc = lstk[2 * depth * 64 + lane];
-          cmax = lstk[(2 * depth + 1) * 64 + lane];
-          myhop = hstk[depth * 64 + lane];
-        }
-        const Ins cin = prog[ret - 1];
+        acc = lstk[(2 * depth) * 64 + lane];
+        cmax = lstk[(2 * depth + 1) * 64 + lane];
+        myhop = hstk[depth * 64 + lane];
+        const Ins &cin = pre.a;
         const uint32_t cflags = (cin.opf >> 8) & 0xFFu;
-        if (!(cflags & F_ROOT)) count(kp, cnt, (uint32_t)kp.n_slots + cin.slot, popc(st));
+        if (!(cflags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cin.slot, popc(st));
         if (lane_in(st)) ++errh;
-        fold(cflags, u64of(cin.a_lo, cin.a_hi), T, uT, e, st);
-        pc = ret;
+        fold(cflags, u64of(cin.a_lo, cin.a_hi), T, e, st);
         break;
       }
       default:
         __builtin_trap();
     }
+    cur = pre.b;
+    pc = npc;
   }
-
-  // ---- per-trace outputs
-  uint64_t lat;
-  uint32_t hops;
-  if constexpr (STATIC) {
-    lat = uacc;
-    hops = uhop;
-  } else {
-    lat = (uint64_t)acc;
-    hops = hopn;
-  }
-  const bool is500 = lane_in(root_st);
-  if (kp.records != nullptr && valid) {
-    uint4 r;
-    r.x = (uint32_t)lat;
-    r.y = (uint32_t)(lat >> 32);
-    r.z = hops;
-    r.w = (is500 ? 0x80000000u : 0u) | errh;
-    *reinterpret_cast<uint4 *>(kp.records + idx) = r;
-  }
-  hist_add(hist, (is500 ? ISIM_N_PROM : 0u) + prom_bucket(lat), all);
-  const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
-  hist_add(hist + 2 * ISIM_N_PROM, (is500 ? ISIM_N_LOG2 : 0u) + l2, all);
-  const uint64_t s_lat = wave_sum64(valid ? lat : 0);
-  const uint64_t s_hops = wave_sum64(valid ? (uint64_t)hops : 0);
-  const uint64_t s_err = wave_sum64(valid ? (uint64_t)errh : 0);
-  const uint64_t mx = wave_max64(valid ? lat : 0);
-  const uint64_t nmn = wave_max64(valid ? ~lat : 0);
-  if (lane == 0) {
-    atomicAdd(&acc_lds->sum_latency, (unsigned long long)s_lat);
-    atomicAdd(&acc_lds->sum_hops, (unsigned long long)s_hops);
-    atomicAdd(&acc_lds->sum_err, (unsigned long long)s_err);
-    atomicAdd(&acc_lds->n500, (unsigned long long)popc(root_st & all));
-    atomicAdd(&acc_lds->ntr, (unsigned long long)popc(all));
-    atomicMax(&acc_lds->max, (unsigned long long)mx);
-    atomicMax(&acc_lds->notmin, (unsigned long long)nmn);
-  }
+  finish_batch(c, idx, valid, all, (uint64_t)acc, hopn, root_st, errh);
 }
 
-template <bool STATIC, bool MODEB, typename TT>
-__global__ void __launch_bounds__(kWgThreads) isim_walk(KParams kp) {
+
+// ======================================================================
+// DRAW STREAM walk (static walks): every trace executes the same invocation
+// sequence, so the program compiler lays the invocations out in hop order
+// (one 8-byte Node each) and folds the trace-invariant latency (t_static)
+// and hop count.  Per lane and invocation only the stochastic part remains:
+// the Philox error draw, the 500 status (mode B: OR-ed up the call tree at
+// each subtree close), the per-trace error count and the per-site counters.
+// Four records share one Philox block and one s_load_dwordx8; the next
+// group is loaded while the current one is processed.
+// ======================================================================
+struct Node4 {
+  Node n[4];
+};
+
+template <bool MODEB>
+__device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restrict__ stream, uint32_t n_groups,
+                                            uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
+                                            uint64_t n_traces, uint64_t base) {
+  const uint32_t lane = lane_id();
+  const uint64_t idx = base + lane;
+  const bool valid = idx < n_traces;
+  const uint64_t t = trace_begin + idx;
+  const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32);
+  const uint32_t t_hi_u = rfl(t_hi);
+  const bool hi_uniform = ballot(t_hi != t_hi_u) == 0;  // the batch does not straddle 2^32
+  const uint64_t all = ballot(valid);
+  const uint32_t n_all = popc(all);
+
+  uint32_t errh = 0;
+  uint64_t root_st = 0;
+  // mode B: stack of open invocations; the top's running status in SGPRs
+  uint64_t top = 0;
+  uint32_t top_slot = 0, depth = 0;
+  LaneStack<uint64_t> s_mask;
+  LaneStack<uint32_t> s_slot;
+
+  Node4 cur = stream[0];
+  for (uint32_t g = 0; g < n_groups; ++g) {
+    const Node4 nxt = stream[g + 1 < n_groups ? g + 1 : g];  // prefetch the next group
+    uint32_t x[4] = {0, 0, 0, 0};
+    if ((cur.n[0].thr | cur.n[1].thr | cur.n[2].thr | cur.n[3].thr) != 0) {
+      uint32_t a = t_lo, b = t_hi, cc = g, d = 0;
+      if (hi_uniform) {
+        // rounds 1-2 with the uniform counter words (t_hi, g, 0) in SGPR math
+        uint32_t k0a = c.k0, k1a = c.k1;
+        asm volatile("" : "+s"(k0a), "+s"(k1a));
+        const uint64_t q1 = (uint64_t)M1 * g;                      // scalar
+        const uint64_t p0 = (uint64_t)M0 * t_lo;                   // per lane
+        const uint32_t u0 = (uint32_t)(q1 >> 32) ^ t_hi_u ^ k0a;   // uniform
+        const uint32_t u1 = (uint32_t)q1;                          // uniform
+        const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;            // per lane
+        const uint32_t v3 = (uint32_t)p0;                          // per lane
+        const uint32_t k0b = k0a + W0, k1b = k1a + W1;
+        const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
+        const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
+        a = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+        b = (uint32_t)p1;
+        cc = (uint32_t)(q0 >> 32) ^ v3 ^ k1b;
+        d = (uint32_t)q0;
+        uint32_t k0 = k0b + W0, k1 = k1b + W1;
+#pragma unroll
+        for (int r = 2; r < 10; ++r) {
+          round1(a, b, cc, d, k0, k1);
+          k0 += W0;
+          k1 += W1;
+        }
+      } else {
+        philox10(a, b, cc, d, c.k0, c.k1);
+      }
+      x[0] = a;
+      x[1] = b;
+      x[2] = cc;
+      x[3] = d;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t meta = cur.n[j].meta;
+      const uint32_t slot = meta & 0xFFFFFFu;
+      if (slot == kSlotPad) continue;
+      const uint64_t own = (meta & 0x80000000u) ? all : (ballot(x[j] < cur.n[j].thr) & all);
+      if constexpr (!MODEB) {
+        // mode A: an invocation's status is its own error draw
+        if (lane_in(own)) ++errh;
+        if (slot == kSlotRoot) {
+          root_st = own;
+        } else {
+          count(c.gstats, c.cnt, slot, n_all);
+          count(c.gstats, c.cnt, c.n_slots + slot, popc(own));
+        }
+      } else {
+        if (slot != kSlotRoot) count(c.gstats, c.cnt, slot, n_all);
+        if (depth > 0) {
+          s_mask.put(depth - 1, top);
+          s_slot.put(depth - 1, top_slot);
+        }
+        top = own;
+        top_slot = slot;
+        ++depth;
+        for (uint32_t k = (meta >> 24) & 0x7Fu; k > 0; --k) {  // subtree closes
+          const uint64_t st = top;
+          if (lane_in(st)) ++errh;
+          if (top_slot != kSlotRoot) count(c.gstats, c.cnt, c.n_slots + top_slot, popc(st));
+          --depth;
+          if (depth > 0) {
+            top = s_mask.get(depth - 1) | st;  // a callee's 500 fails the caller (mode B)
+            top_slot = s_slot.get(depth - 1);
+          } else {
+            root_st = st;
+          }
+        }
+      }
+    }
+    cur = nxt;
+  }
+  finish_batch(c, idx, valid, all, t_static, n_nodes, root_st, errh);
+}
+
+// KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream
+template <int KIND, bool MODEB>
+__global__ void __launch_bounds__(kWgThreads)
+    isim_walk(const Ins *__restrict__ prog, isim_trace_rec *__restrict__ records, uint64_t *__restrict__ gstats,
+              KParams kp) {
+  using TT = typename std::conditional<KIND == 0 || KIND == 2, uint32_t, uint64_t>::type;
+  constexpr bool STATIC = KIND < 2 || KIND == 4;
   extern __shared__ __align__(16) unsigned char lds[];
-  WgAcc *acc = reinterpret_cast<WgAcc *>(lds);
-  uint32_t *hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
-  uint32_t *cnt = kp.lds_counters ? hist + kHistWords : nullptr;
+  Ctx c;
+  c.prog = prog;
+  c.records = records;
+  c.gstats = gstats;
+  c.acc = reinterpret_cast<WgAcc *>(lds);
+  c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
+  c.cnt = kp.lds_counters ? c.hist + kHistWords : nullptr;
+  c.n_slots = kp.n_slots;
+  c.k0 = kp.seed_lo;
+  c.k1 = kp.seed_hi;
   unsigned char *stk = lds + kLdsAccBytes + kHistWords * 4 + (kp.lds_counters ? 8u * kp.n_slots : 0u);
   stk = (unsigned char *)(((uintptr_t)stk + 15) & ~(uintptr_t)15);
   const uint32_t wave = threadIdx.x >> 6;
@@ -419,11 +668,10 @@ __global__ void __launch_bounds__(kWgThreads) isim_walk(KParams kp) {
   TT *lstk = nullptr;
   uint32_t *hstk = nullptr;
   if constexpr (!STATIC) {
-    const uint32_t per_wave = kp.max_frames * 64u * (2u * sizeof(TT) + 4u);
+    const uint32_t per_wave = kp.max_frames * 64u * (2u * (uint32_t)sizeof(TT) + 4u);
     lstk = reinterpret_cast<TT *>(stk + wave * per_wave);
-    hstk = reinterpret_cast<uint32_t *>(stk + wave * per_wave + kp.max_frames * 64u * 2u * sizeof(TT));
+    hstk = reinterpret_cast<uint32_t *>(stk + wave * per_wave + kp.max_frames * 64u * 2u * (uint32_t)sizeof(TT));
   }
-  // zero the workgroup accumulators
   const uint32_t zero_words = (kLdsAccBytes / 4) + kHistWords + (kp.lds_counters ? 2u * kp.n_slots : 0u);
   uint32_t *z = reinterpret_cast<uint32_t *>(lds);
   for (uint32_t i = threadIdx.x; i < zero_words; i += blockDim.x) z[i] = 0;
@@ -431,40 +679,45 @@ __global__ void __launch_bounds__(kWgThreads) isim_walk(KParams kp) {
 
   const uint64_t n_batches = (kp.n_traces + 63) / 64;
   const uint64_t stride = (uint64_t)gridDim.x * waves;
-  for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride)
-    walk_batch<STATIC, MODEB, TT>(kp, b * 64, cnt, hist, acc, lstk, hstk);
+  for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
+    if constexpr (KIND == 4)
+      walk_stream<MODEB>(c, reinterpret_cast<const Node4 *>(prog), kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0,
+                         kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces, b * 64);
+    else if constexpr (STATIC) walk_static<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64);
+    else walk_dynamic<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64, lstk, hstk);
+  }
 
   __syncthreads();
   // ---- flush workgroup accumulators to HBM
-  unsigned long long *st = reinterpret_cast<unsigned long long *>(kp.stats);
+  unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
-    if (hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)hist[i]);
-  if (cnt) {
+    if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
+  if (c.cnt) {
     for (uint32_t i = threadIdx.x; i < 2u * kp.n_slots; i += blockDim.x)
-      if (cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)cnt[i]);
+      if (c.cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)c.cnt[i]);
   }
-  if (threadIdx.x == 0 && acc->ntr) {
-    atomicAdd(st + ISIM_ST_N_TRACES, acc->ntr);
-    atomicAdd(st + ISIM_ST_SUM_LATENCY, acc->sum_latency);
-    atomicAdd(st + ISIM_ST_SUM_HOPS, acc->sum_hops);
-    atomicAdd(st + ISIM_ST_SUM_ERR_HOPS, acc->sum_err);
-    atomicAdd(st + ISIM_ST_N_500, acc->n500);
-    atomicMax(st + ISIM_ST_NOT_MIN_LATENCY, acc->notmin);
-    atomicMax(st + ISIM_ST_MAX_LATENCY, acc->max);
+  if (threadIdx.x == 0 && c.acc->ntr) {
+    atomicAdd(st + ISIM_ST_N_TRACES, c.acc->ntr);
+    atomicAdd(st + ISIM_ST_SUM_LATENCY, c.acc->sum_latency);
+    atomicAdd(st + ISIM_ST_SUM_HOPS, c.acc->sum_hops);
+    atomicAdd(st + ISIM_ST_SUM_ERR_HOPS, c.acc->sum_err);
+    atomicAdd(st + ISIM_ST_N_500, c.acc->n500);
+    atomicMax(st + ISIM_ST_NOT_MIN_LATENCY, c.acc->notmin);
+    atomicMax(st + ISIM_ST_MAX_LATENCY, c.acc->max);
   }
 }
 
 }  // namespace dev
 
-// Kernel table: [static][modeB][time64]
-void *walk_kernel(bool is_static, bool modeb, bool time64) {
+void *walk_kernel(int kind, bool modeb) {
   using namespace dev;
-  if (is_static) {
-    return modeb ? (void *)&isim_walk<true, true, uint64_t> : (void *)&isim_walk<true, false, uint64_t>;
+  switch (kind) {
+    case 4: return modeb ? (void *)&isim_walk<4, true> : (void *)&isim_walk<4, false>;
+    case 0: return modeb ? (void *)&isim_walk<0, true> : (void *)&isim_walk<0, false>;
+    case 1: return modeb ? (void *)&isim_walk<1, true> : (void *)&isim_walk<1, false>;
+    case 2: return modeb ? (void *)&isim_walk<2, true> : (void *)&isim_walk<2, false>;
+    default: return modeb ? (void *)&isim_walk<3, true> : (void *)&isim_walk<3, false>;
   }
-  if (time64)
-    return modeb ? (void *)&isim_walk<false, true, uint64_t> : (void *)&isim_walk<false, false, uint64_t>;
-  return modeb ? (void *)&isim_walk<false, true, uint32_t> : (void *)&isim_walk<false, false, uint32_t>;
 }
 
 }  // namespace isim

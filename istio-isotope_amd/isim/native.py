@@ -22,6 +22,7 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
+FLAG_NO_STREAM = 1
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
@@ -42,7 +43,8 @@ class IsimError(RuntimeError):
 class Params(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("hop_base_ns", C.c_uint64),
                 ("req_ps_per_byte", C.c_uint64), ("resp_ps_per_byte", C.c_uint64),
-                ("error_mode", C.c_uint32), ("max_depth", C.c_uint32)]
+                ("error_mode", C.c_uint32), ("max_depth", C.c_uint32),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class TraceRec(C.Structure):
@@ -55,6 +57,11 @@ class HandlerInfo(C.Structure):
                 ("time_bits", C.c_int32), ("program_len", C.c_int32),
                 ("max_latency_ns", C.c_uint64), ("hops_upper", C.c_uint64),
                 ("stats_words", C.c_uint64)]
+
+
+class LaunchInfo(C.Structure):
+    _fields_ = [("wg_threads", C.c_int32), ("lds_bytes", C.c_int32), ("lds_counters", C.c_int32),
+                ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32)]
 
 
 # every function declared in include/isim.h: name -> (restype, argtypes)
@@ -73,6 +80,7 @@ SIGNATURES = {
     "isim_handler_create": (C.c_int, [_VP, C.c_char_p, C.POINTER(Params), C.POINTER(_VP)]),
     "isim_handler_free": (None, [_VP]),
     "isim_handler_info_get": (C.c_int, [_VP, C.POINTER(HandlerInfo)]),
+    "isim_handler_launch_info": (C.c_int, [_VP, C.c_int, C.POINTER(LaunchInfo)]),
     "isim_handler_slots": (C.c_int, [_VP, _VP, _VP]),
     "isim_serve_device": (C.c_int, [_VP, C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
     "isim_serve": (C.c_int, [_VP, C.c_int, C.c_uint64, C.c_uint64, _VP, _VP]),

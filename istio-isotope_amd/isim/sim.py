@@ -32,10 +32,11 @@ class SimParams:
     resp_ps_per_byte: int = 80
     error_mode: int = native.MODE_A
     max_depth: int = 0
+    flags: int = 0
 
     def to_c(self) -> native.Params:
         return native.Params(self.seed & ((1 << 64) - 1), self.hop_base_ns, self.req_ps_per_byte,
-                             self.resp_ps_per_byte, self.error_mode, self.max_depth)
+                             self.resp_ps_per_byte, self.error_mode, self.max_depth, self.flags, 0)
 
 
 class Handler:
@@ -62,6 +63,11 @@ class Handler:
         if h is not None and h.value and native._lib is not None:
             native._lib.isim_handler_free(h)
             self._h = None
+
+    def launch_info(self, device: int = 0) -> dict:
+        li = native.LaunchInfo()
+        native.check(native.load().isim_handler_launch_info(self._h, device, C.byref(li)))
+        return {k: getattr(li, k) for k, _ in native.LaunchInfo._fields_}
 
     @property
     def stats_words(self) -> int:

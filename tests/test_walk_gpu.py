@@ -26,16 +26,28 @@ def _fixture_json(path, error_rate=None):
     return j
 
 
+KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM}
+
+
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
 @pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
-def test_reference_topologies(gpu, path, mode):
-    c = Case(_fixture_json(path, error_rate=0.05), None, isim.SimParams(error_mode=mode))
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_reference_topologies(gpu, path, mode, kernel):
+    c = Case(_fixture_json(path, error_rate=0.05), None, isim.SimParams(error_mode=mode, flags=KERNELS[kernel]))
+    kind = c.handler.launch_info(0)["kernel_kind"]
+    tb64 = c.handler.info.time_bits == 64
+    if c.handler.info.static_walk:
+        assert kind == (4 if kernel == "stream" else int(tb64))
+    else:
+        assert kind == 2 + int(tb64)
     c.compare(0, 3000)
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4097])
-def test_ragged_batches(gpu, n):
-    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3))
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_ragged_batches(gpu, n, kernel):
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
+             isim.SimParams(flags=KERNELS[kernel]))
     c.compare(777, n)
 
 
@@ -45,18 +57,21 @@ def test_zero_traces(gpu):
     assert stats.sum() == 0
 
 
-def test_trace_ids_cross_2_32(gpu):
-    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3))
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_trace_ids_cross_2_32(gpu, kernel):
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
+             isim.SimParams(flags=KERNELS[kernel]))
     c.compare((1 << 32) - 1000, 2000)
 
 
-def test_error_always_and_never(gpu):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_error_always_and_never(gpu, kernel):
     j = json.dumps({"services": [
         {"name": "e", "isEntrypoint": True, "script": [{"call": "a"}, [{"call": "b"}, {"call": "a"}]]},
         {"name": "a", "errorRate": 1.0},
         {"name": "b", "errorRate": "0%", "script": [{"call": "a"}, {"sleep": "1ms"}]}]})
     for mode in (isim.MODE_A, isim.MODE_B):
-        Case(j, None, isim.SimParams(error_mode=mode)).compare(0, 500)
+        Case(j, None, isim.SimParams(error_mode=mode, flags=KERNELS[kernel])).compare(0, 500)
 
 
 def test_probability_and_mode_b_abort(gpu):
@@ -89,16 +104,18 @@ def test_large_latency_u64(gpu):
     c.compare(0, 5000)
 
 
-def test_tree_sequential_config2(gpu):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_tree_sequential_config2(gpu, kernel):
     j = obj_to_json(config2_topology())
-    c = Case(with_defaults(j, errorRate=0.01))
+    c = Case(with_defaults(j, errorRate=0.01), None, isim.SimParams(flags=KERNELS[kernel]))
     c.compare(0, 2048)
 
 
-def test_realistic_config3(gpu):
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_realistic_config3(gpu, kernel):
     j = obj_to_json(config3_topology())
     for mode in (isim.MODE_A, isim.MODE_B):
-        Case(j, None, isim.SimParams(error_mode=mode)).compare(1 << 20, 1024)
+        Case(j, None, isim.SimParams(error_mode=mode, flags=KERNELS[kernel])).compare(1 << 20, 1024)
 
 
 def test_realistic_sequential_probability(gpu):
