@@ -120,8 +120,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
+    from isim.dist import merge_stats, shard_begin
+
     def step(s):
-        begin = (s * world + rank) * B
+        begin = shard_begin(rank, world, s, B)
         h.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), sptr)
 
     for s in range(args.warmup):
@@ -138,11 +140,7 @@ def main():
         step(args.warmup + i)
         ev[i][1].record(stream)
     if world > 1:
-        # one all-reduce of the counters/histograms; extrema words merge with MAX
-        ext = stats[isim.native.ST_NOT_MIN_LATENCY:isim.native.ST_MAX_LATENCY + 1].clone()
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
-        dist.all_reduce(ext, op=dist.ReduceOp.MAX)
-        stats[isim.native.ST_NOT_MIN_LATENCY:isim.native.ST_MAX_LATENCY + 1] = ext
+        merge_stats(stats)  # one RCCL all-reduce (SUM) + the 2-word extrema MAX
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

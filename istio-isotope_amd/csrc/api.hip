@@ -34,6 +34,7 @@ int fail(int code, const std::string &msg) {
 
 struct DevState {
   void *d_prog = nullptr;  // Ins[] (interpreters) or Node[] (draw stream)
+  uint32_t *d_mult = nullptr;  // draw stream: per-slot call multiplicity
   void *kernel = nullptr;
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
@@ -59,6 +60,7 @@ struct isim_handler {
       int cur = 0;
       if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
         (void)hipFree(kv.second.d_prog);
+        (void)hipFree(kv.second.d_mult);
         (void)hipSetDevice(cur);
       }
     }
@@ -111,7 +113,7 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   st.lds_counters = counters ? 1u : 0u;
   st.kind = p.stream_nodes ? 4u : (p.static_walk ? 0u : 2u) + (p.time_bits == 64 ? 1u : 0u);
   if ((h->params.flags & ISIM_FLAG_NO_STREAM) && st.kind == 4) st.kind = p.time_bits == 64 ? 1u : 0u;
-  st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B);
+  st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
   HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)st.lds_bytes));
   int per_cu = 0;
@@ -124,6 +126,11 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   const size_t bytes = st.kind == 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
   HIPCHK(hipMalloc(&st.d_prog, bytes));
   HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
+  if (st.kind == 4 && p.n_slots > 0) {
+    HIPCHK(hipMalloc(&st.d_mult, p.stream_mult.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(st.d_mult, p.stream_mult.data(), p.stream_mult.size() * sizeof(uint32_t),
+                     hipMemcpyHostToDevice));
+  }
   auto res = h->dev.emplace(device, st);
   out = &res.first->second;
   return ISIM_OK;
@@ -291,6 +298,13 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   void *args[] = {&prog, &d_records, &d_stats, &kp};
   HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
                          (hipStream_t)hip_stream));
+  if (st->kind == 4 && h->prog.n_slots > 0) {
+    uint32_t n_slots = (uint32_t)h->prog.n_slots;
+    const uint32_t *mult = st->d_mult;
+    void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};
+    HIPCHK(hipLaunchKernel(isim::stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args2, 0,
+                           (hipStream_t)hip_stream));
+  }
   return ISIM_OK;
 }
 

@@ -310,6 +310,9 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
       }
     }
     out.stream_nodes = (uint32_t)out.stream.size();
+    out.stream_mult.assign((size_t)out.n_slots, 0u);
+    for (const Node &nd : out.stream)
+      if ((nd.meta & 0xFFFFFFu) != kSlotRoot) out.stream_mult[nd.meta & 0xFFFFFFu] += 1;
     while (out.stream.size() % 4) out.stream.push_back(Node{0u, kSlotPad});
   }
   if (code.size() >= (1u << 30)) {

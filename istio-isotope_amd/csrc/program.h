@@ -34,6 +34,7 @@ struct Program {
   // draw stream (static walks whose unrolled invocation tree is <= kMaxStreamNodes)
   std::vector<Node> stream;                     // padded to a multiple of 4
   uint32_t stream_nodes = 0;                    // invocations per trace (unpadded)
+  std::vector<uint32_t> stream_mult;            // per slot: calls through it per trace
 };
 
 // Returns an isim_status; on error `err` holds the message.

@@ -529,22 +529,70 @@ __device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin,
 // ======================================================================
 // DRAW STREAM walk (static walks): every trace executes the same invocation
 // sequence, so the program compiler lays the invocations out in hop order
-// (one 8-byte Node each) and folds the trace-invariant latency (t_static)
-// and hop count.  Per lane and invocation only the stochastic part remains:
-// the Philox error draw, the 500 status (mode B: OR-ed up the call tree at
-// each subtree close), the per-trace error count and the per-site counters.
-// Four records share one Philox block and one s_load_dwordx8; the next
-// group is loaded while the current one is processed.
+// (one 8-byte Node each) and folds the trace-invariant latency (t_static),
+// hop count and per-site call multiplicities (the executed-call counters are
+// mult[slot] x n_traces, added by isim_stream_calls).  Per lane and
+// invocation only the stochastic part remains: the Philox error draw, the
+// 500 status (mode B: OR-ed up the call tree at each subtree close), the
+// per-trace error count and the per-site error counters.  Four records share
+// one Philox block and one s_load_dwordx8; two group buffers ping-pong so the
+// next group's load is in flight while the current one is processed.
 // ======================================================================
 struct Node4 {
   Node n[4];
 };
 
-template <bool MODEB>
+template <bool LDSC>
+__device__ __forceinline__ void count_t(uint64_t *__restrict__ gstats, uint32_t *cnt, uint32_t idx, uint32_t v,
+                                        bool lane0) {
+  if (lane0) {
+    if constexpr (LDSC) atomicAdd(cnt + idx, v);
+    else atomicAdd((unsigned long long *)(gstats + ISIM_ST_SITES + idx), (unsigned long long)v);
+  }
+}
+
+// Philox4x32-10 of counter (t_lo, t_hi, g, 0); rounds 1-2 fold the
+// wave-uniform words (t_hi when the batch does not straddle 2^32, g, 0) into
+// scalar math.
+__device__ __forceinline__ void philox_group(uint32_t t_lo, uint32_t t_hi, uint32_t t_hi_u, bool hi_uniform,
+                                             uint32_t g, uint32_t k0a, uint32_t k1a, uint32_t (&x)[4]) {
+  uint32_t a = t_lo, b = t_hi, cc = g, d = 0;
+  if (hi_uniform) {
+    const uint64_t q1 = (uint64_t)M1 * g;                      // scalar
+    const uint64_t p0 = (uint64_t)M0 * t_lo;                   // per lane
+    const uint32_t u0 = (uint32_t)(q1 >> 32) ^ t_hi_u ^ k0a;   // uniform
+    const uint32_t u1 = (uint32_t)q1;                          // uniform
+    const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;            // per lane
+    const uint32_t v3 = (uint32_t)p0;                          // per lane
+    const uint32_t k0b = k0a + W0, k1b = k1a + W1;
+    const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
+    const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
+    a = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+    b = (uint32_t)p1;
+    cc = (uint32_t)(q0 >> 32) ^ v3 ^ k1b;
+    d = (uint32_t)q0;
+    uint32_t k0 = k0b + W0, k1 = k1b + W1;
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+      round1(a, b, cc, d, k0, k1);
+      k0 += W0;
+      k1 += W1;
+    }
+  } else {
+    philox10(a, b, cc, d, k0a, k1a);
+  }
+  x[0] = a;
+  x[1] = b;
+  x[2] = cc;
+  x[3] = d;
+}
+
+template <bool MODEB, bool LDSC>
 __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restrict__ stream, uint32_t n_groups,
                                             uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
                                             uint64_t n_traces, uint64_t base) {
   const uint32_t lane = lane_id();
+  const bool lane0 = lane == 0;
   const uint64_t idx = base + lane;
   const bool valid = idx < n_traces;
   const uint64_t t = trace_begin + idx;
@@ -552,7 +600,6 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
   const uint32_t t_hi_u = rfl(t_hi);
   const bool hi_uniform = ballot(t_hi != t_hi_u) == 0;  // the batch does not straddle 2^32
   const uint64_t all = ballot(valid);
-  const uint32_t n_all = popc(all);
 
   uint32_t errh = 0;
   uint64_t root_st = 0;
@@ -562,90 +609,90 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
   LaneStack<uint64_t> s_mask;
   LaneStack<uint32_t> s_slot;
 
-  Node4 cur = stream[0];
-  for (uint32_t g = 0; g < n_groups; ++g) {
-    const Node4 nxt = stream[g + 1 < n_groups ? g + 1 : g];  // prefetch the next group
-    uint32_t x[4] = {0, 0, 0, 0};
-    if ((cur.n[0].thr | cur.n[1].thr | cur.n[2].thr | cur.n[3].thr) != 0) {
-      uint32_t a = t_lo, b = t_hi, cc = g, d = 0;
-      if (hi_uniform) {
-        // rounds 1-2 with the uniform counter words (t_hi, g, 0) in SGPR math
-        uint32_t k0a = c.k0, k1a = c.k1;
-        asm volatile("" : "+s"(k0a), "+s"(k1a));
-        const uint64_t q1 = (uint64_t)M1 * g;                      // scalar
-        const uint64_t p0 = (uint64_t)M0 * t_lo;                   // per lane
-        const uint32_t u0 = (uint32_t)(q1 >> 32) ^ t_hi_u ^ k0a;   // uniform
-        const uint32_t u1 = (uint32_t)q1;                          // uniform
-        const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;            // per lane
-        const uint32_t v3 = (uint32_t)p0;                          // per lane
-        const uint32_t k0b = k0a + W0, k1b = k1a + W1;
-        const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
-        const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
-        a = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
-        b = (uint32_t)p1;
-        cc = (uint32_t)(q0 >> 32) ^ v3 ^ k1b;
-        d = (uint32_t)q0;
-        uint32_t k0 = k0b + W0, k1 = k1b + W1;
-#pragma unroll
-        for (int r = 2; r < 10; ++r) {
-          round1(a, b, cc, d, k0, k1);
-          k0 += W0;
-          k1 += W1;
-        }
-      } else {
-        philox10(a, b, cc, d, c.k0, c.k1);
+  auto node = [&](uint32_t thr, uint32_t meta, uint32_t xw) {
+    const uint32_t slot = meta & 0xFFFFFFu;
+    const uint64_t own = (meta & 0x80000000u) ? all : (ballot(xw < thr) & all);
+    if constexpr (!MODEB) {
+      // mode A: an invocation's status is its own error draw; padding
+      // records (thr 0, never always) draw nothing.
+      // (the root, record 0, is peeled off before the loop)
+      errh += lane_in(own) ? 1u : 0u;
+      if (own) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, popc(own), lane0);
+    } else {
+      if (slot == kSlotPad) return;
+      if (depth > 0) {
+        s_mask.put(depth - 1, top);
+        s_slot.put(depth - 1, top_slot);
       }
-      x[0] = a;
-      x[1] = b;
-      x[2] = cc;
-      x[3] = d;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t meta = cur.n[j].meta;
-      const uint32_t slot = meta & 0xFFFFFFu;
-      if (slot == kSlotPad) continue;
-      const uint64_t own = (meta & 0x80000000u) ? all : (ballot(x[j] < cur.n[j].thr) & all);
-      if constexpr (!MODEB) {
-        // mode A: an invocation's status is its own error draw
-        if (lane_in(own)) ++errh;
-        if (slot == kSlotRoot) {
-          root_st = own;
-        } else {
-          count(c.gstats, c.cnt, slot, n_all);
-          count(c.gstats, c.cnt, c.n_slots + slot, popc(own));
-        }
-      } else {
-        if (slot != kSlotRoot) count(c.gstats, c.cnt, slot, n_all);
+      top = own;
+      top_slot = slot;
+      ++depth;
+      for (uint32_t k = (meta >> 24) & 0x7Fu; k > 0; --k) {  // subtree closes
+        const uint64_t st = top;
+        errh += lane_in(st) ? 1u : 0u;
+        if (st && top_slot != kSlotRoot) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + top_slot, popc(st), lane0);
+        --depth;
         if (depth > 0) {
-          s_mask.put(depth - 1, top);
-          s_slot.put(depth - 1, top_slot);
-        }
-        top = own;
-        top_slot = slot;
-        ++depth;
-        for (uint32_t k = (meta >> 24) & 0x7Fu; k > 0; --k) {  // subtree closes
-          const uint64_t st = top;
-          if (lane_in(st)) ++errh;
-          if (top_slot != kSlotRoot) count(c.gstats, c.cnt, c.n_slots + top_slot, popc(st));
-          --depth;
-          if (depth > 0) {
-            top = s_mask.get(depth - 1) | st;  // a callee's 500 fails the caller (mode B)
-            top_slot = s_slot.get(depth - 1);
-          } else {
-            root_st = st;
-          }
+          top = s_mask.get(depth - 1) | st;  // a callee's 500 fails the caller (mode B)
+          top_slot = s_slot.get(depth - 1);
+        } else {
+          root_st = st;
         }
       }
     }
-    cur = nxt;
+  };
+  auto draws = [&](const Node4 &q, uint32_t g, uint32_t (&x)[4]) {
+    if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0)
+      philox_group(t_lo, t_hi, t_hi_u, hi_uniform, g, c.k0, c.k1, x);
+  };
+  auto group = [&](const Node4 &q, uint32_t g) {
+    uint32_t x[4] = {0, 0, 0, 0};
+    draws(q, g, x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) node(q.n[j].thr, q.n[j].meta, x[j]);
+  };
+
+  Node4 bufA = stream[0];
+  Node4 bufB;
+  if (n_groups > 1) bufB = stream[1];
+  {  // group 0: record 0 is the entry invocation (the client request)
+    uint32_t x[4] = {0, 0, 0, 0};
+    draws(bufA, 0, x);
+    if constexpr (!MODEB) {
+      const uint64_t own = (bufA.n[0].meta & 0x80000000u) ? all : (ballot(x[0] < bufA.n[0].thr) & all);
+      errh += lane_in(own) ? 1u : 0u;
+      root_st = own;
+    } else {
+      node(bufA.n[0].thr, bufA.n[0].meta, x[0]);
+    }
+#pragma unroll
+    for (int j = 1; j < 4; ++j) node(bufA.n[j].thr, bufA.n[j].meta, x[j]);
+  }
+  uint32_t g = 1;
+  while (g < n_groups) {
+    if (g + 1 < n_groups) bufA = stream[g + 1];
+    group(bufB, g);
+    if (++g >= n_groups) break;
+    if (g + 1 < n_groups) bufB = stream[g + 1];
+    group(bufA, g);
+    if (++g >= n_groups) break;
   }
   finish_batch(c, idx, valid, all, t_static, n_nodes, root_st, errh);
 }
 
+// Executed-call counters of a static walk: every trace makes mult[slot] calls
+// through each reachable call site, so a launch over n_traces adds
+// mult[slot] * n_traces (exact; added once per launch).
+__global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_slots, uint64_t n_traces,
+                                  uint64_t *__restrict__ gstats) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_slots) gstats[ISIM_ST_SITES + i] += (uint64_t)mult[i] * n_traces;
+}
+
 // KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream
-template <int KIND, bool MODEB>
-__global__ void __launch_bounds__(kWgThreads)
+// LDSC: per-site counters in the workgroup LDS table (else global atomics)
+template <int KIND, bool MODEB, bool LDSC>
+__global__ void __launch_bounds__(kWgThreads, KIND == 4 ? 8 : 1)
     isim_walk(const Ins *__restrict__ prog, isim_trace_rec *__restrict__ records, uint64_t *__restrict__ gstats,
               KParams kp) {
   using TT = typename std::conditional<KIND == 0 || KIND == 2, uint32_t, uint64_t>::type;
@@ -657,11 +704,11 @@ __global__ void __launch_bounds__(kWgThreads)
   c.gstats = gstats;
   c.acc = reinterpret_cast<WgAcc *>(lds);
   c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
-  c.cnt = kp.lds_counters ? c.hist + kHistWords : nullptr;
+  c.cnt = LDSC ? c.hist + kHistWords : nullptr;
   c.n_slots = kp.n_slots;
   c.k0 = kp.seed_lo;
   c.k1 = kp.seed_hi;
-  unsigned char *stk = lds + kLdsAccBytes + kHistWords * 4 + (kp.lds_counters ? 8u * kp.n_slots : 0u);
+  unsigned char *stk = lds + kLdsAccBytes + kHistWords * 4 + (LDSC ? 8u * kp.n_slots : 0u);
   stk = (unsigned char *)(((uintptr_t)stk + 15) & ~(uintptr_t)15);
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t waves = blockDim.x >> 6;
@@ -672,7 +719,7 @@ __global__ void __launch_bounds__(kWgThreads)
     lstk = reinterpret_cast<TT *>(stk + wave * per_wave);
     hstk = reinterpret_cast<uint32_t *>(stk + wave * per_wave + kp.max_frames * 64u * 2u * (uint32_t)sizeof(TT));
   }
-  const uint32_t zero_words = (kLdsAccBytes / 4) + kHistWords + (kp.lds_counters ? 2u * kp.n_slots : 0u);
+  const uint32_t zero_words = (kLdsAccBytes / 4) + kHistWords + (LDSC ? 2u * kp.n_slots : 0u);
   uint32_t *z = reinterpret_cast<uint32_t *>(lds);
   for (uint32_t i = threadIdx.x; i < zero_words; i += blockDim.x) z[i] = 0;
   __syncthreads();
@@ -681,7 +728,7 @@ __global__ void __launch_bounds__(kWgThreads)
   const uint64_t stride = (uint64_t)gridDim.x * waves;
   for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
     if constexpr (KIND == 4)
-      walk_stream<MODEB>(c, reinterpret_cast<const Node4 *>(prog), kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0,
+      walk_stream<MODEB, LDSC>(c, reinterpret_cast<const Node4 *>(prog), kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0,
                          kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces, b * 64);
     else if constexpr (STATIC) walk_static<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64);
     else walk_dynamic<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64, lstk, hstk);
@@ -692,7 +739,7 @@ __global__ void __launch_bounds__(kWgThreads)
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
-  if (c.cnt) {
+  if constexpr (LDSC) {
     for (uint32_t i = threadIdx.x; i < 2u * kp.n_slots; i += blockDim.x)
       if (c.cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)c.cnt[i]);
   }
@@ -709,15 +756,23 @@ __global__ void __launch_bounds__(kWgThreads)
 
 }  // namespace dev
 
-void *walk_kernel(int kind, bool modeb) {
+template <int K>
+static void *pick(bool modeb, bool ldsc) {
   using namespace dev;
+  if (ldsc) return modeb ? (void *)&isim_walk<K, true, true> : (void *)&isim_walk<K, false, true>;
+  return modeb ? (void *)&isim_walk<K, true, false> : (void *)&isim_walk<K, false, false>;
+}
+
+void *walk_kernel(int kind, bool modeb, bool lds_counters) {
   switch (kind) {
-    case 4: return modeb ? (void *)&isim_walk<4, true> : (void *)&isim_walk<4, false>;
-    case 0: return modeb ? (void *)&isim_walk<0, true> : (void *)&isim_walk<0, false>;
-    case 1: return modeb ? (void *)&isim_walk<1, true> : (void *)&isim_walk<1, false>;
-    case 2: return modeb ? (void *)&isim_walk<2, true> : (void *)&isim_walk<2, false>;
-    default: return modeb ? (void *)&isim_walk<3, true> : (void *)&isim_walk<3, false>;
+    case 0: return pick<0>(modeb, lds_counters);
+    case 1: return pick<1>(modeb, lds_counters);
+    case 2: return pick<2>(modeb, lds_counters);
+    case 3: return pick<3>(modeb, lds_counters);
+    default: return pick<4>(modeb, lds_counters);
   }
 }
+
+void *stream_calls_kernel() { return (void *)&dev::isim_stream_calls; }
 
 }  // namespace isim

@@ -15,7 +15,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libisim.so")
+LIB_PATH = os.environ.get("ISIM_LIB") or os.path.join(_HERE, "libisim.so")
 
 # isim_status
 OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = range(10)

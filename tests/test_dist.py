@@ -1,0 +1,93 @@
+"""Multi-process path on CPU (gloo, world_size 2): trace sharding and the
+stats merge used by bench.py (isim.dist), with the C oracle producing each
+rank's shard.  The merged buffer must equal one process over the union."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _graph_json():
+    from isim.generators import realistic_topology
+    from isim.yamljson import obj_to_json
+    return obj_to_json(realistic_topology(300, "multitier", seed=5, concurrent=True, sleep_ms=(1, 5),
+                                          error_rate=(0, 0.2)))
+
+
+def _oracle_stats(begin, n):
+    from oracle import executor as oc
+    from oracle import graph_ref as gr
+    from oracle.executor_py import SimGraph, SimParams
+    sg = SimGraph(gr.unmarshal_service_graph(_graph_json()))
+    _, st = oc.run(sg, SimParams(), sg.entry(), begin, n, records=False, n_threads=1)
+    return st
+
+
+def _to_isim_layout(st):
+    # oracle layout keeps min at word 5; isim keeps ~min
+    out = st.astype(np.uint64).copy()
+    out[5] = ~out[5]
+    return out.view(np.int64)
+
+
+def _worker(rank, world, port, steps, batch, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "istio-isotope_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from isim.dist import merge_stats, shard_begin
+    acc = None
+    for s in range(steps):
+        st = _to_isim_layout(_oracle_stats(shard_begin(rank, world, s, batch), batch))
+        acc = st if acc is None else _combine(acc, st)
+    t = torch.from_numpy(acc.copy())
+    merge_stats(t)
+    if rank == 0:
+        q.put(t.numpy().copy())
+    dist.destroy_process_group()
+
+
+def _combine(a, b):
+    out = a + b
+    ua, ub = a.view(np.uint64), b.view(np.uint64)
+    out.view(np.uint64)[5] = max(ua[5], ub[5])
+    out.view(np.uint64)[6] = max(ua[6], ub[6])
+    return out
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_merge_equals_single_process(world):
+    steps, batch = 2, 150
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    merged = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    single = _to_isim_layout(_oracle_stats(0, steps * world * batch))
+    assert np.array_equal(merged.view(np.uint64), single.view(np.uint64))
+
+
+def test_shard_ranges_partition():
+    from isim.dist import shard_begin
+    world, steps, batch = 4, 3, 10
+    ids = sorted(i for s in range(steps) for r in range(world)
+                 for i in range(shard_begin(r, world, s, batch), shard_begin(r, world, s, batch) + batch))
+    assert ids == list(range(world * steps * batch))
