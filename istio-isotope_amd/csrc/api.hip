@@ -290,7 +290,8 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   kp.lds_counters = st->lds_counters;
   kp.n_nodes = h->prog.stream_nodes;
   kp.t_static = h->prog.max_latency;
-  const uint64_t batches = (n_traces + 63) / 64;
+  const uint64_t per_wave = st->kind == 4 ? isim::stream_traces_per_wave() : 64u;
+  const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);

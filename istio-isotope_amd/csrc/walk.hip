@@ -36,9 +36,17 @@
 
 #include "kernel_abi.h"
 
+#ifndef ISIM_STREAM_TPL
+#define ISIM_STREAM_TPL 2
+#endif
+#ifndef ISIM_STREAM_WAVES
+#define ISIM_STREAM_WAVES 8  // waves per SIMD the draw-stream kernel is compiled for
+#endif
+
 namespace isim {
 namespace dev {
 
+constexpr int kStreamTPL = ISIM_STREAM_TPL;  // traces per lane in the draw-stream kernel
 constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
 constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 
@@ -587,86 +595,143 @@ __device__ __forceinline__ void philox_group(uint32_t t_lo, uint32_t t_hi, uint3
   x[3] = d;
 }
 
-template <bool MODEB, bool LDSC>
+// TPL traces per lane: the wave walks 64*TPL traces through one pass over the
+// stream, so the per-record scalar work (fetch, decode, counter adds) is
+// shared and each lane runs TPL independent Philox chains (ILP).
+template <bool MODEB, bool LDSC, int TPL>
 __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restrict__ stream, uint32_t n_groups,
                                             uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
                                             uint64_t n_traces, uint64_t base) {
   const uint32_t lane = lane_id();
   const bool lane0 = lane == 0;
-  const uint64_t idx = base + lane;
-  const bool valid = idx < n_traces;
-  const uint64_t t = trace_begin + idx;
-  const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32);
-  const uint32_t t_hi_u = rfl(t_hi);
-  const bool hi_uniform = ballot(t_hi != t_hi_u) == 0;  // the batch does not straddle 2^32
-  const uint64_t all = ballot(valid);
+  uint64_t idx[TPL], all[TPL];
+  uint32_t t_lo[TPL], t_hi[TPL], t_hi_u[TPL];
+  bool valid[TPL];
+  bool hi_uniform = true;
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    idx[u] = base + 64u * u + lane;
+    valid[u] = idx[u] < n_traces;
+    const uint64_t t = trace_begin + idx[u];
+    t_lo[u] = (uint32_t)t;
+    t_hi[u] = (uint32_t)(t >> 32);
+    t_hi_u[u] = rfl(t_hi[u]);
+    hi_uniform = hi_uniform && ballot(t_hi[u] != t_hi_u[u]) == 0;  // no straddle of 2^32
+    all[u] = ballot(valid[u]);
+  }
 
-  uint32_t errh = 0;
-  uint64_t root_st = 0;
+  uint32_t errh[TPL];
+  uint64_t root_st[TPL];
   // mode B: stack of open invocations; the top's running status in SGPRs
-  uint64_t top = 0;
+  uint64_t top[TPL];
   uint32_t top_slot = 0, depth = 0;
-  LaneStack<uint64_t> s_mask;
+  LaneStack<uint64_t> s_mask[TPL];
   LaneStack<uint32_t> s_slot;
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    errh[u] = 0;
+    root_st[u] = 0;
+    top[u] = 0;
+  }
 
-  auto node = [&](uint32_t thr, uint32_t meta, uint32_t xw) {
+  auto node = [&](uint32_t thr, uint32_t meta, const uint32_t (&xw)[TPL]) {
     const uint32_t slot = meta & 0xFFFFFFu;
-    const uint64_t own = (meta & 0x80000000u) ? all : (ballot(xw < thr) & all);
+    uint64_t own[TPL];
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) own[u] = (meta & 0x80000000u) ? all[u] : (ballot(xw[u] < thr) & all[u]);
     if constexpr (!MODEB) {
       // mode A: an invocation's status is its own error draw; padding
-      // records (thr 0, never always) draw nothing.
-      // (the root, record 0, is peeled off before the loop)
-      errh += lane_in(own) ? 1u : 0u;
-      if (own) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, popc(own), lane0);
+      // records (thr 0, never always) draw nothing.  The root (record 0)
+      // is peeled off before the loop.
+      uint64_t any = 0;
+      uint32_t n = 0;
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) {
+        errh[u] += lane_in(own[u]) ? 1u : 0u;
+        any |= own[u];
+        n += popc(own[u]);
+      }
+      if (any) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, n, lane0);
     } else {
       if (slot == kSlotPad) return;
       if (depth > 0) {
-        s_mask.put(depth - 1, top);
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) s_mask[u].put(depth - 1, top[u]);
         s_slot.put(depth - 1, top_slot);
       }
-      top = own;
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) top[u] = own[u];
       top_slot = slot;
       ++depth;
       for (uint32_t k = (meta >> 24) & 0x7Fu; k > 0; --k) {  // subtree closes
-        const uint64_t st = top;
-        errh += lane_in(st) ? 1u : 0u;
-        if (st && top_slot != kSlotRoot) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + top_slot, popc(st), lane0);
+        uint64_t any = 0;
+        uint32_t n = 0;
+        uint64_t st[TPL];
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) {
+          st[u] = top[u];
+          errh[u] += lane_in(st[u]) ? 1u : 0u;
+          any |= st[u];
+          n += popc(st[u]);
+        }
+        if (any && top_slot != kSlotRoot) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + top_slot, n, lane0);
         --depth;
         if (depth > 0) {
-          top = s_mask.get(depth - 1) | st;  // a callee's 500 fails the caller (mode B)
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) top[u] = s_mask[u].get(depth - 1) | st[u];  // mode B: 500 fails the caller
           top_slot = s_slot.get(depth - 1);
         } else {
-          root_st = st;
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) root_st[u] = st[u];
         }
       }
     }
   };
-  auto draws = [&](const Node4 &q, uint32_t g, uint32_t (&x)[4]) {
-    if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0)
-      philox_group(t_lo, t_hi, t_hi_u, hi_uniform, g, c.k0, c.k1, x);
+  auto draws = [&](const Node4 &q, uint32_t g, uint32_t (&x)[TPL][4]) {
+    if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0) {
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) philox_group(t_lo[u], t_hi[u], t_hi_u[u], hi_uniform, g, c.k0, c.k1, x[u]);
+    }
   };
   auto group = [&](const Node4 &q, uint32_t g) {
-    uint32_t x[4] = {0, 0, 0, 0};
+    uint32_t x[TPL][4];
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
     draws(q, g, x);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) node(q.n[j].thr, q.n[j].meta, x[j]);
+    for (int j = 0; j < 4; ++j) {
+      uint32_t xw[TPL];
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) xw[u] = x[u][j];
+      node(q.n[j].thr, q.n[j].meta, xw);
+    }
   };
 
   Node4 bufA = stream[0];
   Node4 bufB;
   if (n_groups > 1) bufB = stream[1];
   {  // group 0: record 0 is the entry invocation (the client request)
-    uint32_t x[4] = {0, 0, 0, 0};
-    draws(bufA, 0, x);
-    if constexpr (!MODEB) {
-      const uint64_t own = (bufA.n[0].meta & 0x80000000u) ? all : (ballot(x[0] < bufA.n[0].thr) & all);
-      errh += lane_in(own) ? 1u : 0u;
-      root_st = own;
-    } else {
-      node(bufA.n[0].thr, bufA.n[0].meta, x[0]);
-    }
+    uint32_t x[TPL][4];
 #pragma unroll
-    for (int j = 1; j < 4; ++j) node(bufA.n[j].thr, bufA.n[j].meta, x[j]);
+    for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
+    draws(bufA, 0, x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t xw[TPL];
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) xw[u] = x[u][j];
+      if (j == 0 && !MODEB) {
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) {
+          const uint64_t own =
+              (bufA.n[0].meta & 0x80000000u) ? all[u] : (ballot(xw[u] < bufA.n[0].thr) & all[u]);
+          errh[u] += lane_in(own) ? 1u : 0u;
+          root_st[u] = own;
+        }
+      } else {
+        node(bufA.n[j].thr, bufA.n[j].meta, xw);
+      }
+    }
   }
   uint32_t g = 1;
   while (g < n_groups) {
@@ -677,7 +742,8 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
     group(bufA, g);
     if (++g >= n_groups) break;
   }
-  finish_batch(c, idx, valid, all, t_static, n_nodes, root_st, errh);
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st[u], errh[u]);
 }
 
 // Executed-call counters of a static walk: every trace makes mult[slot] calls
@@ -692,7 +758,7 @@ __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_
 // KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream
 // LDSC: per-site counters in the workgroup LDS table (else global atomics)
 template <int KIND, bool MODEB, bool LDSC>
-__global__ void __launch_bounds__(kWgThreads, KIND == 4 ? 8 : 1)
+__global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
     isim_walk(const Ins *__restrict__ prog, isim_trace_rec *__restrict__ records, uint64_t *__restrict__ gstats,
               KParams kp) {
   using TT = typename std::conditional<KIND == 0 || KIND == 2, uint32_t, uint64_t>::type;
@@ -724,12 +790,14 @@ __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? 8 : 1)
   for (uint32_t i = threadIdx.x; i < zero_words; i += blockDim.x) z[i] = 0;
   __syncthreads();
 
-  const uint64_t n_batches = (kp.n_traces + 63) / 64;
+  constexpr uint64_t kBatch = KIND == 4 ? 64ull * kStreamTPL : 64ull;
+  const uint64_t n_batches = (kp.n_traces + kBatch - 1) / kBatch;
   const uint64_t stride = (uint64_t)gridDim.x * waves;
   for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
     if constexpr (KIND == 4)
-      walk_stream<MODEB, LDSC>(c, reinterpret_cast<const Node4 *>(prog), kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0,
-                         kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces, b * 64);
+      walk_stream<MODEB, LDSC, kStreamTPL>(c, reinterpret_cast<const Node4 *>(prog),
+                                           kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0, kp.n_nodes, kp.t_static,
+                                           kp.trace_begin, kp.n_traces, b * 64 * kStreamTPL);
     else if constexpr (STATIC) walk_static<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64);
     else walk_dynamic<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64, lstk, hstk);
   }
@@ -774,5 +842,6 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters) {
 }
 
 void *stream_calls_kernel() { return (void *)&dev::isim_stream_calls; }
+uint32_t stream_traces_per_wave() { return 64u * (uint32_t)dev::kStreamTPL; }
 
 }  // namespace isim
