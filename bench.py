@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--mode", default="A", choices=["A", "B"])
     ap.add_argument("--no-records", action="store_true")
+    ap.add_argument("--no-svc-dur", action="store_true",
+                    help="dynamic walks: skip the per-service duration histograms")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-traces", type=int, default=0, help="cpu_baseline sample size (0 = auto)")
     return ap.parse_args()
@@ -91,6 +93,22 @@ def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
             "hop_visits_per_s": float(st[2]) / dt}
 
 
+def compute_roofline(stream: bool, info, B: int, kern_ms: float):
+    """The draw-stream kernel is bound by integer VALU, not HBM: one
+    Philox4x32-10 block per lane per group of 4 invocations.  Peak = the
+    measured Philox block rate of tools/philox_peak.hip on MI355X
+    (profiles/philox_peak.json)."""
+    path = os.path.join(ROOT, "profiles", "philox_peak.json")
+    if not stream or not os.path.exists(path):
+        return None
+    peak = json.load(open(path))["philox_blocks_per_s"]
+    blocks = B * -(-info.hops_upper // 4)
+    achieved = blocks / (kern_ms * 1e-3)
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Philox4x32-10 blocks/s",
+            "frac": achieved / peak, "per_launch": blocks,
+            "peak_source": "profiles/philox_peak.json (tools/philox_peak.hip)"}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -110,7 +128,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     json_text, desc = build_graph(args.config)
-    params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A)
+    params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A,
+                            flags=isim.native.FLAG_NO_SVC_DUR if args.no_svc_dur else 0)
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
@@ -159,7 +178,10 @@ def main():
     hops_per_trace = folded["sum_hops"] / total
 
     # algorithmic bytes of one launch: 16 B records per trace + program read + stats written
-    alg_bytes = B * (0 if args.no_records else 16) + info.program_len * 32 + info.stats_words * 8
+    # (the draw stream is 8 B per invocation, padded to groups of 4; the interpreter 32 B per instruction)
+    stream = launch["kernel_kind"] == 4
+    prog_bytes = (-(-info.hops_upper // 4) * 4 * 8 + info.n_slots * 4) if stream else info.program_len * 32
+    alg_bytes = B * (0 if args.no_records else 16) + prog_bytes + info.stats_words * 8
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -193,6 +215,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+        "compute_roofline": compute_roofline(stream, info, B, kern_ms),
         "hop_visits_per_s": value * hops_per_trace,
         "n_500_frac": folded["n_500"] / total,
     }

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 1
+#define ISIM_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -83,7 +83,8 @@ typedef struct {
 } isim_params;
 
 /* isim_params.flags */
-#define ISIM_FLAG_NO_STREAM 1u /* run static walks on the interpreter kernel instead of the draw stream */
+#define ISIM_FLAG_NO_STREAM 1u  /* run static walks on the interpreter kernel instead of the draw stream */
+#define ISIM_FLAG_NO_SVC_DUR 2u /* dynamic walks: do not record per-service invocation durations */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -107,6 +108,15 @@ typedef struct {
 #define ISIM_N_LOG2 64
 #define ISIM_ST_SITES (ISIM_ST_LOG2 + 2 * ISIM_N_LOG2) /* [2][n_slots]: executed calls, then callee 500s,
                                                           per reachable call site slot */
+/* Per-service duration table (service_request_duration_seconds and its _sum,
+ * prometheus/handler.go:55-69,101-106), one row of ISIM_SVC_DUR_WORDS per
+ * reachable service: [code 200|500][33] bucket counts, then the two duration
+ * sums in ns.  Present in the stats buffer only when info.svc_dur_rows > 0
+ * (dynamic walks); for static walks every invocation of a service lasts the
+ * same T(s) and isim_stats_fold_durations derives the table from the
+ * counters. */
+#define ISIM_SVC_DUR_WORDS (2 * ISIM_N_PROM + 2)
+#define ISIM_ST_SVC_DUR(n_slots) (ISIM_ST_SITES + 2 * (uint64_t)(n_slots))
 
 typedef struct {
   int32_t n_services;        /* services in the graph */
@@ -120,6 +130,8 @@ typedef struct {
   uint64_t max_latency_ns;   /* static upper bound of any trace's latency */
   uint64_t hops_upper;       /* static upper bound of invocations per trace */
   uint64_t stats_words;      /* u64 words of the stats buffer */
+  int32_t svc_dur_rows;      /* rows of the device duration table (0: derived on the host) */
+  int32_t n_reachable;       /* services reachable from the entry */
 } isim_handler_info;
 
 /* Launch configuration chosen for a device (filled on first use of that device). */
@@ -129,7 +141,7 @@ typedef struct {
   int32_t lds_counters;      /* 1: per-site counters in LDS; 0: global atomics */
   int32_t blocks_per_cu;     /* resident workgroups per CU (occupancy query) */
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
-  int32_t kernel_kind;       /* 0/1 static u32/u64 time, 2/3 dynamic u32/u64 */
+  int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream */
 } isim_launch_info;
 
 ISIM_API const char *isim_last_error(void);
@@ -182,6 +194,14 @@ ISIM_API int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint6
  * Any output may be NULL. */
 ISIM_API int isim_stats_fold(const isim_handler *h, const uint64_t *stats, uint64_t *svc_calls,
                     uint64_t *svc_errs, uint64_t *site_calls);
+
+/* Per-service invocation-duration histograms (RecordResponseSent's duration
+ * observation, prometheus/handler.go:101-106, made at handler.go:56-58):
+ * svc_dur[n_services][ISIM_SVC_DUR_WORDS] = per service [code][33] bucket
+ * counts (non-cumulative; code 0 = 200, 1 = 500) then the [code] sums in ns.
+ * ISIM_EINVAL when the handler was created with ISIM_FLAG_NO_SVC_DUR for a
+ * dynamic walk. */
+ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *stats, uint64_t *svc_dur);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/isim.h"
 #include "gounits.h"
@@ -35,6 +36,7 @@ int fail(int code, const std::string &msg) {
 struct DevState {
   void *d_prog = nullptr;  // Ins[] (interpreters) or Node[] (draw stream)
   uint32_t *d_mult = nullptr;  // draw stream: per-slot call multiplicity
+  uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
   void *kernel = nullptr;
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
@@ -61,6 +63,7 @@ struct isim_handler {
       if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
         (void)hipFree(kv.second.d_prog);
         (void)hipFree(kv.second.d_mult);
+        (void)hipFree(kv.second.d_dur);
         (void)hipSetDevice(cur);
       }
     }
@@ -68,6 +71,16 @@ struct isim_handler {
 };
 
 namespace {
+
+// Rows of the device per-service duration table (dynamic walks only).
+uint64_t svc_dur_rows(const isim_handler *h) {
+  if (h->prog.static_walk || (h->params.flags & ISIM_FLAG_NO_SVC_DUR)) return 0;
+  return h->prog.row_svc.size();
+}
+
+uint64_t stats_words(const isim_handler *h) {
+  return ISIM_ST_SVC_DUR(h->prog.n_slots) + (uint64_t)ISIM_SVC_DUR_WORDS * svc_dur_rows(h);
+}
 
 // LDS layout of the walk kernel for a given workgroup size (walk.hip).
 uint32_t lds_need(const isim::Program &p, uint32_t waves, bool counters) {
@@ -130,6 +143,10 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
     HIPCHK(hipMalloc(&st.d_mult, p.stream_mult.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_mult, p.stream_mult.data(), p.stream_mult.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
+  }
+  if (svc_dur_rows(h) && p.n_slots > 0) {
+    HIPCHK(hipMalloc(&st.d_dur, p.slot_dur.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(st.d_dur, p.slot_dur.data(), p.slot_dur.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   }
   auto res = h->dev.emplace(device, st);
   out = &res.first->second;
@@ -241,7 +258,9 @@ int isim_handler_info_get(const isim_handler *h, isim_handler_info *out) {
   out->program_len = (int32_t)p.code.size();
   out->max_latency_ns = p.max_latency;
   out->hops_upper = p.hops_upper;
-  out->stats_words = ISIM_ST_SITES + 2ull * (uint64_t)p.n_slots;
+  out->stats_words = stats_words(h);
+  out->svc_dur_rows = (int32_t)svc_dur_rows(h);
+  out->n_reachable = (int32_t)p.row_svc.size();
   return ISIM_OK;
 }
 
@@ -290,13 +309,16 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   kp.lds_counters = st->lds_counters;
   kp.n_nodes = h->prog.stream_nodes;
   kp.t_static = h->prog.max_latency;
+  kp.svc_dur = svc_dur_rows(h) ? 1u : 0u;
+  kp.root_dur = h->prog.root_dur;
   const uint64_t per_wave = st->kind == 4 ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);
   const void *prog = st->d_prog;
-  void *args[] = {&prog, &d_records, &d_stats, &kp};
+  const uint32_t *dur = st->d_dur;
+  void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
   HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
                          (hipStream_t)hip_stream));
   if (st->kind == 4 && h->prog.n_slots > 0) {
@@ -315,7 +337,7 @@ int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint64_t n_tra
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   HIPCHK(hipSetDevice(device));
-  const uint64_t words = ISIM_ST_SITES + 2ull * (uint64_t)h->prog.n_slots;
+  const uint64_t words = stats_words(h);
   uint64_t *d_stats = nullptr;
   isim_trace_rec *d_rec = nullptr;
   int rc = ISIM_OK;
@@ -367,6 +389,33 @@ int isim_stats_fold(const isim_handler *h, const uint64_t *stats, uint64_t *svc_
   // the client request into the entry is not a call site
   if (svc_calls) svc_calls[p.entry] += stats[ISIM_ST_N_TRACES];
   if (svc_errs) svc_errs[p.entry] += stats[ISIM_ST_N_500];
+  return ISIM_OK;
+}
+
+int isim_stats_fold_durations(const isim_handler *h, const uint64_t *stats, uint64_t *svc_dur) {
+  if (!h || !stats || !svc_dur) return fail(ISIM_EINVAL, "null argument");
+  const isim::Program &p = h->prog;
+  constexpr uint32_t W = ISIM_SVC_DUR_WORDS;
+  std::fill(svc_dur, svc_dur + (size_t)p.n_services * W, 0);
+  if (!p.static_walk) {
+    if (!svc_dur_rows(h)) return fail(ISIM_EINVAL, "per-service durations disabled (ISIM_FLAG_NO_SVC_DUR)");
+    const uint64_t *tab = stats + ISIM_ST_SVC_DUR(p.n_slots);
+    for (size_t r = 0; r < p.row_svc.size(); ++r)
+      std::copy(tab + r * W, tab + (r + 1) * W, svc_dur + (size_t)p.row_svc[r] * W);
+    return ISIM_OK;
+  }
+  // static walk: every invocation of s lasts T(s); split by code with the counters
+  std::vector<uint64_t> calls(p.n_services, 0), errs(p.n_services, 0);
+  isim_stats_fold(h, stats, calls.data(), errs.data(), nullptr);
+  for (int32_t s : p.row_svc) {
+    const uint64_t T = p.svc_time[s];
+    const uint32_t b = isim::prom_bucket_ns(T);
+    uint64_t *row = svc_dur + (size_t)s * W;
+    row[b] = calls[s] - errs[s];
+    row[ISIM_N_PROM + b] = errs[s];
+    row[2 * ISIM_N_PROM] = T * (calls[s] - errs[s]);
+    row[2 * ISIM_N_PROM + 1] = T * errs[s];
+  }
   return ISIM_OK;
 }
 

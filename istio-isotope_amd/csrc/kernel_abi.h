@@ -48,6 +48,9 @@ constexpr uint32_t kSlotRoot = 0xFFFFFFu;  // the entry invocation (no call site
 constexpr uint32_t kSlotPad = 0xFFFFFEu;   // padding to a multiple of 4 records
 constexpr uint32_t kMaxStreamNodes = 1u << 24;
 
+// Per-service duration table word: row (bits 0-23) | bucket of a leaf callee (24-31).
+constexpr uint32_t kDurRowMask = 0xFFFFFFu;
+
 // Scalar kernel arguments (the program, records and stats pointers are
 // separate __restrict__ kernel arguments so program fetches become s_load).
 struct KParams {
@@ -59,6 +62,8 @@ struct KParams {
   uint32_t lds_counters;    // 1: per-site counters in the LDS table
   uint32_t n_nodes;         // stream kernel: invocations per trace
   uint64_t t_static;        // stream kernel: the (trace-invariant) latency
+  uint32_t svc_dur;         // dynamic walks: 1 = record per-service durations
+  uint32_t root_dur;        // the entry's duration-table word (row | leaf bucket << 24)
 };
 
 constexpr uint32_t kWgThreads = 1024;                 // max workgroup size (launch bound)

@@ -29,6 +29,14 @@ uint64_t sleep_ns(int64_t d) { return d > 0 ? (uint64_t)d : 0; }
 
 }  // namespace
 
+uint32_t prom_bucket_ns(uint64_t t) {
+  static const uint64_t edges_ms[32] = {7,  8,  9,  10, 11,  12,  14,  16,  18,  20,  25,  30,  35,  40,  45,  50,
+                                        60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
+  for (uint32_t i = 0; i < 32; ++i)
+    if (t <= edges_ms[i] * 1000000ull) return i;
+  return 32;
+}
+
 int32_t service_index(const ServiceGraph &g, const std::string &name) {
   for (size_t i = 0; i < g.services.size(); ++i)
     if (g.services[i].name == name) return (int32_t)i;
@@ -207,6 +215,22 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     }
   }
   out.n_slots = (int32_t)out.slot_site.size();
+  // per-service duration table rows: reachable services in preorder (entry = row 0)
+  if (pre.size() > (size_t)kDurRowMask) {
+    err = "more than 2^24 services reachable from the entry";
+    return ISIM_ERANGE;
+  }
+  out.svc_time = tmax;
+  out.svc_row.assign(n, -1);
+  for (int32_t s : pre) {
+    out.svc_row[s] = (int32_t)out.row_svc.size();
+    out.row_svc.push_back(s);
+  }
+  auto dur_word = [&](int32_t callee) -> uint32_t {
+    return (uint32_t)out.svc_row[callee] | ((leaf[callee] ? prom_bucket_ns(tmax[callee]) : 0u) << 24);
+  };
+  for (int32_t sl = 0; sl < out.n_slots; ++sl) out.slot_dur.push_back(dur_word(out.slot_callee[sl]));
+  out.root_dur = dur_word(entry);
 
   // ---- emit
   auto err_flags = [&](int32_t callee) -> uint32_t {

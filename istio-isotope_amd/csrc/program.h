@@ -35,7 +35,17 @@ struct Program {
   std::vector<Node> stream;                     // padded to a multiple of 4
   uint32_t stream_nodes = 0;                    // invocations per trace (unpadded)
   std::vector<uint32_t> stream_mult;            // per slot: calls through it per trace
+  // per-service invocation durations (RecordResponseSent, prometheus/handler.go:101-106)
+  std::vector<uint64_t> svc_time;   // per service: T_max; the exact duration when static_walk
+  std::vector<int32_t> svc_row;     // per service: row in the duration table (-1: unreachable)
+  std::vector<int32_t> row_svc;     // per row: service (rows = reachable services, preorder)
+  std::vector<uint32_t> slot_dur;   // per slot: callee row | leaf-callee bucket << 24
+  uint32_t root_dur = 0;            // the entry: row 0 | bucket << 24 when the entry is a leaf
 };
+
+// Bucket of an invocation duration on the service_request_duration_seconds
+// edges (prometheus/handler.go:26-31, `le`): 0..31, 32 = +Inf.
+uint32_t prom_bucket_ns(uint64_t t);
 
 // Returns an isim_status; on error `err` holds the message.
 int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, Program &out,

@@ -149,6 +149,17 @@ __device__ __forceinline__ void hist_add(uint32_t *h, uint32_t key, uint64_t lan
   }
 }
 
+// Wave-aggregated global histogram add (u64 words): one atomic per distinct key.
+__device__ __forceinline__ void hist_add_global(uint64_t *h, uint32_t key, uint64_t lanes) {
+  while (lanes) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(lanes);
+    const uint32_t k = rdl(key, leader);
+    const uint64_t m = ballot(key == k) & lanes;
+    if (lane_id() == leader) atomicAdd((unsigned long long *)(h + k), (unsigned long long)popc(m));
+    lanes &= ~m;
+  }
+}
+
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -172,6 +183,9 @@ struct Ctx {
   const Ins *__restrict__ prog;
   isim_trace_rec *__restrict__ records;
   uint64_t *__restrict__ gstats;
+  const uint32_t *__restrict__ dur;  // dynamic walks: per-slot duration-table words, or null
+  uint64_t *svc_tab;                 // dynamic walks: per-service duration table (HBM), or null
+  uint32_t root_dur;
   uint32_t *cnt;   // LDS per-site counters or null
   uint32_t *hist;  // LDS histograms
   WgAcc *acc;      // LDS accumulators
@@ -372,6 +386,37 @@ __device__ __forceinline__ void walk_static(const Ctx &c, uint64_t trace_begin, 
 // ======================================================================
 // DYNAMIC walk: per-lane time (TT) and hop ids, LDS frame stack.
 // ======================================================================
+// Per-service invocation durations (RecordResponseSent, srv/prometheus/
+// handler.go:101-106): row = [code][33] bucket counts + [code] sums (ns).
+// A leaf callee's duration is its fixed latency (bucket precomputed in the
+// table word); a RET has per-lane durations.
+__device__ __forceinline__ void leaf_duration(const Ctx &c, uint32_t w, uint64_t T, uint64_t e, uint64_t st) {
+  if (lane_id() != 0) return;
+  unsigned long long *row = (unsigned long long *)(c.svc_tab + (uint64_t)(w & kDurRowMask) * ISIM_SVC_DUR_WORDS);
+  const uint32_t b = w >> 24;
+  const uint32_t n5 = popc(st), n2 = popc(e) - n5;
+  if (n2) {
+    atomicAdd(row + b, (unsigned long long)n2);
+    atomicAdd(row + 2 * ISIM_N_PROM, (unsigned long long)(T * n2));
+  }
+  if (n5) {
+    atomicAdd(row + ISIM_N_PROM + b, (unsigned long long)n5);
+    atomicAdd(row + 2 * ISIM_N_PROM + 1, (unsigned long long)(T * n5));
+  }
+}
+
+__device__ __forceinline__ void ret_duration(const Ctx &c, uint32_t row_i, uint64_t T, uint64_t e, uint64_t st) {
+  uint64_t *row = c.svc_tab + (uint64_t)row_i * ISIM_SVC_DUR_WORDS;
+  const bool is5 = lane_in(st);
+  hist_add_global(row, (is5 ? ISIM_N_PROM : 0u) + prom_bucket(T), e);
+  const uint64_t s2 = wave_sum64(lane_in(e & ~st) ? T : 0);
+  const uint64_t s5 = st ? wave_sum64(is5 ? T : 0) : 0;
+  if (lane_id() == 0) {
+    if (s2) atomicAdd((unsigned long long *)(row + 2 * ISIM_N_PROM), (unsigned long long)s2);
+    if (s5) atomicAdd((unsigned long long *)(row + 2 * ISIM_N_PROM + 1), (unsigned long long)s5);
+  }
+}
+
 template <bool MODEB, typename TT>
 __device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin, uint64_t n_traces,
                                              uint64_t base, TT *__restrict__ lstk, uint32_t *__restrict__ hstk) {
@@ -483,6 +528,8 @@ __device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin,
         if (op == OP_LEAF) {
           if (!(flags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cur.slot, popc(st));
           if (lane_in(st)) ++errh;
+          if (c.svc_tab) leaf_duration(c, (flags & F_ROOT) ? c.root_dur : c.dur[cur.slot],
+                                       u64of(cur.b_lo, cur.b_hi), e, st);
           fold(flags, H, (TT)u64of(cur.b_lo, cur.b_hi), e, st);
         } else {
           f_ret.put(depth, pc + 1);
@@ -521,6 +568,8 @@ __device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin,
         const uint32_t cflags = (cin.opf >> 8) & 0xFFu;
         if (!(cflags & F_ROOT)) count(c.gstats, c.cnt, c.n_slots + cin.slot, popc(st));
         if (lane_in(st)) ++errh;
+        if (c.svc_tab) ret_duration(c, ((cflags & F_ROOT) ? c.root_dur : c.dur[cin.slot]) & kDurRowMask,
+                                    (uint64_t)T, e, st);
         fold(cflags, u64of(cin.a_lo, cin.a_hi), T, e, st);
         break;
       }
@@ -760,7 +809,7 @@ __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_
 template <int KIND, bool MODEB, bool LDSC>
 __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
     isim_walk(const Ins *__restrict__ prog, isim_trace_rec *__restrict__ records, uint64_t *__restrict__ gstats,
-              KParams kp) {
+              const uint32_t *__restrict__ dur, KParams kp) {
   using TT = typename std::conditional<KIND == 0 || KIND == 2, uint32_t, uint64_t>::type;
   constexpr bool STATIC = KIND < 2 || KIND == 4;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -768,6 +817,9 @@ __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
   c.prog = prog;
   c.records = records;
   c.gstats = gstats;
+  c.dur = dur;
+  c.svc_tab = kp.svc_dur ? gstats + ISIM_ST_SVC_DUR(kp.n_slots) : nullptr;
+  c.root_dur = kp.root_dur;
   c.acc = reinterpret_cast<WgAcc *>(lds);
   c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
   c.cnt = LDSC ? c.hist + kHistWords : nullptr;

@@ -22,7 +22,9 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
+ABI_VERSION = 2  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
+FLAG_NO_SVC_DUR = 2
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
@@ -31,6 +33,7 @@ N_PROM, N_LOG2 = 33, 64
 ST_PROM = 8
 ST_LOG2 = ST_PROM + 2 * N_PROM
 ST_SITES = ST_LOG2 + 2 * N_LOG2
+SVC_DUR_WORDS = 2 * N_PROM + 2
 
 
 class IsimError(RuntimeError):
@@ -56,7 +59,7 @@ class HandlerInfo(C.Structure):
                 ("entry", C.c_int32), ("max_depth", C.c_int32), ("static_walk", C.c_int32),
                 ("time_bits", C.c_int32), ("program_len", C.c_int32),
                 ("max_latency_ns", C.c_uint64), ("hops_upper", C.c_uint64),
-                ("stats_words", C.c_uint64)]
+                ("stats_words", C.c_uint64), ("svc_dur_rows", C.c_int32), ("n_reachable", C.c_int32)]
 
 
 class LaunchInfo(C.Structure):
@@ -85,6 +88,7 @@ SIGNATURES = {
     "isim_serve_device": (C.c_int, [_VP, C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
     "isim_serve": (C.c_int, [_VP, C.c_int, C.c_uint64, C.c_uint64, _VP, _VP]),
     "isim_stats_fold": (C.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    "isim_stats_fold_durations": (C.c_int, [_VP, _VP, _VP]),
 }
 
 _lib = None
@@ -106,7 +110,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.isim_abi_version() != 1:
+    if lib.isim_abi_version() != ABI_VERSION:
         raise ImportError("libisim ABI version mismatch")
     _lib = lib
     return lib

@@ -103,6 +103,11 @@ class Handler:
         d["svc_calls"] = svc_calls[:n]
         d["svc_errs"] = svc_errs[:n]
         d["site_calls"] = site_calls[:m]
+        dur = np.zeros((max(1, n), native.SVC_DUR_WORDS), np.uint64)
+        rc = native.load().isim_stats_fold_durations(self._h, stats.ctypes.data, dur.ctypes.data)
+        # per service: [code][33] duration bucket counts, then [code] sums (ns);
+        # absent when a dynamic walk was created with FLAG_NO_SVC_DUR
+        d["svc_dur"] = dur[:n] if rc == 0 else None
         return d
 
 

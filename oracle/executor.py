@@ -22,6 +22,7 @@ ST_HDR = 8
 ST_PROM = ST_HDR
 ST_LOG2 = ST_PROM + 2 * N_PROM
 ST_SVC = ST_LOG2 + 2 * N_LOG2
+SVC_DUR_WORDS = 2 * N_PROM + 2
 
 
 class _Cmd(C.Structure):
@@ -162,6 +163,10 @@ def split_stats(stats: np.ndarray, n_services: int, n_sites: int) -> dict:
         "svc_calls": stats[ST_SVC:ST_SVC + n_services],
         "svc_errs": stats[ST_SVC + n_services:ST_SVC + 2 * n_services],
         "site_calls": stats[ST_SVC + 2 * n_services:ST_SVC + 2 * n_services + n_sites],
+        # [n_services][68]: duration buckets [code][33] then sums [code] (ns)
+        "svc_dur": stats[ST_SVC + 2 * n_services + n_sites:
+                         ST_SVC + 2 * n_services + n_sites + SVC_DUR_WORDS * n_services].reshape(n_services,
+                                                                                               SVC_DUR_WORDS),
     }
 
 

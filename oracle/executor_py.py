@@ -114,6 +114,13 @@ class Stats:
         self.svc_calls = [0] * n
         self.svc_errs = [0] * n
         self.site_calls = [0] * len(sg.sites)
+        # RecordResponseSent (prometheus/handler.go:101-106): per service, the
+        # invocation's own duration on the duration buckets [code][33] + sums
+        self.svc_dur = [[[0] * N_PROM for _ in range(2)] for _ in range(n)]
+        self.svc_dur_sum = [[0, 0] for _ in range(n)]
+        # optional per-event log, in the order the reference process would
+        # record them: ("recv", svc) / ("sent", caller, site) / ("resp", svc, T, err)
+        self.events = None
         self.lat_prom = [[0] * N_PROM for _ in range(2)]
         self.lat_log2 = [[0] * N_LOG2 for _ in range(2)]
         self.n_traces = 0
@@ -147,6 +154,8 @@ def _invoke(sg: SimGraph, p: SimParams, st: Stats, tr: _Trace, s: int):
     hop = tr.next_hop
     tr.next_hop += 1
     st.svc_calls[s] += 1                      # RecordRequestReceived (handler.go:43)
+    if st.events is not None:
+        st.events.append(("recv", s))
     thr = sg.thr[s]
     T = 0
     failed = False
@@ -161,6 +170,8 @@ def _invoke(sg: SimGraph, p: SimParams, st: Stats, tr: _Trace, s: int):
                 continue
             tc, e = _invoke(sg, p, st, tr, sg.sites[site][1])
             st.site_calls[site] += 1          # RecordRequestSent (executable.go:124-129)
+            if st.events is not None:
+                st.events.append(("sent", s, site))
             T += sg.hop_cost(site, p) + tc
             if p.error_mode == MODE_B and e:
                 failed = True
@@ -178,6 +189,8 @@ def _invoke(sg: SimGraph, p: SimParams, st: Stats, tr: _Trace, s: int):
                     continue
                 tc, e = _invoke(sg, p, st, tr, sg.sites[site][1])
                 st.site_calls[site] += 1
+                if st.events is not None:
+                    st.events.append(("sent", s, site))
                 m = max(m, sg.hop_cost(site, p) + tc)
                 if p.error_mode == MODE_B and e:
                     cerr = True
@@ -192,13 +205,20 @@ def _invoke(sg: SimGraph, p: SimParams, st: Stats, tr: _Trace, s: int):
     if err:
         st.svc_errs[s] += 1
         tr.err_hops += 1
+    st.svc_dur[s][int(err)][prom_bucket(T)] += 1   # handler.go:56-58
+    if st.events is not None:
+        st.events.append(("resp", s, T, int(err)))
+    st.svc_dur_sum[s][int(err)] += T
     return T, err
 
 
-def run(sg: SimGraph, p: SimParams, entry: int, trace_begin: int, n_traces: int):
+def run(sg: SimGraph, p: SimParams, entry: int, trace_begin: int, n_traces: int, events: bool = False):
     """Simulate traces [trace_begin, trace_begin + n_traces). Returns
-    (records, stats); a record is (latency_ns, hops, status500, err_hops)."""
+    (records, stats); a record is (latency_ns, hops, status500, err_hops).
+    events=True also logs every Record* call into stats.events."""
     st = Stats(sg)
+    if events:
+        st.events = []
     recs = []
     for i in range(n_traces):
         tr = _Trace(trace_begin + i)

@@ -60,6 +60,10 @@ typedef struct {
  * [8 .. 8+2*33)    latency prometheus buckets [status][33]
  * [74 .. 74+2*64)  latency log2 buckets [status][64]
  * [202 .. +n_services) svc_calls, then svc_errs [n_services], then site_calls [n_sites]
+ * then svc_dur [n_services][68]: per service, invocation durations on the
+ *   Prometheus duration buckets [code 200|500][33] + duration sums [2] in ns
+ *   (RecordResponseSent, prometheus/handler.go:101-106, observed at
+ *   handler.go:56-58 with the invocation's own duration)
  */
 #define ST_HDR 8
 #define N_PROM 33
@@ -67,6 +71,7 @@ typedef struct {
 #define ST_PROM ST_HDR
 #define ST_LOG2 (ST_PROM + 2 * N_PROM)
 #define ST_SVC (ST_LOG2 + 2 * N_LOG2)
+#define SVC_DUR_WORDS (2 * N_PROM + 2)
 
 static const uint64_t PROM_EDGES_NS[32] = {
     7000000ull, 8000000ull, 9000000ull, 10000000ull, 11000000ull, 12000000ull, 14000000ull,
@@ -74,6 +79,12 @@ static const uint64_t PROM_EDGES_NS[32] = {
     45000000ull, 50000000ull, 60000000ull, 70000000ull, 80000000ull, 90000000ull, 100000000ull,
     120000000ull, 140000000ull, 160000000ull, 180000000ull, 200000000ull, 250000000ull,
     300000000ull, 350000000ull, 400000000ull, 450000000ull, 500000000ull};
+
+static int prom_bucket(uint64_t T) {
+    for (int j = 0; j < 32; ++j)
+        if (T <= PROM_EDGES_NS[j]) return j;
+    return 32;
+}
 
 static void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
     for (int r = 0; r < 10; ++r) {
@@ -179,12 +190,16 @@ static uint64_t invoke(tstate *s, int32_t svc, int *err_out) {
         s->st[ST_SVC + g->n_services + svc] += 1;
         s->err_hops += 1;
     }
+    uint64_t *dur = s->st + ST_SVC + 2 * (uint64_t)g->n_services + (uint64_t)g->n_sites +
+                    (uint64_t)svc * SVC_DUR_WORDS;
+    dur[err * N_PROM + prom_bucket(T)] += 1;
+    dur[2 * N_PROM + err] += T;
     *err_out = err;
     return T;
 }
 
 uint64_t isim_oracle_stats_words(int32_t n_services, int32_t n_sites) {
-    return ST_SVC + 2 * (uint64_t)n_services + (uint64_t)n_sites;
+    return ST_SVC + 2 * (uint64_t)n_services + (uint64_t)n_sites + (uint64_t)n_services * SVC_DUR_WORDS;
 }
 
 /* records: 16 B per trace {u64 latency, u32 hops, u32 (status500<<31)|err_hops}
@@ -236,10 +251,7 @@ int isim_oracle_run(const ograph *g, const oparams *p, uint64_t trace_begin, uin
             st[4] += (uint64_t)e;
             if (T < st[5]) st[5] = T;
             if (T > st[6]) st[6] = T;
-            int b = 32;
-            for (int j = 0; j < 32; ++j)
-                if (T <= PROM_EDGES_NS[j]) { b = j; break; }
-            st[ST_PROM + e * N_PROM + b] += 1;
+            st[ST_PROM + e * N_PROM + prom_bucket(T)] += 1;
             int l = T == 0 ? 0 : 64 - __builtin_clzll(T);
             st[ST_LOG2 + e * N_LOG2 + l] += 1;
         }

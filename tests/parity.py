@@ -65,6 +65,12 @@ def assert_stats_equal(f: dict, o: dict):
         assert f["min_latency"] == o["min_latency"], (f["min_latency"], o["min_latency"])
     for k in ("lat_prom", "lat_log2", "svc_calls", "svc_errs", "site_calls"):
         assert np.array_equal(np.asarray(f[k], np.uint64), np.asarray(o[k], np.uint64)), k
+    if f.get("svc_dur") is not None:
+        fd, od = np.asarray(f["svc_dur"], np.uint64), np.asarray(o["svc_dur"], np.uint64)
+        bad = np.argwhere(fd != od)
+        assert bad.size == 0, f"svc_dur differs at (service, word) {bad[:4].tolist()}: gpu {fd[tuple(bad[0])]} " \
+                              f"oracle {od[tuple(bad[0])]}"
+
 
 
 def with_defaults(json_text: str, **defaults) -> str:

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert native.load().isim_abi_version() == 1
+    assert native.load().isim_abi_version() == 2
 
 
 def _handler(doc, entry=None, **kw):
@@ -136,3 +136,36 @@ def test_stats_fold_host_only():
     assert dict(zip(names, f["svc_calls"].tolist())) == {"a": 20, "b": 20, "c": 10, "d": 10}
     assert int(f["svc_errs"][names.index("d")]) == 2
     assert f["site_calls"].tolist() == [10, 10, 10, 10, 10]
+
+
+def test_stats_fold_durations_static_derivation():
+    # static walk: every invocation of a service lasts T(s); the fold splits
+    # calls by code from the counters (no device table)
+    h = isim.handler_from_service_graph_yaml(os.path.join(TOPOLOGIES, "canonical.yaml"))
+    import numpy as np
+    assert h.info.svc_dur_rows == 0 and h.info.n_reachable == 4
+    st = h.new_stats()
+    st[native.ST_N_TRACES] = 10
+    st[native.ST_N_500] = 2
+    st[native.ST_SITES:native.ST_SITES + 5] = 10
+    st[native.ST_SITES + 5:native.ST_SITES + 10] = [1, 0, 0, 3, 0]
+    f = h.fold(st)
+    names = [s.name for s in h.graph.services]
+    dur = f["svc_dur"]
+    d = dur[names.index("d")]
+    b = int(np.nonzero(d[:native.N_PROM])[0][0])
+    # d's T = 4 hops of 250163 ns (1.0007 ms) -> the first bucket (<= 7 ms)
+    assert b == 0 and int(d[b]) == 8 and int(d[native.N_PROM + b]) == 2
+    assert int(d[2 * native.N_PROM]) == 8 * 250163 * 4 and int(d[2 * native.N_PROM + 1]) == 2 * 250163 * 4
+    assert dur[:, :2 * native.N_PROM].sum(axis=1).tolist() == f["svc_calls"].tolist()
+
+
+def test_dynamic_walk_has_duration_table():
+    doc = {"services": [{"name": "a", "isEntrypoint": True, "script": [{"call": {"service": "b", "probability": 50}}]},
+                        {"name": "b"}, {"name": "unreachable"}]}
+    h = _handler(doc)
+    assert h.info.static_walk == 0 and h.info.svc_dur_rows == 2 and h.info.n_reachable == 2
+    assert h.stats_words == native.ST_SITES + 2 * 1 + 2 * native.SVC_DUR_WORDS
+    off = _handler(doc, flags=native.FLAG_NO_SVC_DUR)
+    assert off.info.svc_dur_rows == 0 and off.stats_words == native.ST_SITES + 2
+    assert off.fold(off.new_stats())["svc_dur"] is None

@@ -1,0 +1,110 @@
+"""Full-size GPU runs (BASELINE-scale batches) checked through size-independent
+properties, plus bit-exact windows sampled across the trace range and
+recomputed by the CPU oracle."""
+import numpy as np
+import pytest
+
+import isim
+from isim.generators import config2_topology, config3_topology, mesh_topology
+from isim.yamljson import obj_to_json
+
+from parity import Case, assert_records_equal, with_defaults
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_run(case: Case, begin: int, n: int):
+    import torch
+    h = case.handler
+    dev = torch.device("cuda", 0)
+    stats = torch.zeros(h.stats_words, dtype=torch.int64, device=dev)
+    recs = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    h.serve_device(begin, n, recs.data_ptr(), stats.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    r = recs.cpu().numpy().view(np.uint64)
+    rec = np.zeros(n, isim.REC_DTYPE)
+    rec["latency_ns"] = r[:, 0]
+    rec["hops"] = (r[:, 1] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    rec["status_err"] = (r[:, 1] >> np.uint64(32)).astype(np.uint32)
+    return rec, h.fold(stats.cpu().numpy().view(np.uint64))
+
+
+def _sampled_windows(case: Case, rec, begin, n, windows=8, width=256, seed=0):
+    rng = np.random.default_rng(seed)
+    starts = sorted(set([0, n - width] + list(rng.integers(0, n - width, windows))))
+    for s0 in starts:
+        orec, _ = case.cpu(begin + int(s0), width)
+        assert_records_equal(rec[s0:s0 + width], orec)
+
+
+def _common_properties(f, rec, n):
+    assert f["n_traces"] == n
+    assert f["sum_hops"] == int(rec["hops"].astype(np.uint64).sum())
+    assert f["sum_latency"] == int(rec["latency_ns"].astype(np.uint64).sum())
+    err = (rec["status_err"] & 0x7FFFFFFF).astype(np.uint64)
+    st500 = (rec["status_err"] >> 31).astype(np.uint64)
+    assert f["sum_err_hops"] == int(err.sum())
+    assert f["n_500"] == int(st500.sum())
+    assert int(f["lat_prom"].sum()) == n and int(f["lat_log2"].sum()) == n
+    assert int(f["lat_prom"][1].sum()) == f["n_500"]
+    assert f["min_latency"] == int(rec["latency_ns"].min()) and f["max_latency"] == int(rec["latency_ns"].max())
+    # every 500 response is one invocation's: services' 500s add up to err_hops
+    assert int(f["svc_errs"].sum()) == f["sum_err_hops"]
+    assert int(f["svc_calls"].sum()) == f["sum_hops"]
+
+
+def test_config3_full_batch():
+    """BASELINE config 3 graph, one full bench batch (2^22 traces) at a
+    trace offset beyond 2^32; mode A."""
+    c = Case(obj_to_json(config3_topology()))
+    n, begin = 1 << 22, (1 << 32) - (1 << 21)
+    rec, f = _device_run(c, begin, n)
+    info = c.handler.info
+    _common_properties(f, rec, n)
+    # static walk: every trace visits every service once, same latency
+    assert np.all(rec["hops"] == 10000)
+    assert np.all(rec["latency_ns"] == info.max_latency_ns)
+    assert np.all(f["svc_calls"] == n)
+    # per-service error frequencies match errorRate (binomial, 6 sigma)
+    p = np.array([s.error_rate for s in c.graph.services])
+    e = f["svc_errs"].astype(np.float64)
+    sigma = np.sqrt(n * p * (1 - p)) + 1.0
+    assert np.all(np.abs(e - n * p) < 6 * sigma)
+    _sampled_windows(c, rec, begin, n)
+
+
+def test_config3_mode_b_full_batch():
+    c = Case(obj_to_json(config3_topology()), None, isim.SimParams(error_mode=isim.MODE_B))
+    n = 1 << 21
+    rec, f = _device_run(c, 123, n)
+    _common_properties(f, rec, n)
+    # mode B: a failing invocation fails all its ancestors, so the entry's
+    # 500s are at least as frequent as any single service's
+    assert f["n_500"] >= int(f["svc_errs"].max())
+    _sampled_windows(c, rec, 123, n, windows=4)
+
+
+def test_config2_full_batch():
+    """BASELINE config 2 (tree 4x8, sequential) with a 0.1% errorRate."""
+    c = Case(with_defaults(obj_to_json(config2_topology()), errorRate=0.001))
+    n = 1 << 23
+    rec, f = _device_run(c, 0, n)
+    _common_properties(f, rec, n)
+    assert np.all(rec["hops"] == 585) and np.all(rec["latency_ns"] == c.handler.info.max_latency_ns)
+    _sampled_windows(c, rec, 0, n)
+
+
+def test_config4_mesh_full_batch():
+    """BASELINE config 4 graph (100k-service mesh, probability 30): dynamic
+    walk; hop counts vary per trace."""
+    c = Case(with_defaults(obj_to_json(mesh_topology()), errorRate=0.01))
+    assert not c.handler.info.static_walk
+    n = 1 << 21
+    rec, f = _device_run(c, 7, n)
+    _common_properties(f, rec, n)
+    hops = rec["hops"].astype(np.float64)
+    # E[hops] = sum_k 0.9^k over 8 layers (3 calls at probability 30 each)
+    expected = sum(0.9 ** k for k in range(8))
+    assert abs(hops.mean() - expected) < 0.05
+    _sampled_windows(c, rec, 7, n)

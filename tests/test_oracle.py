@@ -230,6 +230,15 @@ def test_python_vs_c_executor(j, mode, seed, begin):
     assert list(cs["svc_calls"]) == st_.svc_calls
     assert list(cs["svc_errs"]) == st_.svc_errs
     assert list(cs["site_calls"]) == st_.site_calls
+    dur = cs["svc_dur"]
+    assert dur[:, :2 * ex.N_PROM].reshape(-1, 2, ex.N_PROM).tolist() == st_.svc_dur
+    assert dur[:, 2 * ex.N_PROM:].tolist() == st_.svc_dur_sum
+    # the entry's own duration histogram is the end-to-end latency histogram
+    assert dur[0, :2 * ex.N_PROM].reshape(2, ex.N_PROM).tolist() == cs["lat_prom"].tolist()
+    assert int(dur[0, 2 * ex.N_PROM:].sum()) == cs["sum_latency"]
+    # one observation per invocation, split by code as the 500 counters
+    assert dur[:, ex.N_PROM:2 * ex.N_PROM].sum(axis=1).tolist() == list(cs["svc_errs"])
+    assert dur[:, :2 * ex.N_PROM].sum(axis=1).tolist() == list(cs["svc_calls"])
     assert cs["lat_prom"].tolist() == st_.lat_prom and cs["lat_log2"].tolist() == st_.lat_log2
     assert (cs["sum_latency"], cs["sum_hops"], cs["n_500"]) == (st_.sum_latency, st_.sum_hops, st_.n_500)
 

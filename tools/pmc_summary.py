@@ -1,0 +1,89 @@
+"""Summarise a rocprofv3 profile set of bench.py (produced by tools/profile.sh)
+into profiles/pmc_summary.json and copy the CSVs judged into profiles/<round>/.
+
+    python tools/pmc_summary.py gpurun_out/prof3 r01
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3): the
+FETCH_SIZE and WRITE_SIZE passes run separately; FETCH_SIZE (KiB) is doubled
+on gfx950 (it tallies 128-B streaming requests at 64 B), WRITE_SIZE is taken
+as-is.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "isim_walk"
+
+
+def counters(path):
+    agg = collections.defaultdict(list)
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        if KERNEL in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {"kernel": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "wg": int(r["Workgroup_Size"]),
+                    "vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]), "lds": int(r["LDS_Block_Size"]),
+                    "scratch": int(r["Scratch_Size"])}
+    return {k: sum(v) / len(v) for k, v in agg.items()}, meta
+
+
+def main(src, rnd):
+    dst = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(dst, exist_ok=True)
+    stats_rows = list(csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv"))))
+    walk = [r for r in stats_rows if KERNEL in r["Name"]][0]
+    shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "stats", "run_kernel_trace.csv"), os.path.join(dst, "kernel_trace.csv"))
+    for p in ("fetch", "write", "sq1", "sq2"):
+        shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
+    bench_line = [l for l in open(os.path.join(src, "stats.log")) if l.startswith("{")][-1]
+    with open(os.path.join(dst, "bench_under_rocprof.json"), "w") as f:
+        f.write(bench_line)
+    bench = json.loads(bench_line)
+    fetch, meta = counters(os.path.join(src, "fetch", "run_counter_collection.csv"))
+    write, _ = counters(os.path.join(src, "write", "run_counter_collection.csv"))
+    sq1, _ = counters(os.path.join(src, "sq1", "run_counter_collection.csv"))
+    sq2, _ = counters(os.path.join(src, "sq2", "run_counter_collection.csv"))
+    n = bench["config"]["global_batch"] // bench["n_gpus"]
+    hops = bench["config"]["hop_visits_per_trace"]
+    # per invocation per 64 traces (one wave64's worth of lanes)
+    unit = n / 64 * hops
+    kernel_ns = float(walk["AverageNs"])
+    xcds = 8
+    out = {
+        "round": int(rnd.lstrip("r")),
+        "config": bench["config"].get("name", "c3"),
+        "batch": n,
+        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py ; PMC passes: --pmc FETCH_SIZE | "
+                   "WRITE_SIZE | SQ_* (bench.py --steps 3 --warmup 1 --no-cpu)",
+        "kernel": walk["Name"],
+        "kernel_avg_ns": kernel_ns,
+        "kernel_calls": int(walk["Calls"]),
+        "resources": meta,
+        "fetch_size_kb_per_launch": fetch["FETCH_SIZE"],
+        "write_size_kb_per_launch": write["WRITE_SIZE"],
+        "hbm_bytes_per_launch": 2 * fetch["FETCH_SIZE"] * 1024 + write["WRITE_SIZE"] * 1024,
+        "hbm_bytes_note": "gfx950 correction: FETCH_SIZE doubled (MI355X_MICROARCH.md §HBM); WRITE_SIZE "
+                          "taken as-is (16 B/lane record stores); includes the per-workgroup global-atomic flush",
+        "per_invocation_per_64_traces": {
+            "valu": sq1["SQ_INSTS_VALU"] / unit, "salu": sq1["SQ_INSTS_SALU"] / unit,
+            "smem": sq1["SQ_INSTS_SMEM"] / unit, "lds": sq2["SQ_INSTS_LDS"] / unit},
+        "wave_cycle_shares": {
+            "wait_any": sq1["SQ_WAIT_ANY"] / sq1["SQ_WAVE_CYCLES"],
+            "wait_inst_any": sq1["SQ_WAIT_INST_ANY"] / sq1["SQ_WAVE_CYCLES"],
+            "active_inst_any": sq1["SQ_ACTIVE_INST_ANY"] / sq1["SQ_WAVE_CYCLES"]},
+        "waves": sq1["SQ_WAVES"],
+        "grbm_gui_active": sq2["GRBM_GUI_ACTIVE"],
+        "effective_clock_ghz": sq2["GRBM_GUI_ACTIVE"] / xcds / kernel_ns,
+    }
+    with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
