@@ -644,10 +644,59 @@ __device__ __forceinline__ void philox_group(uint32_t t_lo, uint32_t t_hi, uint3
   x[3] = d;
 }
 
+// TPL Philox blocks (one per trace of the lane) of counter (t_lo[u], t_hi, g, 0)
+// in lockstep: the round keys and the scalar rounds 1-2 (all counter words
+// but t_lo are wave-uniform) are shared by the TPL chains.
+template <int TPL>
+__device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uint32_t t_hi_u, uint32_t g,
+                                                uint32_t k0a, uint32_t k1a, uint32_t (&x)[TPL][4]) {
+  const uint64_t q1 = (uint64_t)M1 * g;                      // scalar
+  const uint32_t u0 = (uint32_t)(q1 >> 32) ^ t_hi_u ^ k0a;   // uniform
+  const uint32_t u1 = (uint32_t)q1;                          // uniform
+  const uint32_t k0b = k0a + W0, k1b = k1a + W1;
+  const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar (round 2)
+  uint32_t a[TPL], b[TPL], cc[TPL], d[TPL];
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    const uint64_t p0 = (uint64_t)M0 * t_lo[u];              // per lane
+    const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;
+    const uint64_t p1 = (uint64_t)M1 * v2;
+    a[u] = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+    b[u] = (uint32_t)p1;
+    cc[u] = (uint32_t)(q0 >> 32) ^ (uint32_t)p0 ^ k1b;
+    d[u] = (uint32_t)q0;
+  }
+  uint32_t k0 = k0b + W0, k1 = k1b + W1;
+#pragma unroll
+  for (int r = 2; r < 10; ++r) {
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) round1(a[u], b[u], cc[u], d[u], k0, k1);
+    k0 += W0;
+    k1 += W1;
+  }
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    x[u][0] = a[u];
+    x[u][1] = b[u];
+    x[u][2] = cc[u];
+    x[u][3] = d[u];
+  }
+}
+
+#ifndef ISIM_LOCKSTEP
+#define ISIM_LOCKSTEP 1
+#endif
+#ifndef ISIM_EARLY_WAIT
+#define ISIM_EARLY_WAIT 0
+#endif
+#ifndef ISIM_FAST_A
+#define ISIM_FAST_A 1
+#endif
+
 // TPL traces per lane: the wave walks 64*TPL traces through one pass over the
 // stream, so the per-record scalar work (fetch, decode, counter adds) is
 // shared and each lane runs TPL independent Philox chains (ILP).
-template <bool MODEB, bool LDSC, int TPL>
+template <bool MODEB, bool LDSC, int TPL, bool FULL>
 __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restrict__ stream, uint32_t n_groups,
                                             uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
                                             uint64_t n_traces, uint64_t base) {
@@ -665,7 +714,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
     t_lo[u] = (uint32_t)t;
     t_hi[u] = (uint32_t)(t >> 32);
     t_hi_u[u] = rfl(t_hi[u]);
-    hi_uniform = hi_uniform && ballot(t_hi[u] != t_hi_u[u]) == 0;  // no straddle of 2^32
+    hi_uniform = hi_uniform && ballot(t_hi[u] != t_hi_u[u]) == 0 && t_hi_u[u] == t_hi_u[0];  // no 2^32 straddle
     all[u] = ballot(valid[u]);
   }
 
@@ -738,8 +787,12 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
   };
   auto draws = [&](const Node4 &q, uint32_t g, uint32_t (&x)[TPL][4]) {
     if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0) {
+      if (ISIM_LOCKSTEP && hi_uniform) {
+        philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
+      } else {
 #pragma unroll
-      for (int u = 0; u < TPL; ++u) philox_group(t_lo[u], t_hi[u], t_hi_u[u], hi_uniform, g, c.k0, c.k1, x[u]);
+        for (int u = 0; u < TPL; ++u) philox_group(t_lo[u], t_hi[u], t_hi_u[u], hi_uniform, g, c.k0, c.k1, x[u]);
+      }
     }
   };
   auto group = [&](const Node4 &q, uint32_t g) {
@@ -747,6 +800,32 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
 #pragma unroll
     for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
     draws(q, g, x);
+    if constexpr (!MODEB && ISIM_FAST_A) {
+      // mode A, no errorRate-1 record in the group: per record one compare
+      // per trace; counts only on the (rarer) records where some lane errs
+      if (((q.n[0].meta | q.n[1].meta | q.n[2].meta | q.n[3].meta) & 0x80000000u) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint64_t own[TPL], any = 0;
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) {
+            own[u] = ballot(x[u][j] < q.n[j].thr);
+            if constexpr (!FULL) own[u] &= all[u];
+            any |= own[u];
+          }
+          if (any) {
+            uint32_t n = 0;
+#pragma unroll
+            for (int u = 0; u < TPL; ++u) {
+              errh[u] += lane_in(own[u]) ? 1u : 0u;
+              n += popc(own[u]);
+            }
+            count_t<LDSC>(c.gstats, c.cnt, c.n_slots + (q.n[j].meta & 0xFFFFFFu), n, lane0);
+          }
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       uint32_t xw[TPL];
@@ -783,10 +862,20 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
     }
   }
   uint32_t g = 1;
+  // Wait for the group loaded one iteration ago before issuing the next
+  // load, so s_waitcnt lgkmcnt(0) never waits on the load just issued.
+  auto settle = [&](const Node4 &q) {
+    if (ISIM_EARLY_WAIT)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(q.n[0].thr), "s"(q.n[0].meta), "s"(q.n[1].thr), "s"(q.n[1].meta),
+                   "s"(q.n[2].thr), "s"(q.n[2].meta), "s"(q.n[3].thr), "s"(q.n[3].meta)
+                   : "memory");
+  };
   while (g < n_groups) {
+    settle(bufB);
     if (g + 1 < n_groups) bufA = stream[g + 1];
     group(bufB, g);
     if (++g >= n_groups) break;
+    settle(bufA);
     if (g + 1 < n_groups) bufB = stream[g + 1];
     group(bufA, g);
     if (++g >= n_groups) break;
@@ -846,10 +935,17 @@ __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
   const uint64_t n_batches = (kp.n_traces + kBatch - 1) / kBatch;
   const uint64_t stride = (uint64_t)gridDim.x * waves;
   for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
-    if constexpr (KIND == 4)
-      walk_stream<MODEB, LDSC, kStreamTPL>(c, reinterpret_cast<const Node4 *>(prog),
-                                           kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0, kp.n_nodes, kp.t_static,
-                                           kp.trace_begin, kp.n_traces, b * 64 * kStreamTPL);
+    if constexpr (KIND == 4) {
+      const uint64_t base = b * 64 * kStreamTPL;
+      const Node4 *st = reinterpret_cast<const Node4 *>(prog);
+      const uint32_t ng = kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0;
+      if (base + 64 * kStreamTPL <= kp.n_traces)  // every lane of every trace slot valid
+        walk_stream<MODEB, LDSC, kStreamTPL, true>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
+                                                   kp.n_traces, base);
+      else
+        walk_stream<MODEB, LDSC, kStreamTPL, false>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
+                                                    kp.n_traces, base);
+    }
     else if constexpr (STATIC) walk_static<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64);
     else walk_dynamic<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64, lstk, hstk);
   }
