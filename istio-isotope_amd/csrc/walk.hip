@@ -752,16 +752,33 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
       if (any) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, n, lane0);
     } else {
       if (slot == kSlotPad) return;
-      if (depth > 0) {
+      uint32_t k = (meta >> 24) & 0x7Fu;
+      if (k > 0 && depth > 0) {
+        // a leaf (opens and closes here): no push; its status is its own
+        // draw, OR-ed into the caller's running status
+        uint64_t any = 0;
+        uint32_t n = 0;
 #pragma unroll
-        for (int u = 0; u < TPL; ++u) s_mask[u].put(depth - 1, top[u]);
-        s_slot.put(depth - 1, top_slot);
+        for (int u = 0; u < TPL; ++u) {
+          errh[u] += lane_in(own[u]) ? 1u : 0u;
+          any |= own[u];
+          n += popc(own[u]);
+          top[u] |= own[u];
+        }
+        if (any) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, n, lane0);
+        --k;
+      } else {
+        if (depth > 0) {
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) s_mask[u].put(depth - 1, top[u]);
+          s_slot.put(depth - 1, top_slot);
+        }
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) top[u] = own[u];
+        top_slot = slot;
+        ++depth;
       }
-#pragma unroll
-      for (int u = 0; u < TPL; ++u) top[u] = own[u];
-      top_slot = slot;
-      ++depth;
-      for (uint32_t k = (meta >> 24) & 0x7Fu; k > 0; --k) {  // subtree closes
+      for (; k > 0; --k) {  // subtree closes
         uint64_t any = 0;
         uint32_t n = 0;
         uint64_t st[TPL];
