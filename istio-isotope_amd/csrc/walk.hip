@@ -54,12 +54,17 @@ struct Ins2 {
   Ins a, b;
 };
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (LUT 0x96) instead of two v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 __device__ __forceinline__ void round1(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t k0,
                                        uint32_t k1) {
   const uint64_t p0 = (uint64_t)M0 * c0;
   const uint64_t p1 = (uint64_t)M1 * c2;
-  const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-  const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+  const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+  const uint32_t n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
   c0 = n0;
   c1 = (uint32_t)p1;
   c2 = n2;
@@ -624,9 +629,9 @@ __device__ __forceinline__ void philox_group(uint32_t t_lo, uint32_t t_hi, uint3
     const uint32_t k0b = k0a + W0, k1b = k1a + W1;
     const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
     const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
-    a = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+    a = xor3((uint32_t)(p1 >> 32), u1, k0b);
     b = (uint32_t)p1;
-    cc = (uint32_t)(q0 >> 32) ^ v3 ^ k1b;
+    cc = xor3((uint32_t)(q0 >> 32), v3, k1b);
     d = (uint32_t)q0;
     uint32_t k0 = k0b + W0, k1 = k1b + W1;
 #pragma unroll
@@ -661,9 +666,9 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
     const uint64_t p0 = (uint64_t)M0 * t_lo[u];              // per lane
     const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;
     const uint64_t p1 = (uint64_t)M1 * v2;
-    a[u] = (uint32_t)(p1 >> 32) ^ u1 ^ k0b;
+    a[u] = xor3((uint32_t)(p1 >> 32), u1, k0b);
     b[u] = (uint32_t)p1;
-    cc[u] = (uint32_t)(q0 >> 32) ^ (uint32_t)p0 ^ k1b;
+    cc[u] = xor3((uint32_t)(q0 >> 32), (uint32_t)p0, k1b);
     d[u] = (uint32_t)q0;
   }
   uint32_t k0 = k0b + W0, k1 = k1b + W1;
