@@ -137,8 +137,12 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
   const void *src = st.kind == 4 ? (const void *)p.stream.data() : (const void *)p.code.data();
   const size_t bytes = st.kind == 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
-  HIPCHK(hipMalloc(&st.d_prog, bytes));
+  // the draw-stream kernel prefetches group g+1 unconditionally: two zero
+  // groups (32 B each) of tail padding keep those reads inside the buffer
+  const size_t tail = st.kind == 4 ? 2 * 4 * sizeof(isim::Node) : 0;
+  HIPCHK(hipMalloc(&st.d_prog, bytes + tail));
   HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
+  if (tail) HIPCHK(hipMemset((char *)st.d_prog + bytes, 0, tail));
   if (st.kind == 4 && p.n_slots > 0) {
     HIPCHK(hipMalloc(&st.d_mult, p.stream_mult.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_mult, p.stream_mult.data(), p.stream_mult.size() * sizeof(uint32_t),

@@ -603,6 +603,20 @@ __device__ __forceinline__ void walk_dynamic(const Ctx &c, uint64_t trace_begin,
 struct Node4 {
   Node n[4];
 };
+// The stream is read-only for the whole launch: reading it through the
+// constant address space lets the compiler issue s_load_dwordx8 (a uniform
+// global-space load after the loop's stores would become a VMEM load +
+// v_readfirstlane with an immediate vmcnt wait).
+typedef const __attribute__((address_space(4))) Node4 CNode4;
+__device__ __forceinline__ Node4 load_group(CNode4 *p) {
+  Node4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r.n[j].thr = p->n[j].thr;
+    r.n[j].meta = p->n[j].meta;
+  }
+  return r;
+}
 
 template <bool LDSC>
 __device__ __forceinline__ void count_t(uint64_t *__restrict__ gstats, uint32_t *cnt, uint32_t idx, uint32_t v,
@@ -702,7 +716,7 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
 // stream, so the per-record scalar work (fetch, decode, counter adds) is
 // shared and each lane runs TPL independent Philox chains (ILP).
 template <bool MODEB, bool LDSC, int TPL, bool FULL>
-__device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restrict__ stream, uint32_t n_groups,
+__device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ stream, uint32_t n_groups,
                                             uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
                                             uint64_t n_traces, uint64_t base) {
   const uint32_t lane = lane_id();
@@ -857,9 +871,8 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
     }
   };
 
-  Node4 bufA = stream[0];
-  Node4 bufB;
-  if (n_groups > 1) bufB = stream[1];
+  const Node4 bufA = load_group(stream);
+  const Node4 bufB = load_group(stream + 1);  // zero tail padding when n_groups == 1
   {  // group 0: record 0 is the entry invocation (the client request)
     uint32_t x[TPL][4];
 #pragma unroll
@@ -883,24 +896,15 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, const Node4 *__restric
       }
     }
   }
-  uint32_t g = 1;
-  // Wait for the group loaded one iteration ago before issuing the next
-  // load, so s_waitcnt lgkmcnt(0) never waits on the load just issued.
-  auto settle = [&](const Node4 &q) {
-    if (ISIM_EARLY_WAIT)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(q.n[0].thr), "s"(q.n[0].meta), "s"(q.n[1].thr), "s"(q.n[1].meta),
-                   "s"(q.n[2].thr), "s"(q.n[2].meta), "s"(q.n[3].thr), "s"(q.n[3].meta)
-                   : "memory");
-  };
-  while (g < n_groups) {
-    settle(bufB);
-    if (g + 1 < n_groups) bufA = stream[g + 1];
-    group(bufB, g);
-    if (++g >= n_groups) break;
-    settle(bufA);
-    if (g + 1 < n_groups) bufB = stream[g + 1];
-    group(bufA, g);
-    if (++g >= n_groups) break;
+  // Group g+1 is loaded (unconditionally: the device buffer carries two zero
+  // groups of tail padding) before group g is processed, and handed over by
+  // a loop-carried copy after it, so the s_waitcnt for the load lands after
+  // a whole group of Philox work.
+  Node4 cur = bufB;
+  for (uint32_t g = 1; g < n_groups; ++g) {
+    const Node4 nxt = load_group(stream + g + 1);
+    group(cur, g);
+    cur = nxt;
   }
 #pragma unroll
   for (int u = 0; u < TPL; ++u) finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st[u], errh[u]);
@@ -959,7 +963,7 @@ __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
   for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
     if constexpr (KIND == 4) {
       const uint64_t base = b * 64 * kStreamTPL;
-      const Node4 *st = reinterpret_cast<const Node4 *>(prog);
+      CNode4 *st = (CNode4 *)(const __attribute__((address_space(1))) Ins *)prog;
       const uint32_t ng = kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0;
       if (base + 64 * kStreamTPL <= kp.n_traces)  // every lane of every trace slot valid
         walk_stream<MODEB, LDSC, kStreamTPL, true>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
