@@ -643,9 +643,9 @@ __device__ __forceinline__ void philox_group(uint32_t t_lo, uint32_t t_hi, uint3
     const uint32_t k0b = k0a + W0, k1b = k1a + W1;
     const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar
     const uint64_t p1 = (uint64_t)M1 * v2;                     // per lane
-    a = xor3((uint32_t)(p1 >> 32), u1, k0b);
+    a = (uint32_t)(p1 >> 32) ^ (u1 ^ k0b);
     b = (uint32_t)p1;
-    cc = xor3((uint32_t)(q0 >> 32), v3, k1b);
+    cc = v3 ^ ((uint32_t)(q0 >> 32) ^ k1b);
     d = (uint32_t)q0;
     uint32_t k0 = k0b + W0, k1 = k1b + W1;
 #pragma unroll
@@ -674,20 +674,28 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
   const uint32_t u1 = (uint32_t)q1;                          // uniform
   const uint32_t k0b = k0a + W0, k1b = k1a + W1;
   const uint64_t q0 = (uint64_t)M0 * u0;                     // scalar (round 2)
+  // a VOP3 reads one SGPR: pre-xor the uniform words (opaque, so the
+  // compiler does not re-fold them into a two-SGPR v_bitop3 + v_mov)
+  uint32_t uk0 = u1 ^ k0b, uk1 = (uint32_t)(q0 >> 32) ^ k1b;
+  asm volatile("" : "+s"(uk0), "+s"(uk1));
   uint32_t a[TPL], b[TPL], cc[TPL], d[TPL];
 #pragma unroll
   for (int u = 0; u < TPL; ++u) {
     const uint64_t p0 = (uint64_t)M0 * t_lo[u];              // per lane
     const uint32_t v2 = (uint32_t)(p0 >> 32) ^ k1a;
     const uint64_t p1 = (uint64_t)M1 * v2;
-    a[u] = xor3((uint32_t)(p1 >> 32), u1, k0b);
+    a[u] = (uint32_t)(p1 >> 32) ^ uk0;
     b[u] = (uint32_t)p1;
-    cc[u] = xor3((uint32_t)(q0 >> 32), (uint32_t)p0, k1b);
+    cc[u] = (uint32_t)p0 ^ uk1;
     d[u] = (uint32_t)q0;
   }
   uint32_t k0 = k0b + W0, k1 = k1b + W1;
 #pragma unroll
   for (int r = 2; r < 10; ++r) {
+    // recompute the round keys per group (2 s_add) instead of letting the
+    // compiler hoist all 16 into SGPRs, which spill to VGPR lanes and come
+    // back as v_readlane (VALU) in the hot loop
+    asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int u = 0; u < TPL; ++u) round1(a[u], b[u], cc[u], d[u], k0, k1);
     k0 += W0;
