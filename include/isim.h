@@ -154,6 +154,15 @@ ISIM_API int isim_graph_num_services(const isim_graph *g);
 /* Exact implementation-neutral dump of the decoded graph.
  * Writes at most cap bytes (NUL-terminated when it fits); *len = bytes needed. */
 ISIM_API int isim_graph_canonical_json(const isim_graph *g, char *buf, size_t cap, size_t *len);
+/* json.Marshal(graph.ServiceGraph): svc/service.go:25-51 json tags + omitempty,
+ * script.Script.MarshalJSON (script/script.go:24-31, command.go:30-53),
+ * ByteSize/Percentage/ServiceType MarshalJSON (size/byte_size.go:31-34,
+ * pct/percentage.go:32-35, svctype/service_type.go:45-48).  Same buffer
+ * contract as isim_graph_canonical_json. */
+ISIM_API int isim_graph_marshal_json(const isim_graph *g, char *buf, size_t cap, size_t *len);
+/* graphviz.ServiceGraphToDotLanguage (convert/pkg/graphviz/graphviz.go:28-41):
+ * the Graphviz DOT text of `isotope convert graphviz`. */
+ISIM_API int isim_graph_to_dot(const isim_graph *g, char *buf, size_t cap, size_t *len);
 /* extractService: first service with that name (graph.go:97-109); -1 if absent. */
 ISIM_API int isim_graph_service_index(const isim_graph *g, const char *name);
 

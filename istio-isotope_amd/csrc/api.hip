@@ -14,6 +14,7 @@
 #include "../../include/isim.h"
 #include "gounits.h"
 #include "graph.h"
+#include "marshal.h"
 #include "kernel_abi.h"
 #include "program.h"
 
@@ -191,6 +192,26 @@ int isim_graph_canonical_json(const isim_graph *g, char *buf, size_t cap, size_t
     buf[n] = 0;
   }
   return ISIM_OK;
+}
+
+static int emit(const std::string &s, char *buf, size_t cap, size_t *len) {
+  if (len) *len = s.size() + 1;
+  if (buf && cap) {
+    size_t n = std::min(cap - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return ISIM_OK;
+}
+
+int isim_graph_marshal_json(const isim_graph *g, char *buf, size_t cap, size_t *len) {
+  if (!g) return fail(ISIM_EINVAL, "null graph");
+  return emit(isim::marshal_json(g->g), buf, cap, len);
+}
+
+int isim_graph_to_dot(const isim_graph *g, char *buf, size_t cap, size_t *len) {
+  if (!g) return fail(ISIM_EINVAL, "null graph");
+  return emit(isim::to_dot(g->g), buf, cap, len);
 }
 
 int isim_graph_service_index(const isim_graph *g, const char *name) {

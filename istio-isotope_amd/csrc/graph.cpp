@@ -388,15 +388,17 @@ bool unmarshal_service_graph(const char *json, size_t len, ServiceGraph &g, std:
   def_req.kind = Command::Request;
   def_req.size = d.request_size;
   g.services.clear();
+  g.services_nil = true;
   Saver sv;
   static const char *const kTop[] = {"services"};
   if (doc.kind == JVal::Obj) {
     for (const auto &kv : doc.obj) {
       if (match_field(kv.first, kTop, 1) != 0) continue;
       const JVal &v = kv.second;
-      if (v.kind == JVal::Null) { g.services.clear(); continue; }
+      if (v.kind == JVal::Null) { g.services.clear(); g.services_nil = true; continue; }
       if (v.kind != JVal::Arr) { sv.save(type_err(v.kind_name(), "[]svc.Service")); continue; }
       g.services.assign(v.arr.size(), Service());
+      g.services_nil = false;
       for (size_t i = 0; i < v.arr.size(); ++i)
         if (!unmarshal_service(v.arr[i], def, def_req, g.services[i], err)) return false;
     }

@@ -36,6 +36,7 @@ struct Service {
 
 struct ServiceGraph {
   std::vector<Service> services;
+  bool services_nil = true;  // Go: a nil slice (key absent or null) marshals as null, [] as []
 };
 
 // (*ServiceGraph).UnmarshalJSON (convert/pkg/graph/unmarshal.go:30-48):

@@ -6,6 +6,8 @@ the C++ loader in libisim.
                                      -> (*ServiceGraph).UnmarshalJSON, unmarshal.go:30-48
     size_from_string / duration_parse / percentage_from_string
                                    ~ size.FromString, time.ParseDuration, pct.FromString
+    ServiceGraph.marshal_json()    ~ json.Marshal(sg)
+    ServiceGraph.to_dot()          ~ graphviz.ServiceGraphToDotLanguage(sg)
 
 Load errors raise ``GraphError`` carrying the Go error text.  The decoded
 services are exposed as plain dataclasses with the Go field meanings
@@ -104,15 +106,26 @@ class ServiceGraph:
     def handle(self) -> C.c_void_p:
         return self._h
 
+    def _text(self, fn) -> bytes:
+        n = C.c_size_t()
+        native.check(fn(self._h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        native.check(fn(self._h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value - 1]
+
     def canonical(self) -> dict:
         if self._canon is None:
-            lib = native.load()
-            n = C.c_size_t()
-            native.check(lib.isim_graph_canonical_json(self._h, None, 0, C.byref(n)))
-            buf = C.create_string_buffer(n.value)
-            native.check(lib.isim_graph_canonical_json(self._h, buf, n.value, C.byref(n)))
-            self._canon = json.loads(buf.value.decode("utf-8"))
+            self._canon = json.loads(self._text(native.load().isim_graph_canonical_json).decode("utf-8"))
         return self._canon
+
+    def marshal_json(self) -> bytes:
+        """json.Marshal(graph.ServiceGraph): the bytes Go would produce
+        (svc/service.go json tags, script/command.go:30-53)."""
+        return self._text(native.load().isim_graph_marshal_json)
+
+    def to_dot(self) -> str:
+        """graphviz.ServiceGraphToDotLanguage (convert/pkg/graphviz/graphviz.go:28-41)."""
+        return self._text(native.load().isim_graph_to_dot).decode("utf-8")
 
     @property
     def services(self) -> List[Service]:

@@ -76,6 +76,8 @@ SIGNATURES = {
     "isim_graph_free": (None, [_VP]),
     "isim_graph_num_services": (C.c_int, [_VP]),
     "isim_graph_canonical_json": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "isim_graph_marshal_json": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "isim_graph_to_dot": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "isim_graph_service_index": (C.c_int, [_VP, C.c_char_p]),
     "isim_size_from_string": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     "isim_duration_parse": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),

@@ -149,6 +149,7 @@ class Service:
 @dataclass
 class ServiceGraph:
     services: List[Service] = field(default_factory=list)
+    services_nil: bool = True   # Go nil slice (key absent / null): json.Marshal writes null
 
 
 # ------------------------------------------------------- decode helpers ---
@@ -485,11 +486,13 @@ def unmarshal_service_graph(text) -> ServiceGraph:
                 continue
             if val is None:
                 g.services = []
+                g.services_nil = True
                 continue
             if _kind(val) != "array":
                 sv.save(UnmarshalTypeError(_kind(val), "[]svc.Service"))
                 continue
             g.services = [unmarshal_service(e, default_service, default_req) for e in val]
+            g.services_nil = False
     sv.done()
     validate(g)
     return g
