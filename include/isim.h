@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 2
+#define ISIM_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -117,6 +117,18 @@ typedef struct {
  * counters. */
 #define ISIM_SVC_DUR_WORDS (2 * ISIM_N_PROM + 2)
 #define ISIM_ST_SVC_DUR(n_slots) (ISIM_ST_SITES + 2 * (uint64_t)(n_slots))
+
+/* Per-service row of the DES table filled by isim_serve_des* (config 5,
+ * DESIGN.md §10): the service's invocation durations from request receipt to
+ * response, queueing included, as ISIM_SVC_DUR_WORDS ([code][33] buckets on
+ * the Prometheus duration edges, then the [code] sums in ns), followed by
+ * the replica-queue figures.  Rows follow the duration-table row order
+ * (reachable services in preorder; isim_des_fold maps them to services). */
+#define ISIM_DES_COUNT ISIM_SVC_DUR_WORDS          /* invocations */
+#define ISIM_DES_SUM_WAIT (ISIM_SVC_DUR_WORDS + 1) /* sum of queue waits, ns */
+#define ISIM_DES_MAX_WAIT (ISIM_SVC_DUR_WORDS + 2) /* longest queue wait, ns */
+#define ISIM_DES_SUM_HOLD (ISIM_SVC_DUR_WORDS + 3) /* worker busy time, ns */
+#define ISIM_DES_ROW_WORDS (ISIM_SVC_DUR_WORDS + 4)
 
 typedef struct {
   int32_t n_services;        /* services in the graph */
@@ -211,6 +223,48 @@ ISIM_API int isim_stats_fold(const isim_handler *h, const uint64_t *stats, uint6
  * ISIM_EINVAL when the handler was created with ISIM_FLAG_NO_SVC_DUR for a
  * dynamic walk. */
 ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *stats, uint64_t *svc_dur);
+
+/* ---- per-replica worker-pool DES (BASELINE config 5) ----
+ * Open-loop Poisson arrivals of the client requests at the entry; every
+ * replica of a service (svc.Service.NumReplicas, convert/pkg/graph/svc/
+ * service.go:30-31) is a FIFO queue in front of ONE worker, held for the
+ * invocation's sleep total; an invocation's script (Handler.ServeHTTP,
+ * handler.go:37-79) starts when the worker takes it.  Statuses, hops and
+ * call counters are those of the static walk; latencies and the per-service
+ * durations include queueing.  Exact (bit-identical to the sequential
+ * event-driven oracle) for the DES v1 graph class: static walks whose
+ * services are invoked at most once per trace, whose scripts have at most
+ * one step with calls, and whose multi-replica services are leaves
+ * (isim_des_info_get returns ISIM_EINVAL with the reason otherwise). */
+typedef struct {
+  uint64_t mean_interarrival_ns; /* 1 .. 2^34: mean gap of the exponential arrivals */
+  uint32_t flags;                /* must be 0 */
+  uint32_t reserved;             /* must be 0 */
+} isim_des_params;
+
+typedef struct {
+  int32_t n_positions;           /* invocations per trace */
+  int32_t n_levels;              /* depth of the invocation tree */
+  int32_t max_width;             /* widest level */
+  int32_t table_rows;            /* rows of the DES table (reachable services) */
+} isim_des_info;
+
+ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);
+/* Device workspace a batch of n_traces needs (8 B per invocation per trace + 20 B per trace). */
+ISIM_API int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes);
+/* One DES batch (trace ids [trace_begin, trace_begin+n_traces), arrivals from
+ * time 0, all replicas idle) on the current device, asynchronously on
+ * hip_stream.  d_records may be NULL; d_stats (info.stats_words) and
+ * d_des_table (table_rows * ISIM_DES_ROW_WORDS) are ACCUMULATED into. */
+ISIM_API int isim_serve_des_device(isim_handler *h, const isim_des_params *p, uint64_t trace_begin,
+                          uint64_t n_traces, isim_trace_rec *d_records, uint64_t *d_stats,
+                          uint64_t *d_des_table, void *d_workspace, uint64_t workspace_bytes,
+                          void *hip_stream);
+/* Synchronous convenience: host buffers (any may be NULL). */
+ISIM_API int isim_serve_des(isim_handler *h, int device, const isim_des_params *p, uint64_t trace_begin,
+                   uint64_t n_traces, isim_trace_rec *h_records, uint64_t *h_stats, uint64_t *h_des_table);
+/* DES table rows -> svc_rows[n_services][ISIM_DES_ROW_WORDS] (zero for unreachable services). */
+ISIM_API int isim_des_fold(const isim_handler *h, const uint64_t *des_table, uint64_t *svc_rows);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@
 #include "gounits.h"
 #include "graph.h"
 #include "marshal.h"
+#include "des.h"
 #include "kernel_abi.h"
 #include "program.h"
 
@@ -45,6 +46,9 @@ struct DevState {
   uint32_t max_blocks = 0;  // resident workgroups for the whole device
   uint32_t per_cu = 0;
   uint32_t kind = 0;
+  // DES (config 5): the plan uploaded on first use
+  void *d_des_pos = nullptr;
+  uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
 };
 
 }  // namespace
@@ -58,6 +62,10 @@ struct isim_handler {
   isim_params params{};
   std::mutex mu;
   std::map<int, DevState> dev;
+  bool des_built = false;
+  int des_rc = ISIM_OK;
+  std::string des_err;
+  isim::DesPlan des;
   ~isim_handler() {
     for (auto &kv : dev) {
       int cur = 0;
@@ -65,6 +73,10 @@ struct isim_handler {
         (void)hipFree(kv.second.d_prog);
         (void)hipFree(kv.second.d_mult);
         (void)hipFree(kv.second.d_dur);
+        (void)hipFree(kv.second.d_des_pos);
+        (void)hipFree(kv.second.d_des_child);
+        (void)hipFree(kv.second.d_des_level);
+        (void)hipFree(kv.second.d_des_mult);
         (void)hipSetDevice(cur);
       }
     }
@@ -260,6 +272,14 @@ int isim_handler_create(const isim_graph *g, const char *service_name, const isi
   h->params = *p;
   std::string err;
   int rc = isim::compile_program(g->g, entry, *p, h->prog, err);
+  if (rc == ISIM_OK) {
+    // the DES plan is built from the graph and the program; build it now
+    // (host only, cheap) so the handler does not keep the graph
+    rc = isim::build_des_plan(g->g, h->prog, h->des, h->des_err);
+    h->des_rc = rc;
+    h->des_built = true;
+    rc = ISIM_OK;
+  }
   if (rc != ISIM_OK) {
     delete h;
     return fail(rc, err);
@@ -441,6 +461,173 @@ int isim_stats_fold_durations(const isim_handler *h, const uint64_t *stats, uint
     row[2 * ISIM_N_PROM] = T * (calls[s] - errs[s]);
     row[2 * ISIM_N_PROM + 1] = T * errs[s];
   }
+  return ISIM_OK;
+}
+
+}  // extern "C"
+
+// ---- DES (BASELINE config 5) --------------------------------
+namespace {
+
+int des_prepare(isim_handler *h, int device, DevState *&st) {
+  int rc = prepare_device(h, device, st);
+  if (rc != ISIM_OK) return rc;
+  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (st->d_des_pos) return ISIM_OK;
+  const isim::DesPlan &d = h->des;
+  auto up = [&](void **dst, const void *src, size_t bytes) -> bool {
+    if (hipMalloc(dst, bytes ? bytes : 8) != hipSuccess) return false;
+    return !bytes || hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&st->d_des_pos, d.pos.data(), d.pos.size() * sizeof(isim::DesPos)) ||
+      !up((void **)&st->d_des_child, d.child.data(), d.child.size() * 4) ||
+      !up((void **)&st->d_des_level, d.level_pos.data(), d.level_pos.size() * 4) ||
+      !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4))
+    return fail(ISIM_EHIP, "DES plan upload failed");
+  return ISIM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
+  if (!h || !out) return fail(ISIM_EINVAL, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  out->n_positions = (int32_t)h->des.pos.size();
+  out->n_levels = (int32_t)h->des.level_off.size() - 1;
+  out->max_width = (int32_t)h->des.max_width;
+  out->table_rows = (int32_t)h->prog.row_svc.size();
+  return ISIM_OK;
+}
+
+int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
+  if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
+  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  *bytes = isim::des_workspace_bytes((uint32_t)h->des.pos.size(), n_traces);
+  return ISIM_OK;
+}
+
+int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t trace_begin, uint64_t n_traces,
+                          isim_trace_rec *d_records, uint64_t *d_stats, uint64_t *d_des_table, void *d_workspace,
+                          uint64_t workspace_bytes, void *hip_stream) {
+  if (!h || !dp || !d_stats || !d_des_table) return fail(ISIM_EINVAL, "null argument");
+  if (dp->mean_interarrival_ns == 0 || dp->mean_interarrival_ns > (1ull << 34))
+    return fail(ISIM_EINVAL, "mean_interarrival_ns must be in [1, 2^34]");
+  if (dp->reserved != 0 || dp->flags != 0) return fail(ISIM_EINVAL, "isim_des_params.flags/reserved must be 0");
+  if (n_traces == 0) return ISIM_OK;
+  if (n_traces > (1ull << 31)) return fail(ISIM_EINVAL, "n_traces above 2^31 per DES batch");
+  int device = 0;
+  HIPCHK(hipGetDevice(&device));
+  DevState *st = nullptr;
+  int rc = des_prepare(h, device, st);
+  if (rc != ISIM_OK) return rc;
+  const isim::DesPlan &d = h->des;
+  const uint32_t np = (uint32_t)d.pos.size();
+  if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(np, n_traces))
+    return fail(ISIM_EINVAL, "DES workspace smaller than isim_des_workspace_bytes()");
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  char *ws = (char *)d_workspace;
+  isim::DesLaunch L;
+  L.d_pos = st->d_des_pos;
+  L.d_child = st->d_des_child;
+  L.d_level_pos = st->d_des_level;
+  L.level_off = d.level_off;
+  L.W = (uint64_t *)ws;
+  ws += al((uint64_t)np * n_traces * 8);
+  L.A = (uint64_t *)ws;
+  ws += al(n_traces * 8);
+  L.E = (uint32_t *)ws;
+  ws += al(n_traces * 4);
+  L.blk = (uint64_t *)ws;
+  L.d_stats = d_stats;
+  L.d_table = d_des_table;
+  L.d_records = d_records;
+  L.n_traces = n_traces;
+  L.trace_begin = trace_begin;
+  L.mean_ns = dp->mean_interarrival_ns;
+  L.seed = h->params.seed;
+  L.n_pos = np;
+  L.n_slots = (uint32_t)h->prog.n_slots;
+  L.modeb = h->params.error_mode == ISIM_MODE_B ? 1u : 0u;
+  if (isim::des_launch(L, hip_stream) != 0) return fail(ISIM_EHIP, "DES kernel launch failed");
+  if (h->prog.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
+    uint32_t n_slots = (uint32_t)h->prog.n_slots;
+    const uint32_t *mult = st->d_des_mult;
+    void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};
+    HIPCHK(hipLaunchKernel(isim::stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args2, 0,
+                           (hipStream_t)hip_stream));
+  }
+  return ISIM_OK;
+}
+
+int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint64_t trace_begin, uint64_t n_traces,
+                   isim_trace_rec *h_records, uint64_t *h_stats, uint64_t *h_des_table) {
+  if (!h || !dp) return fail(ISIM_EINVAL, "null argument");
+  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  HIPCHK(hipSetDevice(device));
+  const uint64_t words = stats_words(h);
+  const uint64_t tab_words = (uint64_t)h->prog.row_svc.size() * ISIM_DES_ROW_WORDS;
+  const uint64_t ws_bytes = isim::des_workspace_bytes((uint32_t)h->des.pos.size(), n_traces);
+  uint64_t *d_stats = nullptr, *d_tab = nullptr;
+  void *d_ws = nullptr;
+  isim_trace_rec *d_rec = nullptr;
+  hipStream_t s = nullptr;
+  int rc = ISIM_OK;
+  do {
+    if (hipStreamCreate(&s) != hipSuccess) { rc = fail(ISIM_EHIP, "hipStreamCreate failed"); break; }
+    if (hipMalloc(&d_stats, words * 8) != hipSuccess || hipMalloc(&d_tab, tab_words * 8 + 8) != hipSuccess ||
+        hipMalloc(&d_ws, ws_bytes + 8) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "hipMalloc(DES buffers) failed");
+      break;
+    }
+    if (h_records && n_traces && hipMalloc(&d_rec, n_traces * sizeof(isim_trace_rec)) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "hipMalloc(records) failed");
+      break;
+    }
+    if (hipMemsetAsync(d_stats, 0, words * 8, s) != hipSuccess ||
+        hipMemsetAsync(d_tab, 0, tab_words * 8 + 8, s) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "hipMemset failed");
+      break;
+    }
+    rc = isim_serve_des_device(h, dp, trace_begin, n_traces, d_rec, d_stats, d_tab, d_ws, ws_bytes + 8, s);
+    if (rc != ISIM_OK) break;
+    if (h_stats && hipMemcpyAsync(h_stats, d_stats, words * 8, hipMemcpyDeviceToHost, s) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "copy stats failed");
+      break;
+    }
+    if (h_des_table && tab_words &&
+        hipMemcpyAsync(h_des_table, d_tab, tab_words * 8, hipMemcpyDeviceToHost, s) != hipSuccess) {
+      rc = fail(ISIM_EHIP, "copy DES table failed");
+      break;
+    }
+    if (d_rec && hipMemcpyAsync(h_records, d_rec, n_traces * sizeof(isim_trace_rec), hipMemcpyDeviceToHost, s) !=
+                     hipSuccess) {
+      rc = fail(ISIM_EHIP, "copy records failed");
+      break;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) rc = fail(ISIM_EHIP, "hipStreamSynchronize failed");
+  } while (0);
+  (void)hipFree(d_rec);
+  (void)hipFree(d_ws);
+  (void)hipFree(d_tab);
+  (void)hipFree(d_stats);
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int isim_des_fold(const isim_handler *h, const uint64_t *des_table, uint64_t *svc_rows) {
+  if (!h || !des_table || !svc_rows) return fail(ISIM_EINVAL, "null argument");
+  const isim::Program &p = h->prog;
+  constexpr uint32_t W = ISIM_DES_ROW_WORDS;
+  std::fill(svc_rows, svc_rows + (size_t)p.n_services * W, 0);
+  for (size_t r = 0; r < p.row_svc.size(); ++r)
+    std::copy(des_table + r * W, des_table + (r + 1) * W, svc_rows + (size_t)p.row_svc[r] * W);
   return ISIM_OK;
 }
 

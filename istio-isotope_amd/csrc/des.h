@@ -1,0 +1,88 @@
+// Per-replica worker-pool discrete-event simulation (BASELINE config 5,
+// DESIGN.md §10 "isim DES semantics v1").
+//
+// Host side: the DES plan — the unrolled invocation tree of a static walk
+// (one POSITION per invocation, in hop order = the draw stream's order), the
+// per-position timing constants, and the positions grouped by depth (LEVELS).
+// Device side (des.hip): a level-synchronous exact algorithm over all traces
+// of a batch at once — top-down, one FIFO max-plus scan per position over the
+// traces (the replica queue); bottom-up, finish times, statuses, durations.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/isim.h"
+#include "graph.h"
+#include "program.h"
+
+namespace isim {
+
+constexpr uint32_t kDesNoParent = 0xFFFFFFFFu;
+constexpr uint32_t kDesMaxReplicas = 64;  // per-replica carries of a leaf position live in LDS
+constexpr uint32_t kDesFlagAlways = 1u;   // errorRate 1
+constexpr uint32_t kDesFlagLeaf = 2u;     // no call step
+
+// One invocation position of the unrolled tree (64 bytes, device layout).
+struct DesPos {
+  uint32_t parent;     // caller's position (kDesNoParent: the entry)
+  uint32_t row;        // duration-table row of the service (Program::svc_row)
+  uint32_t slot;       // stats slot of the call site (kSlotRoot: the entry)
+  uint32_t reps;       // replicas of the service (numReplicas, >= 1)
+  uint64_t off;        // arrival = start(parent) + off: the caller's pre-call sleeps + H
+  uint64_t hold;       // worker hold time: the service's sleep total
+  uint64_t floor;      // leaf: script time; else pre-call sleeps + longest sleep of the call step
+  uint64_t post;       // sleeps after the call step
+  uint32_t child_off, child_cnt;  // children in DesPlan::child
+  uint32_t thr;        // error threshold over the u32 draw
+  uint32_t flags;      // kDesFlag*
+};
+static_assert(sizeof(DesPos) == 64, "DesPos must be 64 bytes");
+
+struct DesPlan {
+  std::vector<DesPos> pos;           // hop order (position 0 = the entry)
+  std::vector<uint32_t> child;       // children lists (positions)
+  std::vector<uint32_t> level_pos;   // positions grouped by depth
+  std::vector<uint32_t> level_off;   // [n_levels + 1]
+  std::vector<uint32_t> slot_mult;   // per slot: calls through it per trace
+  uint32_t max_width = 0;            // widest level
+};
+
+// Device buffers and sizes of one DES batch (des.hip: des_launch).
+struct DesLaunch {
+  const void *d_pos;                 // DesPos[n_pos]
+  const uint32_t *d_child, *d_level_pos;
+  std::vector<uint32_t> level_off;   // host copy
+  uint64_t *W, *A, *blk;             // workspace: [n_pos][N], [N], chunk sums
+  uint32_t *E;                       // workspace: [N]
+  uint64_t *d_stats, *d_table;
+  isim_trace_rec *d_records;         // may be null
+  uint64_t n_traces, trace_begin, mean_ns, seed;
+  uint32_t n_pos, n_slots, modeb;
+};
+
+// Workspace bytes for a batch of n traces (W, A, E, chunk sums; 256-B aligned parts).
+uint64_t des_workspace_bytes(uint32_t n_pos, uint64_t n);
+int des_launch(const DesLaunch &L, void *stream);
+
+// Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is
+// outside the DES v1 class.
+int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err);
+
+// -ln(w / 2^24), w = (u >> 8) + 1, in Q24 fixed point:
+// log1p(i/256) table, 16-bit linear interpolation.  Shared by host and device.
+constexpr int32_t kLnQ24[257] = {
+#include "des_ln_table.inc"
+};
+constexpr int64_t kLn2Q24 = 11629080;  // round(ln 2 * 2^24)
+
+inline uint64_t des_exp_q24_host(uint32_t u) {
+  const uint32_t w = (u >> 8) + 1u;
+  const int e = 31 - __builtin_clz(w);
+  const uint32_t f = (w << (24 - e)) & 0xFFFFFFu;
+  const uint32_t idx = f >> 16, rem = f & 0xFFFFu;
+  const int64_t lnm = kLnQ24[idx] + ((((int64_t)kLnQ24[idx + 1] - kLnQ24[idx]) * (int64_t)rem) >> 16);
+  return (uint64_t)(24 * kLn2Q24 - ((int64_t)e * kLn2Q24 + lnm));
+}
+
+}  // namespace isim

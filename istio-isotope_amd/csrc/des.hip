@@ -1,0 +1,506 @@
+// Per-replica worker-pool DES on gfx950: exact,
+// level-synchronous over a batch of N traces.
+//
+//   arrivals   A[t] = sum of exponential inter-arrival times (Philox draw,
+//              integer inverse CDF) — a block scan + a scan of block sums
+//   down pass  per level, one workgroup per position v: the replica queue of
+//              v's service is FIFO over its arrivals a(v,t) = S(parent,t) +
+//              off(v), which are in trace order, so the start
+//              times are one max-plus scan over t:  fin_t = max(fin_{t-1},
+//              a_t) + hold,  S_t = fin_t - hold  (per replica for leaves with
+//              numReplicas > 1).  W[v][t] = S.
+//   up pass    per level from the deepest, (position, trace-range) blocks:
+//              finish F = max(S + floor, max_c F(c)) + post, status (own
+//              Philox error draw; mode B ORs the children's), duration
+//              F - a(v,t) into the per-service histogram.  W[v][t] = F | st<<63.
+//   finalize   latency F(entry) - A[t], records and the stats header.
+//
+// HBM layout: W is [position][trace] u64 so every pass reads and writes
+// whole cache lines of consecutive traces; A (u64) and E (u32, per-trace 500
+// count) are [trace].  All bytes per (position, trace): down 8 R + 8 W, up
+// 8 R (S) + 8 R (parent S) + 8 R per child + 8 W.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "des.h"
+#include "kernel_abi.h"
+
+namespace isim {
+namespace dev {
+
+constexpr uint32_t kDesPer = 8;                   // traces per thread in the down pass / arrivals
+constexpr uint32_t kDesThreads = 1024;
+constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per scan chunk
+constexpr uint32_t kDesUpThreads = 256;
+constexpr uint64_t kMask63 = (1ull << 63) - 1;
+
+__constant__ int32_t c_ln[257] = {
+#include "des_ln_table.inc"
+};
+
+__device__ __forceinline__ uint32_t des_xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Philox4x32-10 (Random123), counter (t_lo, t_hi, w2, w3), key (k0, k1)
+__device__ __forceinline__ void des_philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = des_xor3((uint32_t)(p1 >> 32), c[1], k0);
+    const uint32_t n2 = des_xor3((uint32_t)(p0 >> 32), c[3], k1);
+    c[0] = n0;
+    c[1] = (uint32_t)p1;
+    c[2] = n2;
+    c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ uint32_t des_draw(uint64_t t, uint32_t w2, uint32_t w3, uint32_t word, uint32_t k0,
+                                             uint32_t k1) {
+  uint32_t c[4] = {(uint32_t)t, (uint32_t)(t >> 32), w2, w3};
+  des_philox(c, k0, k1);
+  return word == 0 ? c[0] : word == 1 ? c[1] : word == 2 ? c[2] : c[3];
+}
+
+// -ln(w / 2^24) in Q24, w = (u >> 8) + 1 (des.h / DESIGN §10.2)
+__device__ __forceinline__ uint64_t des_exp_q24(uint32_t u) {
+  const uint32_t w = (u >> 8) + 1u;
+  const int e = 31 - __builtin_clz(w);
+  const uint32_t f = (w << (24 - e)) & 0xFFFFFFu;
+  const uint32_t idx = f >> 16, rem = f & 0xFFFFu;
+  const int64_t lnm = c_ln[idx] + ((((int64_t)c_ln[idx + 1] - c_ln[idx]) * (int64_t)rem) >> 16);
+  return (uint64_t)(24 * kLn2Q24 - ((int64_t)e * kLn2Q24 + lnm));
+}
+
+__device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
+  constexpr uint32_t edges_ms[32] = {7,  8,  9,  10, 11,  12,  14,  16,  18,  20,  25,  30,  35,  40,  45,  50,
+                                     60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
+  uint32_t b = 32;
+#pragma unroll
+  for (int i = 31; i >= 0; --i)
+    if (t <= (uint64_t)edges_ms[i] * 1000000ull) b = (uint32_t)i;
+  return b;
+}
+
+struct DesK {
+  const DesPos *pos;
+  const uint32_t *child;
+  const uint32_t *level_pos;
+  uint64_t *W;  // [n_pos][N]
+  uint64_t *A;  // [N]
+  uint32_t *E;  // [N]
+  uint64_t *blk;
+  uint64_t *stats;
+  uint64_t *table;  // [rows][ISIM_DES_ROW_WORDS]
+  isim_trace_rec *records;
+  uint64_t N, trace_begin, mean_ns;
+  uint32_t k0, k1;
+  uint32_t n_pos, n_slots;
+  uint32_t level_begin, splits;
+  uint32_t modeb, n_blk;
+};
+
+// (B, C) represents x -> max(x + B, C); `then` composes a after b.
+struct MaxPlus {
+  uint64_t B, C;
+};
+__device__ __forceinline__ MaxPlus mp_then(MaxPlus first, MaxPlus second) {
+  const uint64_t c = first.C + second.B;
+  return {first.B + second.B, c > second.C ? c : second.C};
+}
+
+// Inclusive block scan of MaxPlus over kDesThreads threads (wave shuffles +
+// one LDS pass over the 16 wave totals).
+__device__ __forceinline__ MaxPlus mp_block_scan(MaxPlus v, MaxPlus *wtot) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    MaxPlus o;
+    o.B = __shfl_up(v.B, d, 64);
+    o.C = __shfl_up(v.C, d, 64);
+    if (lane >= d) v = mp_then(o, v);
+  }
+  if (lane == 63) wtot[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    MaxPlus w = lane < kDesThreads / 64 ? wtot[lane] : MaxPlus{0, 0};
+#pragma unroll
+    for (uint32_t d = 1; d < kDesThreads / 64; d <<= 1) {
+      MaxPlus o;
+      o.B = __shfl_up(w.B, d, 64);
+      o.C = __shfl_up(w.C, d, 64);
+      if (lane >= d) w = mp_then(o, w);
+    }
+    if (lane < kDesThreads / 64) wtot[lane] = w;
+  }
+  __syncthreads();
+  if (wave > 0) v = mp_then(wtot[wave - 1], v);
+  __syncthreads();  // wtot is reused by the next call
+  return v;
+}
+
+__device__ __forceinline__ uint64_t block_scan_add(uint64_t v, uint64_t *wtot, uint64_t &total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  if (lane == 63) wtot[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t w = lane < kDesThreads / 64 ? wtot[lane] : 0;
+#pragma unroll
+    for (uint32_t d = 1; d < kDesThreads / 64; d <<= 1) {
+      const uint64_t o = __shfl_up(w, d, 64);
+      if (lane >= d) w += o;
+    }
+    if (lane < kDesThreads / 64) wtot[lane] = w;
+  }
+  __syncthreads();
+  if (wave > 0) v += wtot[wave - 1];
+  total = wtot[kDesThreads / 64 - 1];
+  __syncthreads();
+  return v;  // inclusive
+}
+
+// ---- arrivals: per chunk inclusive prefix of the inter-arrival times
+__global__ void __launch_bounds__(kDesThreads) des_arrivals(DesK k) {
+  __shared__ uint64_t wtot[kDesThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kDesChunk + (uint64_t)threadIdx.x * kDesPer;
+  uint64_t x[kDesPer], s = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kDesPer; ++i) {
+    const uint64_t t = base + i;
+    x[i] = 0;
+    if (t < k.N) {
+      const uint32_t u = des_draw(k.trace_begin + t, 0u, 0x80000001u, 0, k.k0, k.k1);
+      x[i] = (k.mean_ns * des_exp_q24(u)) >> 24;
+    }
+    s += x[i];
+  }
+  uint64_t total;
+  uint64_t run = block_scan_add(s, wtot, total) - s;
+#pragma unroll
+  for (uint32_t i = 0; i < kDesPer; ++i) {
+    run += x[i];
+    if (base + i < k.N) k.A[base + i] = run;
+  }
+  if (threadIdx.x == 0) k.blk[blockIdx.x] = total;
+}
+
+// exclusive scan of the chunk totals (one workgroup)
+__global__ void __launch_bounds__(kDesThreads) des_scan_blocks(DesK k) {
+  __shared__ uint64_t wtot[kDesThreads / 64];
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < k.n_blk; b0 += kDesThreads) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint64_t v = b < k.n_blk ? k.blk[b] : 0;
+    uint64_t total;
+    const uint64_t inc = block_scan_add(v, wtot, total);
+    if (b < k.n_blk) k.blk[b] = carry + inc - v;
+    carry += total;
+  }
+}
+
+__global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
+  const uint64_t off = k.blk[blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * kDesChunk;
+  for (uint32_t i = threadIdx.x; i < kDesChunk; i += kDesThreads)
+    if (base + i < k.N) k.A[base + i] += off;
+}
+
+// ---- down pass: FIFO start times, one workgroup per position of the level
+__global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
+  __shared__ MaxPlus wtot[kDesThreads / 64];
+  __shared__ uint64_t carry[kDesMaxReplicas];
+  __shared__ uint64_t red[2 * kDesThreads / 64];
+  __shared__ MaxPlus xs[kDesThreads];
+  const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
+  const DesPos P = k.pos[v];
+  const uint32_t reps = P.reps;
+  if (threadIdx.x < reps) carry[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t N = k.N;
+  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * N;
+  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
+  uint64_t *out = k.W + (uint64_t)v * N;
+  uint64_t wsum = 0, wmax = 0;
+  for (uint64_t c0 = 0; c0 < N; c0 += kDesChunk) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDesPer;
+    uint64_t a[kDesPer];
+    uint32_t rr[kDesPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kDesPer; ++i) {
+      const uint64_t t = base + i;
+      a[i] = t < N ? par[t] + off : 0;
+      rr[i] = (t < N && reps > 1) ? des_draw(k.trace_begin + t, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
+    }
+    for (uint32_t r = 0; r < reps; ++r) {
+      MaxPlus f{0, 0};
+#pragma unroll
+      for (uint32_t i = 0; i < kDesPer; ++i)
+        if (base + i < N && rr[i] == r) f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
+      const MaxPlus inc = mp_block_scan(f, wtot);
+      // exclusive prefix = the previous thread's inclusive one
+      xs[threadIdx.x] = inc;
+      __syncthreads();
+      const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
+      const uint64_t cin = carry[r];
+      uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+#pragma unroll
+      for (uint32_t i = 0; i < kDesPer; ++i) {
+        const uint64_t t = base + i;
+        if (t < N && rr[i] == r) {
+          const uint64_t S = x > a[i] ? x : a[i];
+          out[t] = S;
+          const uint64_t w = S - a[i];
+          wsum += w;
+          wmax = w > wmax ? w : wmax;
+          x = S + P.hold;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == kDesThreads - 1) carry[r] = x;
+      __syncthreads();
+    }
+  }
+  // per-position queue statistics (the service's row: one position per service)
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d, 64);
+    const uint64_t o = __shfl_xor(wmax, d, 64);
+    wmax = o > wmax ? o : wmax;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = wsum;
+    red[kDesThreads / 64 + (threadIdx.x >> 6)] = wmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0, m = 0;
+    for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
+      s += red[i];
+      m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
+    }
+    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
+    atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)N);
+    atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
+    atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
+    atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(N * P.hold));
+  }
+}
+
+// ---- up pass: finish times, statuses, per-service durations
+__global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint64_t red[3 * kDesUpThreads / 64];
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hist[i] = 0;
+  __syncthreads();
+  const uint32_t v = k.level_pos[k.level_begin + blockIdx.y];
+  const DesPos P = k.pos[v];
+  const uint64_t N = k.N;
+  const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
+  const uint64_t *mine = k.W + (uint64_t)v * N;
+  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * N;
+  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
+  const bool leaf = P.flags & kDesFlagLeaf;
+  uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
+  for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
+    const uint64_t S = mine[t];
+    uint64_t F;
+    uint32_t sto = 0;
+    if (leaf) {
+      F = S + P.floor;
+    } else {
+      uint64_t m = S + P.floor;
+      for (uint32_t c = 0; c < P.child_cnt; ++c) {
+        const uint64_t fc = k.W[(uint64_t)k.child[P.child_off + c] * N + t];
+        const uint64_t tc = fc & kMask63;
+        m = tc > m ? tc : m;
+        sto |= (uint32_t)(fc >> 63);
+      }
+      F = m + P.post;
+    }
+    uint32_t own = 0;
+    if (P.flags & kDesFlagAlways) own = 1;
+    else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
+    const uint32_t st = k.modeb ? (own | sto) : own;
+    const uint64_t a = par[t] + off;
+    const uint64_t dur = F - a;
+    ((uint64_t *)mine)[t] = F | ((uint64_t)st << 63);
+    if (st) {
+      atomicAdd(k.E + t, 1u);
+      n500 += 1;
+      dsum1 += dur;
+    } else {
+      dsum0 += dur;
+    }
+    atomicAdd(&hist[st * ISIM_N_PROM + des_prom_bucket(dur)], 1u);
+  }
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    dsum0 += __shfl_xor(dsum0, d, 64);
+    dsum1 += __shfl_xor(dsum1, d, 64);
+    n500 += __shfl_xor(n500, d, 64);
+  }
+  constexpr uint32_t W = kDesUpThreads / 64;
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = dsum0;
+    red[W + (threadIdx.x >> 6)] = dsum1;
+    red[2 * W + (threadIdx.x >> 6)] = n500;
+  }
+  __syncthreads();
+  unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads)
+    if (hist[i]) atomicAdd(row + i, (unsigned long long)hist[i]);
+  if (threadIdx.x == 0) {
+    uint64_t s0 = 0, s1 = 0, e = 0;
+    for (uint32_t i = 0; i < W; ++i) {
+      s0 += red[i];
+      s1 += red[W + i];
+      e += red[2 * W + i];
+    }
+    if (s0) atomicAdd(row + 2 * ISIM_N_PROM, (unsigned long long)s0);
+    if (s1) atomicAdd(row + 2 * ISIM_N_PROM + 1, (unsigned long long)s1);
+    if (e && P.slot != kSlotRoot)
+      atomicAdd((unsigned long long *)(k.stats + ISIM_ST_SITES + k.n_slots + P.slot), (unsigned long long)e);
+  }
+}
+
+// ---- finalize: records and the latency statistics
+__global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
+  __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
+  __shared__ uint64_t red[5 * kDesUpThreads / 64];
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hp[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads) hl[i] = 0;
+  __syncthreads();
+  const uint64_t N = k.N;
+  uint64_t sl = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * kDesUpThreads + threadIdx.x; t < N;
+       t += (uint64_t)gridDim.x * kDesUpThreads) {
+    const uint64_t F = k.W[t];  // position 0 (the entry)
+    const uint32_t st = (uint32_t)(F >> 63);
+    const uint64_t L = (F & kMask63) - k.A[t];
+    const uint32_t e = k.E[t];
+    if (k.records) {
+      isim_trace_rec r;
+      r.latency_ns = L;
+      r.hops = k.n_pos;
+      r.status_err = (st << 31) | e;
+      k.records[t] = r;
+    }
+    sl += L;
+    se += e;
+    n5 += st;
+    mn = L < mn ? L : mn;
+    mx = L > mx ? L : mx;
+    atomicAdd(&hp[st * ISIM_N_PROM + des_prom_bucket(L)], 1u);
+    atomicAdd(&hl[st * ISIM_N_LOG2 + (L ? 64u - (uint32_t)__builtin_clzll(L) : 0u)], 1u);
+  }
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    sl += __shfl_xor(sl, d, 64);
+    se += __shfl_xor(se, d, 64);
+    n5 += __shfl_xor(n5, d, 64);
+    const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  constexpr uint32_t W = kDesUpThreads / 64;
+  if ((threadIdx.x & 63u) == 0) {
+    const uint32_t w = threadIdx.x >> 6;
+    red[w] = sl;
+    red[W + w] = se;
+    red[2 * W + w] = n5;
+    red[3 * W + w] = mn;
+    red[4 * W + w] = mx;
+  }
+  __syncthreads();
+  unsigned long long *st = (unsigned long long *)k.stats;
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads)
+    if (hp[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)hp[i]);
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads)
+    if (hl[i]) atomicAdd(st + ISIM_ST_LOG2 + i, (unsigned long long)hl[i]);
+  if (threadIdx.x == 0) {
+    for (uint32_t i = 1; i < W; ++i) {
+      red[0] += red[i];
+      red[W] += red[W + i];
+      red[2 * W] += red[2 * W + i];
+      red[3 * W] = red[3 * W + i] < red[3 * W] ? red[3 * W + i] : red[3 * W];
+      red[4 * W] = red[4 * W + i] > red[4 * W] ? red[4 * W + i] : red[4 * W];
+    }
+    if (blockIdx.x == 0) {
+      atomicAdd(st + ISIM_ST_N_TRACES, (unsigned long long)N);
+      atomicAdd(st + ISIM_ST_SUM_HOPS, (unsigned long long)(N * k.n_pos));
+    }
+    atomicAdd(st + ISIM_ST_SUM_LATENCY, (unsigned long long)red[0]);
+    atomicAdd(st + ISIM_ST_SUM_ERR_HOPS, (unsigned long long)red[W]);
+    atomicAdd(st + ISIM_ST_N_500, (unsigned long long)red[2 * W]);
+    if (red[3 * W] != ~0ull) atomicMax(st + ISIM_ST_NOT_MIN_LATENCY, (unsigned long long)~red[3 * W]);
+    atomicMax(st + ISIM_ST_MAX_LATENCY, (unsigned long long)red[4 * W]);
+  }
+}
+
+}  // namespace dev
+
+// Host launcher: the whole DES of one batch on `stream` (no allocation, no
+// host synchronisation).
+uint64_t des_workspace_bytes(uint32_t n_pos, uint64_t n) {
+  const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  return al((uint64_t)n_pos * n * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8);
+}
+
+int des_launch(const DesLaunch &L, void *stream_) {
+  using namespace dev;
+  hipStream_t stream = (hipStream_t)stream_;
+  DesK k{};
+  k.pos = (const DesPos *)L.d_pos;
+  k.child = L.d_child;
+  k.level_pos = L.d_level_pos;
+  k.W = L.W;
+  k.A = L.A;
+  k.E = L.E;
+  k.blk = L.blk;
+  k.stats = L.d_stats;
+  k.table = L.d_table;
+  k.records = L.d_records;
+  k.N = L.n_traces;
+  k.trace_begin = L.trace_begin;
+  k.mean_ns = L.mean_ns;
+  k.k0 = (uint32_t)L.seed;
+  k.k1 = (uint32_t)(L.seed >> 32);
+  k.n_pos = L.n_pos;
+  k.n_slots = L.n_slots;
+  k.modeb = L.modeb;
+  k.n_blk = (uint32_t)((L.n_traces + kDesChunk - 1) / kDesChunk);
+  if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
+  hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
+  hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
+  hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
+  const uint32_t levels = (uint32_t)L.level_off.size() - 1;
+  for (uint32_t l = 0; l < levels; ++l) {
+    k.level_begin = L.level_off[l];
+    hipLaunchKernelGGL(des_down, dim3(L.level_off[l + 1] - L.level_off[l]), dim3(kDesThreads), 0, stream, k);
+  }
+  for (uint32_t l = levels; l-- > 0;) {
+    const uint32_t width = L.level_off[l + 1] - L.level_off[l];
+    k.level_begin = L.level_off[l];
+    // enough (position, trace-range) blocks to fill the chip, >= 256 traces each
+    uint64_t splits = (4096 + width - 1) / width;
+    splits = splits < (L.n_traces + 255) / 256 ? splits : (L.n_traces + 255) / 256;
+    k.splits = (uint32_t)(splits ? splits : 1);
+    hipLaunchKernelGGL(des_up, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+  }
+  uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
+  fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;
+  hipLaunchKernelGGL(des_finalize, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // namespace isim

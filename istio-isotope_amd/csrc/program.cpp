@@ -205,7 +205,11 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
   out.time_bits = tmax[entry] < (1ull << 32) ? 32 : 64;
   out.site_callee.resize(sites.size());
   out.site_slot.assign(sites.size(), -1);
-  for (size_t i = 0; i < sites.size(); ++i) out.site_callee[i] = sites[i].callee;
+  out.site_hop.resize(sites.size());
+  for (size_t i = 0; i < sites.size(); ++i) {
+    out.site_callee[i] = sites[i].callee;
+    out.site_hop[i] = sites[i].hop;
+  }
   // stats slots: reachable call sites in document order
   for (size_t i = 0; i < sites.size(); ++i) {
     if (color[sites[i].caller] == 2) {

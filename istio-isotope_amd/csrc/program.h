@@ -31,6 +31,7 @@ struct Program {
   std::vector<int32_t> slot_site, slot_callee;  // per slot
   std::vector<int32_t> site_slot;               // per site (-1: unreachable)
   std::vector<int32_t> site_callee;             // per site
+  std::vector<uint64_t> site_hop;               // per site: hop cost H (ns)
   // draw stream (static walks whose unrolled invocation tree is <= kMaxStreamNodes)
   std::vector<Node> stream;                     // padded to a multiple of 4
   uint32_t stream_nodes = 0;                    // invocations per trace (unpadded)

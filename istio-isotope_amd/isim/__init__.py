@@ -9,3 +9,4 @@ from .native import MODE_A, MODE_B, IsimError  # noqa: F401
 from .sim import REC_DTYPE, Handler, SimParams, decode_stats, handler_from_service_graph_yaml  # noqa: F401
 from .yamljson import yaml_to_json  # noqa: F401
 from . import prometheus  # noqa: F401
+from .des import DesHandler  # noqa: F401

@@ -22,7 +22,7 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 2  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 3  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 
@@ -34,6 +34,9 @@ ST_PROM = 8
 ST_LOG2 = ST_PROM + 2 * N_PROM
 ST_SITES = ST_LOG2 + 2 * N_LOG2
 SVC_DUR_WORDS = 2 * N_PROM + 2
+# DES table row (isim.h ISIM_DES_*)
+DES_COUNT, DES_SUM_WAIT, DES_MAX_WAIT, DES_SUM_HOLD = SVC_DUR_WORDS, SVC_DUR_WORDS + 1, SVC_DUR_WORDS + 2, SVC_DUR_WORDS + 3
+DES_ROW_WORDS = SVC_DUR_WORDS + 4
 
 
 class IsimError(RuntimeError):
@@ -67,6 +70,15 @@ class LaunchInfo(C.Structure):
                 ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32)]
 
 
+class DesParams(C.Structure):
+    _fields_ = [("mean_interarrival_ns", C.c_uint64), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class DesInfo(C.Structure):
+    _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
+                ("table_rows", C.c_int32)]
+
+
 # every function declared in include/isim.h: name -> (restype, argtypes)
 _VP = C.c_void_p
 SIGNATURES = {
@@ -91,6 +103,12 @@ SIGNATURES = {
     "isim_serve": (C.c_int, [_VP, C.c_int, C.c_uint64, C.c_uint64, _VP, _VP]),
     "isim_stats_fold": (C.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "isim_stats_fold_durations": (C.c_int, [_VP, _VP, _VP]),
+    "isim_des_info_get": (C.c_int, [_VP, C.POINTER(DesInfo)]),
+    "isim_des_workspace_bytes": (C.c_int, [_VP, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "isim_serve_des_device": (C.c_int, [_VP, C.POINTER(DesParams), C.c_uint64, C.c_uint64, _VP, _VP, _VP,
+                                        _VP, C.c_uint64, _VP]),
+    "isim_serve_des": (C.c_int, [_VP, C.c_int, C.POINTER(DesParams), C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
+    "isim_des_fold": (C.c_int, [_VP, _VP, _VP]),
 }
 
 _lib = None

@@ -1,0 +1,124 @@
+"""GPU parity of the DES (BASELINE config 5): the HIP
+level-synchronous DES through the C ABI against the sequential event-driven
+C oracle — per-trace records, stats, and the per-service DES table, bit-exact."""
+import json
+
+import numpy as np
+import pytest
+
+import isim
+from isim.generators import config3_topology, realistic_topology, tree_topology
+from isim.yamljson import obj_to_json
+from oracle import des as od
+from oracle import executor as oc
+from oracle import graph_ref as gr
+from oracle.executor_py import SimGraph
+
+from parity import assert_records_equal, assert_stats_equal, oracle_params
+
+pytestmark = pytest.mark.gpu
+
+
+class DesCase:
+    def __init__(self, doc, mean_ns, **kw):
+        self.json = obj_to_json(doc) if isinstance(doc, dict) else doc
+        self.h = isim.Handler(isim.ServiceGraph.from_json(self.json), None, isim.SimParams(**kw))
+        self.d = isim.DesHandler(self.h, mean_ns)
+        self.sg = SimGraph(gr.unmarshal_service_graph(self.json))
+        self.op = oracle_params(self.h.params)
+        self.og = oc.OracleGraph(self.sg, self.op)
+        self.mean = mean_ns
+
+    def compare(self, begin, n, records=True):
+        recs, stats, table = self.d.serve(begin, n, device=0, records=records)
+        orec, ost, odes = od.run(self.sg, self.op, self.sg.entry(), begin, n, self.mean, records=records, og=self.og)
+        if records:
+            assert_records_equal(recs, orec)
+        ns, nsite = len(self.sg.g.services), len(self.sg.sites)
+        o = oc.split_stats(np.concatenate([ost, np.zeros(68 * ns, np.uint64)]), ns, nsite)
+        f = self.h.fold(stats)
+        f["svc_dur"] = None
+        assert_stats_equal(f, o)
+        rows = self.d.fold(table)
+        bad = np.argwhere(rows != odes)
+        assert bad.size == 0, f"DES table differs at (service, word) {bad[:4].tolist()}: " \
+                              f"gpu {rows[tuple(bad[0])]} oracle {odes[tuple(bad[0])]}"
+        return recs, stats, rows
+
+
+def _sleepy_tree(levels, branches, reps_leaves=1):
+    doc = tree_topology(levels, branches)
+    for s in doc["services"]:
+        s["script"] = [{"sleep": "2ms"}] + s.get("script", []) + [{"sleep": "300us"}]
+    if reps_leaves > 1:
+        for s in doc["services"]:
+            if len(s["script"]) == 2:
+                s["numReplicas"] = reps_leaves
+    return doc
+
+
+@pytest.mark.parametrize("mean", [300_000, 2_500_000, 40_000_000])
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_realistic_loads(gpu, mean, mode):
+    c = DesCase(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.05)), mean,
+                error_mode=mode)
+    recs, _, rows = c.compare(3, 5000)
+    if mean == 300_000:
+        assert rows[:, isim.native.DES_SUM_WAIT].sum() > 0
+
+
+@pytest.mark.parametrize("n", [1, 2, 1023, 8191, 8192, 8193, 20000])
+def test_ragged_batches(gpu, n):
+    DesCase(_sleepy_tree(3, 3), 1_000_000, ).compare(1 << 33, n)  # trace ids past 2^32
+
+
+@pytest.mark.parametrize("reps", [2, 5, 64])
+def test_leaf_replicas(gpu, reps):
+    DesCase(_sleepy_tree(3, 4, reps), 700_000).compare(0, 12000)
+
+
+def test_error_rate_extremes(gpu):
+    doc = _sleepy_tree(4, 3)
+    for i, s in enumerate(doc["services"]):
+        s["errorRate"] = [0, 1, 0.5][i % 3]
+    DesCase(doc, 1_500_000, error_mode=isim.MODE_B).compare(0, 3000)
+    DesCase(doc, 1_500_000, error_mode=isim.MODE_A).compare(0, 3000)
+
+
+def test_zero_traces(gpu):
+    c = DesCase(_sleepy_tree(2, 2), 1_000_000)
+    recs, stats, table = c.d.serve(0, 0)
+    assert stats.sum() == 0 and table.sum() == 0
+
+
+def test_config5_slice(gpu):
+    # the config-5 graph (BASELINE config 3's 10k services), a batch the oracle finishes quickly
+    c = DesCase(config3_topology(), 6_000_000)
+    c.compare(0, 256)
+
+
+def test_device_entry_accumulates(gpu):
+    import torch
+    c = DesCase(_sleepy_tree(3, 3), 900_000)
+    n = 5000
+    dev = torch.device("cuda", 0)
+    rec = torch.zeros(n * 2, dtype=torch.int64, device=dev)
+    st = torch.zeros(c.h.stats_words, dtype=torch.int64, device=dev)
+    tab = torch.zeros(max(1, c.d.table_words), dtype=torch.int64, device=dev)
+    wsb = c.d.workspace_bytes(n)
+    ws = torch.empty(wsb // 8 + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for half in (0, 1):  # two batches accumulate into the same stats/table
+        c.d.serve_device(half * n, n, rec.data_ptr(), st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s)
+    torch.cuda.synchronize()
+    _, s0, t0 = c.d.serve(0, n, records=False)
+    _, s1, t1 = c.d.serve(n, n, records=False)
+    stg = st.cpu().numpy().view(np.uint64)
+    assert int(stg[0]) == 2 * n
+    assert int(stg[isim.native.ST_SUM_LATENCY]) == int(s0[1]) + int(s1[1])
+    W = isim.native.DES_ROW_WORDS
+    tg = tab.cpu().numpy().view(np.uint64)[:t0.size].reshape(-1, W)
+    want = (t0 + t1).reshape(-1, W)
+    mw = isim.native.DES_MAX_WAIT  # the longest wait merges with max
+    want[:, mw] = np.maximum(t0.reshape(-1, W)[:, mw], t1.reshape(-1, W)[:, mw])
+    assert np.array_equal(tg, want)
