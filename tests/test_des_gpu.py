@@ -46,13 +46,13 @@ class DesCase:
         return recs, stats, rows
 
 
-def _sleepy_tree(levels, branches, reps_leaves=1):
+def _sleepy_tree(levels, branches, reps_leaves=1, post=True):
     doc = tree_topology(levels, branches)
     for s in doc["services"]:
-        s["script"] = [{"sleep": "2ms"}] + s.get("script", []) + [{"sleep": "300us"}]
+        s["script"] = [{"sleep": "2ms"}] + s.get("script", []) + ([{"sleep": "300us"}] if post else [])
     if reps_leaves > 1:
         for s in doc["services"]:
-            if len(s["script"]) == 2:
+            if not any(isinstance(x, list) for x in s["script"]):
                 s["numReplicas"] = reps_leaves
     return doc
 
@@ -78,11 +78,18 @@ def test_leaf_replicas(gpu, reps):
 
 
 def test_error_rate_extremes(gpu):
-    doc = _sleepy_tree(4, 3)
+    # mode B static walks have no step after a step that can fail: no post-call sleeps
+    doc = _sleepy_tree(4, 3, post=False)
     for i, s in enumerate(doc["services"]):
         s["errorRate"] = [0, 1, 0.5][i % 3]
     DesCase(doc, 1_500_000, error_mode=isim.MODE_B).compare(0, 3000)
     DesCase(doc, 1_500_000, error_mode=isim.MODE_A).compare(0, 3000)
+    doc = _sleepy_tree(4, 3)
+    for i, s in enumerate(doc["services"]):
+        s["errorRate"] = [0, 1, 0.5][i % 3]
+    DesCase(doc, 1_500_000, error_mode=isim.MODE_A).compare(0, 3000)
+    with pytest.raises(isim.IsimError):  # a failing call step followed by a sleep is not a static walk
+        DesCase(doc, 1_500_000, error_mode=isim.MODE_B)
 
 
 def test_zero_traces(gpu):
