@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--mean-interarrival-ns", type=int, default=6_000_000,
+                    help="c5 (DES): mean gap of the open-loop Poisson arrivals")
     ap.add_argument("--mode", default="A", choices=["A", "B"])
     ap.add_argument("--no-records", action="store_true")
     ap.add_argument("--no-svc-dur", action="store_true",
@@ -63,6 +65,12 @@ def build_graph(config: str):
         j = obj_to_json(mesh_topology())
         desc = {"workload": "100k-service 8-layer mesh, fan-out 3 at probability 30, numReplicas + responseSize",
                 "services": 100000}
+    elif config == "c5":
+        j = obj_to_json(config3_topology())
+        desc = {"workload": "config 3's 10k-service graph + per-replica worker-pool contention: open-loop Poisson "
+                            "arrivals, one FIFO worker per replica held for the service's sleep (DES v1, DESIGN.md "
+                            "§10), level-synchronous exact DES",
+                "services": 10000}
     else:
         j = obj_to_json(config3_topology())
         desc = {"workload": "create_realistic_topology.py multitier Barabasi 10k services, concurrent fan-out, "
@@ -91,6 +99,119 @@ def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
             "sample": f"{n_traces} traces of the same workload (trace ids from {trace_begin}), "
                       f"C oracle oracle/isim_oracle.c with OpenMP, {dt:.1f} s",
             "hop_visits_per_s": float(st[2]) / dt}
+
+
+def cpu_baseline_des(json_text: str, params, mean_ns: int, n_traces: int):
+    """The DES oracle (oracle/des_oracle.c: sequential event-driven, one core)."""
+    from oracle import des as od
+    from oracle import graph_ref as gr
+    from oracle.executor_py import SimGraph
+    from oracle.executor_py import SimParams as OParams
+    sg = SimGraph(gr.unmarshal_service_graph(json_text))
+    op = OParams(params.seed, params.hop_base_ns, params.req_ps_per_byte, params.resp_ps_per_byte,
+                 params.error_mode)
+    n = n_traces or 2048
+    t0 = time.perf_counter()
+    _, st, _ = od.run(sg, op, sg.entry(), 0, n, mean_ns, records=False)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "traces/s", "cores": 1, "kind": "port",
+            "sample": f"{n} traces of the same DES workload (trace ids from 0, arrivals from time 0), "
+                      f"event-driven C oracle oracle/des_oracle.c (binary heap, sequential), {dt:.1f} s",
+            "hop_visits_per_s": float(st[2]) / dt}
+
+
+def main_des(args, h, json_text, desc, params, rank, world, dev):
+    """BASELINE config 5: one step = one DES batch of --batch traces per rank
+    (arrivals from time 0, replicas idle), all kernels on one stream.  The DES
+    does not shard a batch: with N ranks each runs an independent replica
+    (its own trace ids, i.e. its own arrival stream) and the stats are summed
+    with one RCCL all-reduce ("replicas only")."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import isim
+    from isim.dist import merge_stats, shard_begin
+
+    d = isim.DesHandler(h, args.mean_interarrival_ns)
+    B = args.batch
+    wsb = d.workspace_bytes(B)
+    ws = torch.empty(wsb // 8 + 1, dtype=torch.int64, device=dev)
+    stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
+    table = torch.zeros(max(1, d.table_words), dtype=torch.int64, device=dev)
+    recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step(s):
+        begin = shard_begin(rank, world, s, B)
+        d.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), table.data_ptr(),
+                       ws.data_ptr(), wsb, sptr)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    stats.zero_()
+    table.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step(args.warmup + i)
+        ev[i][1].record(stream)
+    if world > 1:
+        merge_stats(stats)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    folded = h.fold(stats.cpu().numpy().view(np.uint64))
+    total = args.steps * B * world
+    assert folded["n_traces"] == total, (folded["n_traces"], total)
+    value = total / elapsed
+    npos = d.info.n_positions
+    # algorithmic bytes of one step (DESIGN.md §10.4): down pass 16 B and up
+    # pass 24 B per (position, trace), 8 B per (child edge, trace), arrivals /
+    # finalize / records ~60 B per trace
+    alg_bytes = B * (40 * npos + 8 * (npos - 1) + 44 + (0 if args.no_records else 16))
+    achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
+    rows = d.fold(table.cpu().numpy().view(np.uint64))
+    W = isim.native
+    mean_wait = float(rows[:, W.DES_SUM_WAIT].sum()) / max(1, int(rows[:, W.DES_COUNT].sum()))
+    line = {
+        "metric": "simulated request traces/sec (node), config c5 (DES)",
+        "value": value, "unit": "traces/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": dict(desc, global_batch=B * world, traces_per_rank_per_step=B, error_mode=args.mode,
+                       hop_visits_per_trace=folded["sum_hops"] / total,
+                       mean_interarrival_ns=args.mean_interarrival_ns,
+                       parallelism=f"replicas x{world}", records=not args.no_records,
+                       des_levels=d.info.n_levels, des_max_width=d.info.max_width,
+                       workspace_bytes=wsb),
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "des_* (arrivals, down and up passes of all levels, finalize) per step",
+                     "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+        "mean_latency_ns": folded["sum_latency"] / total,
+        "mean_queue_wait_ns": mean_wait,
+        "hop_visits_per_s": value * folded["sum_hops"] / total,
+        "n_500_frac": folded["n_500"] / total,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_des(json_text, params, args.mean_interarrival_ns, args.cpu_traces)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def compute_roofline(stream: bool, info, B: int, kern_ms: float):
@@ -131,6 +252,10 @@ def main():
     params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A,
                             flags=isim.native.FLAG_NO_SVC_DUR if args.no_svc_dur else 0)
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
+    if args.config == "c5":
+        if args.batch == 1 << 22:
+            args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
+        return main_des(args, h, json_text, desc, params, rank, world, dev)
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
     B = args.batch
