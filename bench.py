@@ -304,7 +304,7 @@ def main():
 
     # algorithmic bytes of one launch: 16 B records per trace + program read + stats written
     # (the draw stream is 8 B per invocation, padded to groups of 4; the interpreter 32 B per instruction)
-    stream = launch["kernel_kind"] == 4
+    stream = launch["kernel_kind"] >= 4
     prog_bytes = (-(-info.hops_upper // 4) * 4 * 8 + info.n_slots * 4) if stream else info.program_len * 32
     alg_bytes = B * (0 if args.no_records else 16) + prog_bytes + info.stats_words * 8
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9

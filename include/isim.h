@@ -153,7 +153,8 @@ typedef struct {
   int32_t lds_counters;      /* 1: per-site counters in LDS; 0: global atomics */
   int32_t blocks_per_cu;     /* resident workgroups per CU (occupancy query) */
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
-  int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream */
+  int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
+                                5 draw stream with the mode-B bit stack (call depth <= 32) */
 } isim_launch_info;
 
 ISIM_API const char *isim_last_error(void);

@@ -139,6 +139,8 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   st.lds_counters = counters ? 1u : 0u;
   st.kind = p.stream_nodes ? 4u : (p.static_walk ? 0u : 2u) + (p.time_bits == 64 ? 1u : 0u);
   if ((h->params.flags & ISIM_FLAG_NO_STREAM) && st.kind == 4) st.kind = p.time_bits == 64 ? 1u : 0u;
+  // mode B on the draw stream: the per-lane bit stack holds 32 stack positions
+  if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B && p.max_depth <= 32) st.kind = 5;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
   HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)st.lds_bytes));
@@ -148,15 +150,15 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   if (per_cu < 1) return fail(ISIM_EHIP, "walk kernel cannot be resident (occupancy 0)");
   st.per_cu = (uint32_t)per_cu;
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-  const void *src = st.kind == 4 ? (const void *)p.stream.data() : (const void *)p.code.data();
-  const size_t bytes = st.kind == 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
+  const void *src = st.kind >= 4 ? (const void *)p.stream.data() : (const void *)p.code.data();
+  const size_t bytes = st.kind >= 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
   // the draw-stream kernel prefetches group g+1 unconditionally: two zero
   // groups (32 B each) of tail padding keep those reads inside the buffer
-  const size_t tail = st.kind == 4 ? 2 * 4 * sizeof(isim::Node) : 0;
+  const size_t tail = st.kind >= 4 ? 2 * 4 * sizeof(isim::Node) : 0;
   HIPCHK(hipMalloc(&st.d_prog, bytes + tail));
   HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
   if (tail) HIPCHK(hipMemset((char *)st.d_prog + bytes, 0, tail));
-  if (st.kind == 4 && p.n_slots > 0) {
+  if (st.kind >= 4 && p.n_slots > 0) {
     HIPCHK(hipMalloc(&st.d_mult, p.stream_mult.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_mult, p.stream_mult.data(), p.stream_mult.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
@@ -356,7 +358,7 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   kp.t_static = h->prog.max_latency;
   kp.svc_dur = svc_dur_rows(h) ? 1u : 0u;
   kp.root_dur = h->prog.root_dur;
-  const uint64_t per_wave = st->kind == 4 ? isim::stream_traces_per_wave() : 64u;
+  const uint64_t per_wave = st->kind >= 4 ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
@@ -366,7 +368,7 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
   HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
                          (hipStream_t)hip_stream));
-  if (st->kind == 4 && h->prog.n_slots > 0) {
+  if (st->kind >= 4 && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;
     void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};

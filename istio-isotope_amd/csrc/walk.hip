@@ -720,10 +720,15 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
 #define ISIM_FAST_A 1
 #endif
 
+
 // TPL traces per lane: the wave walks 64*TPL traces through one pass over the
 // stream, so the per-record scalar work (fetch, decode, counter adds) is
 // shared and each lane runs TPL independent Philox chains (ILP).
-template <bool MODEB, bool LDSC, int TPL, bool FULL>
+// BS: mode B keeps the open invocations' statuses in a per-lane bit stack
+// (bit p = running status of the frame at stack position p; VALU), for
+// call depths <= 32 (kernel kind 5); otherwise (kind 4) as wave masks on a
+// VGPR-lane stack.
+template <bool MODEB, bool LDSC, int TPL, bool FULL, bool BS>
 __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ stream, uint32_t n_groups,
                                             uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
                                             uint64_t n_traces, uint64_t base) {
@@ -752,13 +757,28 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
   uint32_t top_slot = 0, depth = 0;
   LaneStack<uint64_t> s_mask[TPL];
   LaneStack<uint32_t> s_slot;
+  // mode B, bit-stack form (BS): per lane and trace, bit p of stk_lo = the
+  // running 500 status of the open frame at stack position p (p < 32)
+  uint32_t stk_lo[TPL];
 #pragma unroll
   for (int u = 0; u < TPL; ++u) {
     errh[u] = 0;
     root_st[u] = 0;
     top[u] = 0;
+    stk_lo[u] = 0;
   }
-
+  // set / test / clear bit p (wave-uniform, < 32) in the lanes of mask m: VALU only
+  auto bs_set = [&](int u, uint32_t p, uint64_t m) {
+    const uint32_t b = 1u << (p & 31u);
+    stk_lo[u] |= lane_in(m) ? b : 0u;
+  };
+  auto bs_test = [&](int u, uint32_t p) -> uint64_t {
+    const uint32_t b = 1u << (p & 31u);
+    return ballot((stk_lo[u] & b) != 0u);
+  };
+  auto bs_clear = [&](int u, uint32_t p) {
+    stk_lo[u] &= ~(1u << (p & 31u));
+  };
   auto node = [&](uint32_t thr, uint32_t meta, const uint32_t (&xw)[TPL]) {
     const uint32_t slot = meta & 0xFFFFFFu;
     uint64_t own[TPL];
@@ -777,6 +797,68 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
         n += popc(own[u]);
       }
       if (any) count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, n, lane0);
+    } else if constexpr (BS) {
+      if (slot == kSlotPad) return;
+      uint32_t k = (meta >> 24) & 0x7Fu;
+      const uint32_t d = depth;  // this invocation's stack position
+      if (k > 0) {
+        // a leaf opens and closes here: its status is its own draw; it
+        // fails the caller (the open frame at d-1) in mode B
+        uint64_t any = 0;
+        uint32_t n = 0;
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) {
+          errh[u] += lane_in(own[u]) ? 1u : 0u;
+          any |= own[u];
+          n += popc(own[u]);
+        }
+        if (d == 0) {
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) root_st[u] = own[u];
+        } else if (any) {
+          count_t<LDSC>(c.gstats, c.cnt, c.n_slots + slot, n, lane0);
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) bs_set(u, d - 1, own[u]);
+        }
+        --k;
+      } else {
+        uint64_t any = 0;
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) any |= own[u];
+        if (any) {
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) bs_set(u, d, own[u]);
+        }
+        s_slot.put(d, slot);
+        depth = d + 1;
+      }
+      for (; k > 0; --k) {  // the frame at position depth-1 closes
+        const uint32_t p = depth - 1;
+        uint64_t st[TPL], any = 0;
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) {
+          st[u] = bs_test(u, p);
+          any |= st[u];
+        }
+        if (p == 0) {
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) {
+            root_st[u] = st[u];
+            errh[u] += lane_in(st[u]) ? 1u : 0u;
+          }
+        } else if (any) {
+          uint32_t n = 0;
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) {
+            errh[u] += lane_in(st[u]) ? 1u : 0u;
+            n += popc(st[u]);
+            bs_set(u, p - 1, st[u]);  // mode B: a 500 fails the caller
+            bs_clear(u, p);
+          }
+          count_t<LDSC>(c.gstats, c.cnt, c.n_slots + s_slot.get(p), n, lane0);
+        }
+        depth = p;
+      }
     } else {
       if (slot == kSlotPad) return;
       uint32_t k = (meta >> 24) & 0x7Fu;
@@ -927,14 +1009,15 @@ __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_
   if (i < n_slots) gstats[ISIM_ST_SITES + i] += (uint64_t)mult[i] * n_traces;
 }
 
-// KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream
+// KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream,
+// 5 draw stream with the mode-B bit stack (call depth <= 32)
 // LDSC: per-site counters in the workgroup LDS table (else global atomics)
 template <int KIND, bool MODEB, bool LDSC>
-__global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
+__global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
     isim_walk(const Ins *__restrict__ prog, isim_trace_rec *__restrict__ records, uint64_t *__restrict__ gstats,
               const uint32_t *__restrict__ dur, KParams kp) {
   using TT = typename std::conditional<KIND == 0 || KIND == 2, uint32_t, uint64_t>::type;
-  constexpr bool STATIC = KIND < 2 || KIND == 4;
+  constexpr bool STATIC = KIND < 2 || KIND >= 4;
   extern __shared__ __align__(16) unsigned char lds[];
   Ctx c;
   c.prog = prog;
@@ -965,19 +1048,19 @@ __global__ void __launch_bounds__(kWgThreads, KIND == 4 ? ISIM_STREAM_WAVES : 1)
   for (uint32_t i = threadIdx.x; i < zero_words; i += blockDim.x) z[i] = 0;
   __syncthreads();
 
-  constexpr uint64_t kBatch = KIND == 4 ? 64ull * kStreamTPL : 64ull;
+  constexpr uint64_t kBatch = KIND >= 4 ? 64ull * kStreamTPL : 64ull;
   const uint64_t n_batches = (kp.n_traces + kBatch - 1) / kBatch;
   const uint64_t stride = (uint64_t)gridDim.x * waves;
   for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
-    if constexpr (KIND == 4) {
+    if constexpr (KIND >= 4) {
       const uint64_t base = b * 64 * kStreamTPL;
       CNode4 *st = (CNode4 *)(const __attribute__((address_space(1))) Ins *)prog;
       const uint32_t ng = kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0;
       if (base + 64 * kStreamTPL <= kp.n_traces)  // every lane of every trace slot valid
-        walk_stream<MODEB, LDSC, kStreamTPL, true>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
+        walk_stream<MODEB, LDSC, kStreamTPL, true, KIND == 5>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
                                                    kp.n_traces, base);
       else
-        walk_stream<MODEB, LDSC, kStreamTPL, false>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
+        walk_stream<MODEB, LDSC, kStreamTPL, false, KIND == 5>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
                                                     kp.n_traces, base);
     }
     else if constexpr (STATIC) walk_static<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64);
@@ -1019,7 +1102,10 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters) {
     case 1: return pick<1>(modeb, lds_counters);
     case 2: return pick<2>(modeb, lds_counters);
     case 3: return pick<3>(modeb, lds_counters);
-    default: return pick<4>(modeb, lds_counters);
+    case 4: return pick<4>(modeb, lds_counters);
+    default:  // the bit stack only exists in mode B
+      if (!modeb) return pick<4>(false, lds_counters);
+      return lds_counters ? (void *)&dev::isim_walk<5, true, true> : (void *)&dev::isim_walk<5, true, false>;
   }
 }
 

@@ -37,7 +37,8 @@ def test_reference_topologies(gpu, path, mode, kernel):
     kind = c.handler.launch_info(0)["kernel_kind"]
     tb64 = c.handler.info.time_bits == 64
     if c.handler.info.static_walk:
-        assert kind == (4 if kernel == "stream" else int(tb64))
+        bs = mode == isim.MODE_B and c.handler.info.max_depth <= 32
+        assert kind == ((5 if bs else 4) if kernel == "stream" else int(tb64))
     else:
         assert kind == 2 + int(tb64)
     c.compare(0, 3000)
@@ -133,3 +134,23 @@ def test_mesh_config4(gpu):
     j = obj_to_json(mesh_topology(n_services=8000, layers=8, fanout=3, probability=30, seed=11))
     c = Case(with_defaults(j, errorRate=0.02))
     c.compare(0, 20000)
+
+
+def _chain(n, fan=2):
+    """svc-0 -> svc-1 -> ... -> svc-(n-1), each link also calling `fan` leaves."""
+    svcs = []
+    for i in range(n):
+        calls = [[{"call": f"c{i + 1}"}] + [{"call": f"l{i}-{j}"} for j in range(fan)]] if i + 1 < n else []
+        svcs.append({"name": f"c{i}", "script": [{"sleep": "1us"}] + calls, "errorRate": 0.02})
+        svcs += [{"name": f"l{i}-{j}", "errorRate": 0.03} for j in range(fan)]
+    svcs[0]["isEntrypoint"] = True
+    return json.dumps({"services": svcs})
+
+
+@pytest.mark.parametrize("depth,kind", [(31, 5), (32, 5), (33, 4), (64, 4)])
+def test_mode_b_stack_depths(gpu, depth, kind):
+    # the bit-stack kernel (kind 5) holds 32 stack positions; deeper graphs take kind 4
+    c = Case(_chain(depth), None, isim.SimParams(error_mode=isim.MODE_B))
+    assert c.handler.info.max_depth == depth
+    assert c.handler.launch_info(0)["kernel_kind"] == kind
+    c.compare(5, 3000)
