@@ -538,7 +538,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.d_level_pos = st->d_des_level;
   L.level_off = d.level_off;
   L.W = (uint64_t *)ws;
-  ws += al((uint64_t)np * n_traces * 8);
+  ws += al((uint64_t)np * ((n_traces + 7) & ~7ull) * 8);
   L.A = (uint64_t *)ws;
   ws += al(n_traces * 8);
   L.E = (uint32_t *)ws;

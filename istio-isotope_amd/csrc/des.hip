@@ -98,6 +98,7 @@ struct DesK {
   uint64_t *table;  // [rows][ISIM_DES_ROW_WORDS]
   isim_trace_rec *records;
   uint64_t N, trace_begin, mean_ns;
+  uint64_t ld;  // row stride of W in traces: N rounded up to 8 (64-B aligned rows)
   uint32_t k0, k1;
   uint32_t n_pos, n_slots;
   uint32_t level_begin, splits;
@@ -226,20 +227,31 @@ __global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t N = k.N;
-  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * N;
+  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
   const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
-  uint64_t *out = k.W + (uint64_t)v * N;
+  uint64_t *out = k.W + (uint64_t)v * k.ld;
   uint64_t wsum = 0, wmax = 0;
   for (uint64_t c0 = 0; c0 < N; c0 += kDesChunk) {
     const uint64_t base = c0 + (uint64_t)threadIdx.x * kDesPer;
     uint64_t a[kDesPer];
     uint32_t rr[kDesPer];
+    if (base + kDesPer <= N) {
+      // 8 consecutive traces = 64 B per thread: four 16-B loads (rows are 64-B aligned)
+      const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(par + base);
 #pragma unroll
-    for (uint32_t i = 0; i < kDesPer; ++i) {
-      const uint64_t t = base + i;
-      a[i] = t < N ? par[t] + off : 0;
-      rr[i] = (t < N && reps > 1) ? des_draw(k.trace_begin + t, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
+      for (uint32_t i = 0; i < kDesPer / 2; ++i) {
+        const ulonglong2 x = q[i];
+        a[2 * i] = x.x + off;
+        a[2 * i + 1] = x.y + off;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < kDesPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
     }
+#pragma unroll
+    for (uint32_t i = 0; i < kDesPer; ++i)
+      rr[i] = (base + i < N && reps > 1) ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps
+                                         : 0u;
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
 #pragma unroll
@@ -252,17 +264,28 @@ __global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
       const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
       const uint64_t cin = carry[r];
       uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+      uint64_t Sv[kDesPer];
 #pragma unroll
       for (uint32_t i = 0; i < kDesPer; ++i) {
         const uint64_t t = base + i;
+        Sv[i] = 0;
         if (t < N && rr[i] == r) {
           const uint64_t S = x > a[i] ? x : a[i];
-          out[t] = S;
+          Sv[i] = S;
           const uint64_t w = S - a[i];
           wsum += w;
           wmax = w > wmax ? w : wmax;
           x = S + P.hold;
         }
+      }
+      if (reps == 1 && base + kDesPer <= N) {
+        ulonglong2 *q = reinterpret_cast<ulonglong2 *>(out + base);
+#pragma unroll
+        for (uint32_t i = 0; i < kDesPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < kDesPer; ++i)
+          if (base + i < N && rr[i] == r) out[base + i] = Sv[i];
       }
       __syncthreads();
       if (threadIdx.x == kDesThreads - 1) carry[r] = x;
@@ -305,42 +328,58 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
   const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
-  const uint64_t *mine = k.W + (uint64_t)v * N;
-  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * N;
+  uint64_t *mine = k.W + (uint64_t)v * k.ld;
+  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
   const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
   const bool leaf = P.flags & kDesFlagLeaf;
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
-  for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
-    const uint64_t S = mine[t];
-    uint64_t F;
-    uint32_t sto = 0;
-    if (leaf) {
-      F = S + P.floor;
-    } else {
-      uint64_t m = S + P.floor;
+  constexpr uint32_t U = 4;  // independent traces per thread per iteration (memory-level parallelism)
+  for (uint64_t t0 = tb + threadIdx.x; t0 < te; t0 += U * kDesUpThreads) {
+    uint64_t S[U], a[U], m[U];
+    uint32_t sto[U];
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint64_t t = t0 + j * kDesUpThreads;
+      const bool ok = t < te;
+      S[j] = ok ? mine[t] : 0;
+      a[j] = ok ? par[t] + off : 0;
+      sto[j] = 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) m[j] = S[j] + P.floor;
+    if (!leaf) {
       for (uint32_t c = 0; c < P.child_cnt; ++c) {
-        const uint64_t fc = k.W[(uint64_t)k.child[P.child_off + c] * N + t];
-        const uint64_t tc = fc & kMask63;
-        m = tc > m ? tc : m;
-        sto |= (uint32_t)(fc >> 63);
+        const uint64_t *fc = k.W + (uint64_t)k.child[P.child_off + c] * k.ld;
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) {
+          const uint64_t t = t0 + j * kDesUpThreads;
+          const uint64_t f = t < te ? fc[t] : 0;
+          const uint64_t tc = f & kMask63;
+          m[j] = tc > m[j] ? tc : m[j];
+          sto[j] |= (uint32_t)(f >> 63);
+        }
       }
-      F = m + P.post;
     }
-    uint32_t own = 0;
-    if (P.flags & kDesFlagAlways) own = 1;
-    else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
-    const uint32_t st = k.modeb ? (own | sto) : own;
-    const uint64_t a = par[t] + off;
-    const uint64_t dur = F - a;
-    ((uint64_t *)mine)[t] = F | ((uint64_t)st << 63);
-    if (st) {
-      atomicAdd(k.E + t, 1u);
-      n500 += 1;
-      dsum1 += dur;
-    } else {
-      dsum0 += dur;
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint64_t t = t0 + j * kDesUpThreads;
+      if (t >= te) continue;
+      const uint64_t F = leaf ? m[j] : m[j] + P.post;
+      uint32_t own = 0;
+      if (P.flags & kDesFlagAlways) own = 1;
+      else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
+      const uint32_t st = k.modeb ? (own | sto[j]) : own;
+      const uint64_t dur = F - a[j];
+      mine[t] = F | ((uint64_t)st << 63);
+      if (st) {
+        atomicAdd(k.E + t, 1u);
+        n500 += 1;
+        dsum1 += dur;
+      } else {
+        dsum0 += dur;
+      }
+      atomicAdd(&hist[st * ISIM_N_PROM + des_prom_bucket(dur)], 1u);
     }
-    atomicAdd(&hist[st * ISIM_N_PROM + des_prom_bucket(dur)], 1u);
   }
 #pragma unroll
   for (uint32_t d = 32; d > 0; d >>= 1) {
@@ -453,7 +492,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
 uint64_t des_workspace_bytes(uint32_t n_pos, uint64_t n) {
   const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-  return al((uint64_t)n_pos * n * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8);
+  return al((uint64_t)n_pos * ((n + 7) & ~7ull) * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8);
 }
 
 int des_launch(const DesLaunch &L, void *stream_) {
@@ -471,6 +510,7 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.table = L.d_table;
   k.records = L.d_records;
   k.N = L.n_traces;
+  k.ld = (L.n_traces + 7) & ~7ull;
   k.trace_begin = L.trace_begin;
   k.mean_ns = L.mean_ns;
   k.k0 = (uint32_t)L.seed;
