@@ -183,6 +183,15 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
     # finalize / records ~60 B per trace
     alg_bytes = B * (40 * npos + 8 * (npos - 1) + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary_c5.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("batch") == B:
+                traffic = pmc.get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
     rows = d.fold(table.cpu().numpy().view(np.uint64))
     W = isim.native
     mean_wait = float(rows[:, W.DES_SUM_WAIT].sum()) / max(1, int(rows[:, W.DES_COUNT].sum()))
@@ -198,7 +207,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
                        des_levels=d.info.n_levels, des_max_width=d.info.max_width,
                        workspace_bytes=wsb),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "des_* (arrivals, down and up passes of all levels, finalize) per step",
                      "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
         "mean_latency_ns": folded["sum_latency"] / total,
