@@ -49,6 +49,7 @@ struct DevState {
   // DES (config 5): the plan uploaded on first use
   void *d_des_pos = nullptr;
   uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
+  uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr;
 };
 
 }  // namespace
@@ -77,6 +78,8 @@ struct isim_handler {
         (void)hipFree(kv.second.d_des_child);
         (void)hipFree(kv.second.d_des_level);
         (void)hipFree(kv.second.d_des_mult);
+        (void)hipFree(kv.second.d_des_fast);
+        (void)hipFree(kv.second.d_des_sort);
         (void)hipSetDevice(cur);
       }
     }
@@ -485,7 +488,9 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
   if (!up(&st->d_des_pos, d.pos.data(), d.pos.size() * sizeof(isim::DesPos)) ||
       !up((void **)&st->d_des_child, d.child.data(), d.child.size() * 4) ||
       !up((void **)&st->d_des_level, d.level_pos.data(), d.level_pos.size() * 4) ||
-      !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4))
+      !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4) ||
+      !up((void **)&st->d_des_fast, d.fast_pos.data(), d.fast_pos.size() * 4) ||
+      !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4))
     return fail(ISIM_EHIP, "DES plan upload failed");
   return ISIM_OK;
 }
@@ -508,7 +513,7 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
 int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
   if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
   if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
-  *bytes = isim::des_workspace_bytes((uint32_t)h->des.pos.size(), n_traces);
+  *bytes = isim::des_workspace_bytes(h->des, n_traces);
   return ISIM_OK;
 }
 
@@ -528,15 +533,19 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   if (rc != ISIM_OK) return rc;
   const isim::DesPlan &d = h->des;
   const uint32_t np = (uint32_t)d.pos.size();
-  if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(np, n_traces))
+  if (n_traces * (uint64_t)std::max<uint32_t>(1, d.max_sort_pos) > 0xFFFFFFFFull)
+    return fail(ISIM_EINVAL, "n_traces x positions of one service above 2^32 per DES batch");
+  if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(d, n_traces))
     return fail(ISIM_EINVAL, "DES workspace smaller than isim_des_workspace_bytes()");
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   char *ws = (char *)d_workspace;
   isim::DesLaunch L;
+  L.plan = &d;
   L.d_pos = st->d_des_pos;
   L.d_child = st->d_des_child;
   L.d_level_pos = st->d_des_level;
-  L.level_off = d.level_off;
+  L.d_fast_pos = st->d_des_fast;
+  L.d_sort_pos = st->d_des_sort;
   L.W = (uint64_t *)ws;
   ws += al((uint64_t)np * ((n_traces + 7) & ~7ull) * 8);
   L.A = (uint64_t *)ws;
@@ -544,6 +553,8 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.E = (uint32_t *)ws;
   ws += al(n_traces * 4);
   L.blk = (uint64_t *)ws;
+  ws += al(((n_traces + 8191) / 8192 + 1) * 8);
+  L.sort_ws = ws;
   L.d_stats = d_stats;
   L.d_table = d_des_table;
   L.d_records = d_records;
@@ -574,7 +585,7 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
   HIPCHK(hipSetDevice(device));
   const uint64_t words = stats_words(h);
   const uint64_t tab_words = (uint64_t)h->prog.row_svc.size() * ISIM_DES_ROW_WORDS;
-  const uint64_t ws_bytes = isim::des_workspace_bytes((uint32_t)h->des.pos.size(), n_traces);
+  const uint64_t ws_bytes = isim::des_workspace_bytes(h->des, n_traces);
   uint64_t *d_stats = nullptr, *d_tab = nullptr;
   void *d_ws = nullptr;
   isim_trace_rec *d_rec = nullptr;

@@ -39,34 +39,53 @@ struct DesPos {
 };
 static_assert(sizeof(DesPos) == 64, "DesPos must be 64 bytes");
 
+// A service whose queue needs the sort path: several
+// positions per trace, or arrivals not in trace order (a caller upstream
+// has replicas).
+struct DesSortSvc {
+  uint32_t row;       // duration-table row
+  uint32_t reps;      // replicas
+  uint32_t pos_off;   // its positions in DesPlan::sort_pos (hop order)
+  uint32_t pos_cnt;
+  uint64_t hold;      // worker hold time
+};
+
 struct DesPlan {
   std::vector<DesPos> pos;           // hop order (position 0 = the entry)
   std::vector<uint32_t> child;       // children lists (positions)
-  std::vector<uint32_t> level_pos;   // positions grouped by depth
+  std::vector<uint32_t> level_pos;   // positions grouped by depth (up pass)
   std::vector<uint32_t> level_off;   // [n_levels + 1]
   std::vector<uint32_t> slot_mult;   // per slot: calls through it per trace
-  uint32_t max_width = 0;            // widest level
+  uint32_t max_width = 0;            // widest depth level
+  // down pass, by service level (longest call path from the entry):
+  std::vector<uint32_t> fast_pos;    // positions of single-position, trace-ordered services
+  std::vector<uint32_t> fast_off;    // [n_slevels + 1]
+  std::vector<DesSortSvc> sorted;    // sort-path services
+  std::vector<uint32_t> sorted_off;  // [n_slevels + 1]
+  std::vector<uint32_t> sort_pos;    // positions of the sort-path services
+  uint32_t max_sort_pos = 0;         // most positions of one sort-path service
 };
 
 // Device buffers and sizes of one DES batch (des.hip: des_launch).
 struct DesLaunch {
+  const DesPlan *plan;               // host copy (level offsets, sort-path services)
   const void *d_pos;                 // DesPos[n_pos]
-  const uint32_t *d_child, *d_level_pos;
-  std::vector<uint32_t> level_off;   // host copy
+  const uint32_t *d_child, *d_level_pos, *d_fast_pos, *d_sort_pos;
   uint64_t *W, *A, *blk;             // workspace: [n_pos][N], [N], chunk sums
   uint32_t *E;                       // workspace: [N]
+  void *sort_ws;                     // workspace of the sort path (keys, values, radix-sort temp)
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;         // may be null
   uint64_t n_traces, trace_begin, mean_ns, seed;
   uint32_t n_pos, n_slots, modeb;
 };
 
-// Workspace bytes for a batch of n traces (W, A, E, chunk sums; 256-B aligned parts).
-uint64_t des_workspace_bytes(uint32_t n_pos, uint64_t n);
+// Workspace bytes for a batch of n traces (W, A, E, chunk sums, sort path; 256-B aligned parts).
+uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n);
 int des_launch(const DesLaunch &L, void *stream);
 
 // Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is
-// outside the DES v1 class.
+// outside the DES class.
 int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err);
 
 // -ln(w / 2^24), w = (u >> 8) + 1, in Q24 fixed point:

@@ -22,6 +22,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "des.h"
 #include "kernel_abi.h"
 
@@ -103,6 +106,13 @@ struct DesK {
   uint32_t n_pos, n_slots;
   uint32_t level_begin, splits;
   uint32_t modeb, n_blk;
+  // sort path: the service being queued and its sorted arrivals
+  const uint32_t *sort_pos;
+  DesSortSvc svc;
+  const uint64_t *skeys;
+  const uint32_t *svals;
+  uint64_t *keys;
+  uint32_t *vals;
 };
 
 // (B, C) represents x -> max(x + B, C); `then` composes a after b.
@@ -485,14 +495,124 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   }
 }
 
+// ---- sort path: arrivals of all positions of one service,
+// item i = t * P + j (j = the position's rank in hop order), so a stable sort
+// by arrival time leaves ties in (t, hop) order
+__global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
+  const uint32_t P = k.svc.pos_cnt;
+  const uint64_t M = k.N * P;
+  for (uint64_t i = (uint64_t)blockIdx.x * kDesUpThreads + threadIdx.x; i < M;
+       i += (uint64_t)gridDim.x * kDesUpThreads) {
+    const uint64_t t = i / P;
+    const uint32_t v = k.sort_pos[k.svc.pos_off + (uint32_t)(i - t * P)];
+    const DesPos &pp = k.pos[v];
+    k.keys[i] = pp.parent == kDesNoParent ? k.A[t] : k.W[(uint64_t)pp.parent * k.ld + t] + pp.off;
+    k.vals[i] = (uint32_t)i;
+  }
+}
+
+// FIFO scan of one sort-path service over its sorted arrivals (one workgroup)
+__global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
+  __shared__ MaxPlus wtot[kDesThreads / 64];
+  __shared__ uint64_t carry[kDesMaxReplicas];
+  __shared__ uint64_t red[2 * kDesThreads / 64];
+  __shared__ MaxPlus xs[kDesThreads];
+  const DesSortSvc sv = k.svc;
+  const uint32_t P = sv.pos_cnt, reps = sv.reps;
+  const uint64_t M = k.N * P;
+  if (threadIdx.x < reps) carry[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t wsum = 0, wmax = 0;
+  for (uint64_t c0 = 0; c0 < M; c0 += kDesChunk) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDesPer;
+    uint64_t a[kDesPer], tt[kDesPer];
+    uint32_t vv[kDesPer], rr[kDesPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kDesPer; ++i) {
+      const uint64_t q = base + i;
+      a[i] = 0;
+      tt[i] = 0;
+      vv[i] = 0;
+      rr[i] = 0;
+      if (q < M) {
+        a[i] = k.skeys[q];
+        const uint32_t idx = k.svals[q];
+        tt[i] = idx / P;
+        vv[i] = k.sort_pos[sv.pos_off + (idx - (uint32_t)tt[i] * P)];
+        if (reps > 1) rr[i] = des_draw(k.trace_begin + tt[i], vv[i], 0x80000002u, 0, k.k0, k.k1) % reps;
+      }
+    }
+    for (uint32_t r = 0; r < reps; ++r) {
+      MaxPlus f{0, 0};
+#pragma unroll
+      for (uint32_t i = 0; i < kDesPer; ++i)
+        if (base + i < M && rr[i] == r) f = mp_then(f, MaxPlus{sv.hold, a[i] + sv.hold});
+      const MaxPlus inc = mp_block_scan(f, wtot);
+      xs[threadIdx.x] = inc;
+      __syncthreads();
+      const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
+      const uint64_t cin = carry[r];
+      uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+#pragma unroll
+      for (uint32_t i = 0; i < kDesPer; ++i) {
+        if (base + i < M && rr[i] == r) {
+          const uint64_t S = x > a[i] ? x : a[i];
+          k.W[(uint64_t)vv[i] * k.ld + tt[i]] = S;
+          const uint64_t w = S - a[i];
+          wsum += w;
+          wmax = w > wmax ? w : wmax;
+          x = S + sv.hold;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == kDesThreads - 1) carry[r] = x;
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d, 64);
+    const uint64_t o = __shfl_xor(wmax, d, 64);
+    wmax = o > wmax ? o : wmax;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = wsum;
+    red[kDesThreads / 64 + (threadIdx.x >> 6)] = wmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0, m = 0;
+    for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
+      s += red[i];
+      m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
+    }
+    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)sv.row * ISIM_DES_ROW_WORDS);
+    atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)M);
+    atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
+    atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
+    atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(M * sv.hold));
+  }
+}
+
 }  // namespace dev
+
+static size_t sort_temp_bytes(uint64_t m) {
+  size_t bytes = 0;
+  if (m == 0) return 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)m, 0, 64);
+  return bytes;
+}
 
 // Host launcher: the whole DES of one batch on `stream` (no allocation, no
 // host synchronisation).
-uint64_t des_workspace_bytes(uint32_t n_pos, uint64_t n) {
+uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n) {
   const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-  return al((uint64_t)n_pos * ((n + 7) & ~7ull) * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8);
+  const uint64_t m = (uint64_t)plan.max_sort_pos * n;
+  const uint64_t sort = m ? 2 * al(m * 8) + 2 * al(m * 4) + al(sort_temp_bytes(m)) : 0;
+  return al((uint64_t)plan.pos.size() * ((n + 7) & ~7ull) * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8) +
+         sort;
 }
 
 int des_launch(const DesLaunch &L, void *stream_) {
@@ -523,14 +643,48 @@ int des_launch(const DesLaunch &L, void *stream_) {
   hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
-  const uint32_t levels = (uint32_t)L.level_off.size() - 1;
-  for (uint32_t l = 0; l < levels; ++l) {
-    k.level_begin = L.level_off[l];
-    hipLaunchKernelGGL(des_down, dim3(L.level_off[l + 1] - L.level_off[l]), dim3(kDesThreads), 0, stream, k);
+  const DesPlan &pl = *L.plan;
+  // down pass by service level: single-position trace-ordered services scan
+  // in place; the others sort their arrivals first
+  const uint64_t m_max = (uint64_t)pl.max_sort_pos * L.n_traces;
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  char *sw = (char *)L.sort_ws;
+  uint64_t *keys_a = (uint64_t *)sw, *keys_b = (uint64_t *)(sw + al(m_max * 8));
+  uint32_t *vals_a = (uint32_t *)(sw + 2 * al(m_max * 8));
+  uint32_t *vals_b = (uint32_t *)(sw + 2 * al(m_max * 8) + al(m_max * 4));
+  void *sort_tmp = sw + 2 * al(m_max * 8) + 2 * al(m_max * 4);
+  const size_t sort_tmp_bytes = sort_temp_bytes(m_max);
+  const uint32_t slevels = (uint32_t)pl.fast_off.size() - 1;
+  k.sort_pos = L.d_sort_pos;
+  for (uint32_t l = 0; l < slevels; ++l) {
+    const uint32_t nf = pl.fast_off[l + 1] - pl.fast_off[l];
+    if (nf) {
+      k.level_pos = L.d_fast_pos;
+      k.level_begin = pl.fast_off[l];
+      hipLaunchKernelGGL(des_down, dim3(nf), dim3(kDesThreads), 0, stream, k);
+    }
+    for (uint32_t si = pl.sorted_off[l]; si < pl.sorted_off[l + 1]; ++si) {
+      k.svc = pl.sorted[si];
+      const uint64_t m = (uint64_t)k.svc.pos_cnt * L.n_traces;
+      k.keys = keys_a;
+      k.vals = vals_a;
+      uint64_t g = (m + kDesUpThreads - 1) / kDesUpThreads;
+      g = g < 4096 ? g : 4096;
+      hipLaunchKernelGGL(des_sort_keys, dim3((uint32_t)g), dim3(kDesUpThreads), 0, stream, k);
+      size_t tb = sort_tmp_bytes;
+      if (rocprim::radix_sort_pairs(sort_tmp, tb, keys_a, keys_b, vals_a, vals_b, (size_t)m, 0, 64, stream) !=
+          hipSuccess)
+        return 1;
+      k.skeys = keys_b;
+      k.svals = vals_b;
+      hipLaunchKernelGGL(des_down_sorted, dim3(1), dim3(kDesThreads), 0, stream, k);
+    }
   }
+  k.level_pos = L.d_level_pos;
+  const uint32_t levels = (uint32_t)pl.level_off.size() - 1;
   for (uint32_t l = levels; l-- > 0;) {
-    const uint32_t width = L.level_off[l + 1] - L.level_off[l];
-    k.level_begin = L.level_off[l];
+    const uint32_t width = pl.level_off[l + 1] - pl.level_off[l];
+    k.level_begin = pl.level_off[l];
     // enough (position, trace-range) blocks to fill the chip, >= 256 traces each
     uint64_t splits = (4096 + width - 1) / width;
     splits = splits < (L.n_traces + 255) / 256 ? splits : (L.n_traces + 255) / 256;

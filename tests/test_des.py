@@ -48,6 +48,19 @@ def test_exp_q24_is_exponential():
     assert np.max(np.abs(e - exact)) < 2e-5
 
 
+def canonical_concurrent(sleep="300us"):
+    """example-topologies/canonical.yaml with every service's calls in one
+    concurrent step (a and b are then invoked twice per trace: a DAG)."""
+    j = yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read())
+    doc = json.loads(j)
+    for s in doc["services"]:
+        calls = []
+        for st in s.get("script", []):
+            calls += st if isinstance(st, list) else [st]
+        s["script"] = [{"sleep": sleep}] + ([calls] if calls else [])
+    return doc
+
+
 def _handler(doc, **kw):
     return isim.Handler(isim.ServiceGraph.from_json(obj_to_json(doc) if isinstance(doc, dict) else doc),
                         None, isim.SimParams(**kw))
@@ -60,13 +73,8 @@ def _rejects(h, needle):
 
 
 def test_des_class():
-    canon = yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read())
-    _rejects(_handler(canon), "invoked more than once")
     _rejects(_handler(config2_topology()), "more than one step with calls")
     _rejects(_handler(mesh_topology(800, 4)), "static walk")
-    doc = tree_topology(3, 3)
-    doc["services"][1]["numReplicas"] = 3  # a non-leaf with replicas
-    _rejects(_handler(doc), "numReplicas > 1 and makes calls")
     doc = tree_topology(3, 3)
     doc["services"][-1]["numReplicas"] = 65
     _rejects(_handler(doc), "more than 64 replicas")
@@ -74,6 +82,15 @@ def test_des_class():
     assert (d.info.n_positions, d.info.table_rows) == (200, 200)
     assert d.info.n_levels >= 2 and d.info.max_width >= 1
     assert d.workspace_bytes(1000) >= 200 * 1000 * 8 + 1000 * 12
+    # DAG graphs (a service at several positions) and replicated callers take the sort path
+    canon = yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read())
+    _rejects(_handler(canon), "more than one step with calls")  # d and c call sequentially
+    dc = isim.DesHandler(_handler(canonical_concurrent()), 1_000_000)
+    assert dc.info.n_positions == 6
+    assert dc.workspace_bytes(1000) > 6 * 1000 * 8 + 2 * 1000 * 24  # a and b: 2 positions each
+    doc = tree_topology(3, 3)
+    doc["services"][1]["numReplicas"] = 3
+    isim.DesHandler(_handler(doc), 1_000_000)
     # the DES rejects bad parameters
     with pytest.raises(isim.IsimError):
         isim.DesHandler(d.handler, 0).serve(0, 1)

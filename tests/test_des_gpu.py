@@ -129,3 +129,50 @@ def test_device_entry_accumulates(gpu):
     mw = isim.native.DES_MAX_WAIT  # the longest wait merges with max
     want[:, mw] = np.maximum(t0.reshape(-1, W)[:, mw], t1.reshape(-1, W)[:, mw])
     assert np.array_equal(tg, want)
+
+
+# ---- the sort path: DAG graphs (a service at several positions per trace)
+# and replicated callers (arrivals out of trace order)
+
+def _dag(levels=4, width=5, fan=2, seed=3, reps=1):
+    import random
+    rnd = random.Random(seed)
+    svcs = []
+    for l in range(levels):
+        for j in range(width if l else 1):
+            calls = []
+            if l + 1 < levels:
+                calls = [{"call": f"n{l + 1}-{c}"} for c in sorted(rnd.sample(range(width), fan))]
+            script = [{"sleep": f"{rnd.randint(100, 900)}us"}] + ([calls] if calls else []) + \
+                     ([{"sleep": "50us"}] if l % 2 else [])
+            svcs.append({"name": f"n{l}-{j}", "script": script, "errorRate": 0.01,
+                         "numReplicas": reps if l and rnd.random() < 0.5 else 1})
+    svcs[0]["isEntrypoint"] = True
+    return {"services": svcs}
+
+
+@pytest.mark.parametrize("mean", [200_000, 2_000_000])
+def test_canonical_dag(gpu, mean):
+    from test_des import canonical_concurrent
+    DesCase(canonical_concurrent(), mean, error_mode=isim.MODE_A).compare(0, 9000)
+
+
+@pytest.mark.parametrize("reps", [1, 3])
+@pytest.mark.parametrize("mean", [150_000, 1_500_000])
+def test_random_dags(gpu, reps, mean):
+    DesCase(_dag(reps=reps), mean).compare(7, 10000)
+
+
+def test_replicated_callers(gpu):
+    doc = _sleepy_tree(4, 3)
+    for i, s in enumerate(doc["services"]):
+        s["numReplicas"] = 1 + i % 4  # internal services too
+    DesCase(doc, 600_000).compare(0, 12000)
+
+
+def test_dag_mode_b(gpu):
+    doc = _dag(levels=5, width=6, fan=3, reps=2)
+    for s in doc["services"]:
+        s["script"] = [x for x in s["script"] if not (isinstance(x, dict) and x.get("sleep") == "50us")]
+        s["errorRate"] = 0.05
+    DesCase(doc, 400_000, error_mode=isim.MODE_B).compare(0, 6000)
