@@ -33,7 +33,12 @@ namespace dev {
 
 constexpr uint32_t kDesPer = 8;                   // traces per thread in the down pass / arrivals
 constexpr uint32_t kDesThreads = 1024;
-constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per scan chunk
+constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per arrivals chunk
+#ifndef ISIM_DES_DOWN_PER
+#define ISIM_DES_DOWN_PER 4
+#endif
+constexpr uint32_t kDownPer = ISIM_DES_DOWN_PER;        // traces per thread in the down passes
+constexpr uint32_t kDownChunk = kDownPer * kDesThreads;
 constexpr uint32_t kDesUpThreads = 256;
 constexpr uint64_t kMask63 = (1ull << 63) - 1;
 
@@ -226,7 +231,7 @@ __global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
 }
 
 // ---- down pass: FIFO start times, one workgroup per position of the level
-__global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
+__global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   __shared__ MaxPlus wtot[kDesThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
   __shared__ uint64_t red[2 * kDesThreads / 64];
@@ -241,31 +246,31 @@ __global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
   const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
   uint64_t *out = k.W + (uint64_t)v * k.ld;
   uint64_t wsum = 0, wmax = 0;
-  for (uint64_t c0 = 0; c0 < N; c0 += kDesChunk) {
-    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDesPer;
-    uint64_t a[kDesPer];
-    uint32_t rr[kDesPer];
-    if (base + kDesPer <= N) {
+  for (uint64_t c0 = 0; c0 < N; c0 += kDownChunk) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDownPer;
+    uint64_t a[kDownPer];
+    uint32_t rr[kDownPer];
+    if (base + kDownPer <= N) {
       // 8 consecutive traces = 64 B per thread: four 16-B loads (rows are 64-B aligned)
       const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(par + base);
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer / 2; ++i) {
+      for (uint32_t i = 0; i < kDownPer / 2; ++i) {
         const ulonglong2 x = q[i];
         a[2 * i] = x.x + off;
         a[2 * i + 1] = x.y + off;
       }
     } else {
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
+      for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
     }
 #pragma unroll
-    for (uint32_t i = 0; i < kDesPer; ++i)
+    for (uint32_t i = 0; i < kDownPer; ++i)
       rr[i] = (base + i < N && reps > 1) ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps
                                          : 0u;
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer; ++i)
+      for (uint32_t i = 0; i < kDownPer; ++i)
         if (base + i < N && rr[i] == r) f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
       const MaxPlus inc = mp_block_scan(f, wtot);
       // exclusive prefix = the previous thread's inclusive one
@@ -274,9 +279,9 @@ __global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
       const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
       const uint64_t cin = carry[r];
       uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-      uint64_t Sv[kDesPer];
+      uint64_t Sv[kDownPer];
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer; ++i) {
+      for (uint32_t i = 0; i < kDownPer; ++i) {
         const uint64_t t = base + i;
         Sv[i] = 0;
         if (t < N && rr[i] == r) {
@@ -288,13 +293,13 @@ __global__ void __launch_bounds__(kDesThreads) des_down(DesK k) {
           x = S + P.hold;
         }
       }
-      if (reps == 1 && base + kDesPer <= N) {
+      if (reps == 1 && base + kDownPer <= N) {
         ulonglong2 *q = reinterpret_cast<ulonglong2 *>(out + base);
 #pragma unroll
-        for (uint32_t i = 0; i < kDesPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
+        for (uint32_t i = 0; i < kDownPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
       } else {
 #pragma unroll
-        for (uint32_t i = 0; i < kDesPer; ++i)
+        for (uint32_t i = 0; i < kDownPer; ++i)
           if (base + i < N && rr[i] == r) out[base + i] = Sv[i];
       }
       __syncthreads();
@@ -523,12 +528,12 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
   __syncthreads();
   uint64_t wsum = 0, wmax = 0;
-  for (uint64_t c0 = 0; c0 < M; c0 += kDesChunk) {
-    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDesPer;
-    uint64_t a[kDesPer], tt[kDesPer];
-    uint32_t vv[kDesPer], rr[kDesPer];
+  for (uint64_t c0 = 0; c0 < M; c0 += kDownChunk) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDownPer;
+    uint64_t a[kDownPer], tt[kDownPer];
+    uint32_t vv[kDownPer], rr[kDownPer];
 #pragma unroll
-    for (uint32_t i = 0; i < kDesPer; ++i) {
+    for (uint32_t i = 0; i < kDownPer; ++i) {
       const uint64_t q = base + i;
       a[i] = 0;
       tt[i] = 0;
@@ -545,7 +550,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer; ++i)
+      for (uint32_t i = 0; i < kDownPer; ++i)
         if (base + i < M && rr[i] == r) f = mp_then(f, MaxPlus{sv.hold, a[i] + sv.hold});
       const MaxPlus inc = mp_block_scan(f, wtot);
       xs[threadIdx.x] = inc;
@@ -554,7 +559,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
       const uint64_t cin = carry[r];
       uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
 #pragma unroll
-      for (uint32_t i = 0; i < kDesPer; ++i) {
+      for (uint32_t i = 0; i < kDownPer; ++i) {
         if (base + i < M && rr[i] == r) {
           const uint64_t S = x > a[i] ? x : a[i];
           k.W[(uint64_t)vv[i] * k.ld + tt[i]] = S;
