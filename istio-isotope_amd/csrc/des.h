@@ -60,6 +60,7 @@ struct DesPlan {
   // down pass, by service level (longest call path from the entry):
   std::vector<uint32_t> fast_pos;    // positions of single-position, trace-ordered services
   std::vector<uint32_t> fast_off;    // [n_slevels + 1]
+  std::vector<uint32_t> fast_multi;  // [n_slevels]: first multi-replica position of the level
   std::vector<DesSortSvc> sorted;    // sort-path services
   std::vector<uint32_t> sorted_off;  // [n_slevels + 1]
   std::vector<uint32_t> sort_pos;    // positions of the sort-path services

@@ -231,6 +231,7 @@ __global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
 }
 
 // ---- down pass: FIFO start times, one workgroup per position of the level
+template <bool MULTI>  // MULTI: the service has replicas (routing draw per trace)
 __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   __shared__ MaxPlus wtot[kDesThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
@@ -238,7 +239,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   __shared__ MaxPlus xs[kDesThreads];
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
   const DesPos P = k.pos[v];
-  const uint32_t reps = P.reps;
+  const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t N = k.N;
@@ -264,9 +265,12 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
       for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
     }
 #pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i)
-      rr[i] = (base + i < N && reps > 1) ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps
-                                         : 0u;
+    for (uint32_t i = 0; i < kDownPer; ++i) {
+      if constexpr (MULTI)
+        rr[i] = base + i < N ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
+      else
+        rr[i] = 0u;
+    }
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
 #pragma unroll
@@ -665,8 +669,15 @@ int des_launch(const DesLaunch &L, void *stream_) {
     const uint32_t nf = pl.fast_off[l + 1] - pl.fast_off[l];
     if (nf) {
       k.level_pos = L.d_fast_pos;
-      k.level_begin = pl.fast_off[l];
-      hipLaunchKernelGGL(des_down, dim3(nf), dim3(kDesThreads), 0, stream, k);
+      const uint32_t n1 = pl.fast_multi[l] - pl.fast_off[l];
+      if (n1) {
+        k.level_begin = pl.fast_off[l];
+        hipLaunchKernelGGL(des_down<false>, dim3(n1), dim3(kDesThreads), 0, stream, k);
+      }
+      if (nf > n1) {
+        k.level_begin = pl.fast_multi[l];
+        hipLaunchKernelGGL(des_down<true>, dim3(nf - n1), dim3(kDesThreads), 0, stream, k);
+      }
     }
     for (uint32_t si = pl.sorted_off[l]; si < pl.sorted_off[l + 1]; ++si) {
       k.svc = pl.sorted[si];

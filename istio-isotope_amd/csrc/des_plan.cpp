@@ -170,8 +170,13 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     else fast[slev[s]].push_back(svc_pos[s][0]);
   }
   out.fast_off.assign(n_slev + 1, 0);
+  out.fast_multi.assign(n_slev, 0);
   out.sorted_off.assign(n_slev + 1, 0);
   for (uint32_t l = 0; l < n_slev; ++l) {
+    // single-replica positions first: they run a kernel variant without the routing draw
+    std::stable_partition(fast[l].begin(), fast[l].end(), [&](uint32_t v) { return out.pos[v].reps == 1; });
+    out.fast_multi[l] = out.fast_off[l];
+    for (uint32_t v : fast[l]) out.fast_multi[l] += out.pos[v].reps == 1 ? 1u : 0u;
     out.fast_pos.insert(out.fast_pos.end(), fast[l].begin(), fast[l].end());
     out.fast_off[l + 1] = (uint32_t)out.fast_pos.size();
     for (int32_t s : srt[l]) {
