@@ -49,7 +49,8 @@ struct DevState {
   // DES (config 5): the plan uploaded on first use
   void *d_des_pos = nullptr;
   uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
-  uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr;
+  uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr;
+  void *d_des_ext = nullptr, *d_des_steps = nullptr;
 };
 
 }  // namespace
@@ -80,6 +81,9 @@ struct isim_handler {
         (void)hipFree(kv.second.d_des_mult);
         (void)hipFree(kv.second.d_des_fast);
         (void)hipFree(kv.second.d_des_sort);
+        (void)hipFree(kv.second.d_des_arr);
+        (void)hipFree(kv.second.d_des_ext);
+        (void)hipFree(kv.second.d_des_steps);
         (void)hipSetDevice(cur);
       }
     }
@@ -487,7 +491,10 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
   };
   if (!up(&st->d_des_pos, d.pos.data(), d.pos.size() * sizeof(isim::DesPos)) ||
       !up((void **)&st->d_des_child, d.child.data(), d.child.size() * 4) ||
-      !up((void **)&st->d_des_level, d.level_pos.data(), d.level_pos.size() * 4) ||
+      !up((void **)&st->d_des_level, d.fin_pos.data(), d.fin_pos.size() * 4) ||
+      !up((void **)&st->d_des_arr, d.arr_ops.data(), d.arr_ops.size() * 4) ||
+      !up(&st->d_des_ext, d.ext.data(), d.ext.size() * sizeof(isim::DesPosExt)) ||
+      !up(&st->d_des_steps, d.steps.data(), d.steps.size() * sizeof(isim::DesStep)) ||
       !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4) ||
       !up((void **)&st->d_des_fast, d.fast_pos.data(), d.fast_pos.size() * 4) ||
       !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4))
@@ -504,7 +511,7 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   std::memset(out, 0, sizeof(*out));
   if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
   out->n_positions = (int32_t)h->des.pos.size();
-  out->n_levels = (int32_t)h->des.level_off.size() - 1;
+  out->n_levels = (int32_t)h->des.n_levels;
   out->max_width = (int32_t)h->des.max_width;
   out->table_rows = (int32_t)h->prog.row_svc.size();
   return ISIM_OK;
@@ -542,8 +549,11 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   isim::DesLaunch L;
   L.plan = &d;
   L.d_pos = st->d_des_pos;
+  L.d_ext = st->d_des_ext;
+  L.d_steps = st->d_des_steps;
   L.d_child = st->d_des_child;
-  L.d_level_pos = st->d_des_level;
+  L.d_fin_pos = st->d_des_level;
+  L.d_arr_ops = st->d_des_arr;
   L.d_fast_pos = st->d_des_fast;
   L.d_sort_pos = st->d_des_sort;
   L.W = (uint64_t *)ws;
@@ -554,6 +564,8 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   ws += al(n_traces * 4);
   L.blk = (uint64_t *)ws;
   ws += al(((n_traces + 8191) / 8192 + 1) * 8);
+  L.BK = (uint64_t *)ws;
+  ws += al((uint64_t)d.steps.size() * ((n_traces + 7) & ~7ull) * 8);
   L.sort_ws = ws;
   L.d_stats = d_stats;
   L.d_table = d_des_table;

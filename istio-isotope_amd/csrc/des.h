@@ -41,7 +41,7 @@ static_assert(sizeof(DesPos) == 64, "DesPos must be 64 bytes");
 
 // A service whose queue needs the sort path: several
 // positions per trace, or arrivals not in trace order (a caller upstream
-// has replicas).
+// has replicas, or the call is not in the caller's first call step).
 struct DesSortSvc {
   uint32_t row;       // duration-table row
   uint32_t reps;      // replicas
@@ -50,29 +50,54 @@ struct DesSortSvc {
   uint64_t hold;      // worker hold time
 };
 
+// Per position, for scripts with several call steps (16 bytes, device layout).
+struct DesPosExt {
+  uint32_t bk_in;      // BK row whose value + off is the arrival (kDesNone: start(parent) + off)
+  uint32_t bk_last;    // BK row of the position's own last call step (kDesNone: one call step or none)
+  uint32_t last_child; // index in its children list where the last call step's children start
+  uint32_t pad;
+};
+
+// The begin time of call step k of a position, BK[id][t]:
+// step 1: start + add; step k > 1: max(BK[prev] + smax, max F(step k-1 callees)) + add.
+struct DesStep {
+  uint32_t pos;        // the calling position
+  uint32_t prev;       // BK row of step k-1 (kDesNone for step 1)
+  uint64_t add;        // step 1: sleeps before it; k > 1: sleeps between steps k-1 and k
+  uint64_t smax;       // longest sleep of step k-1's concurrent sub-commands
+  uint32_t child_off;  // step k-1's callees: positions child[child_off .. +child_cnt)
+  uint32_t child_cnt;
+};
+static_assert(sizeof(DesStep) == 32, "DesStep must be 32 bytes");
+constexpr uint32_t kDesNone = 0xFFFFFFFFu;
+
 struct DesPlan {
   std::vector<DesPos> pos;           // hop order (position 0 = the entry)
-  std::vector<uint32_t> child;       // children lists (positions)
-  std::vector<uint32_t> level_pos;   // positions grouped by depth (up pass)
-  std::vector<uint32_t> level_off;   // [n_levels + 1]
+  std::vector<DesPosExt> ext;        // [n_pos]
+  std::vector<uint32_t> child;       // children lists (positions, call-step order)
+  std::vector<DesStep> steps;        // BK rows
   std::vector<uint32_t> slot_mult;   // per slot: calls through it per trace
-  uint32_t max_width = 0;            // widest depth level
-  // down pass, by service level (longest call path from the entry):
-  std::vector<uint32_t> fast_pos;    // positions of single-position, trace-ordered services
-  std::vector<uint32_t> fast_off;    // [n_slevels + 1]
-  std::vector<uint32_t> fast_multi;  // [n_slevels]: first multi-replica position of the level
-  std::vector<DesSortSvc> sorted;    // sort-path services
-  std::vector<uint32_t> sorted_off;  // [n_slevels + 1]
-  std::vector<uint32_t> sort_pos;    // positions of the sort-path services
+  uint32_t n_levels = 0, max_width = 0;  // invocation-tree depth, widest depth
+  bool general = false;              // some script has several call steps
+  // the schedule: rounds of (step begins, queues, finishes)
+  std::vector<uint32_t> arr_ops, arr_off;        // BK rows computed in round r
+  std::vector<uint32_t> fast_pos, fast_off;      // single-position trace-ordered services
+  std::vector<uint32_t> fast_multi;              // [rounds]: first multi-replica position
+  std::vector<DesSortSvc> sorted;                // sort-path services
+  std::vector<uint32_t> sorted_off;
+  std::vector<uint32_t> sort_pos;                // positions of the sort-path services
+  std::vector<uint32_t> fin_pos, fin_off;        // finish groups (one depth each), deepest first
+  std::vector<uint32_t> fin_round_off;           // [rounds + 1] into the finish groups
   uint32_t max_sort_pos = 0;         // most positions of one sort-path service
+  uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 
 // Device buffers and sizes of one DES batch (des.hip: des_launch).
 struct DesLaunch {
-  const DesPlan *plan;               // host copy (level offsets, sort-path services)
-  const void *d_pos;                 // DesPos[n_pos]
-  const uint32_t *d_child, *d_level_pos, *d_fast_pos, *d_sort_pos;
-  uint64_t *W, *A, *blk;             // workspace: [n_pos][N], [N], chunk sums
+  const DesPlan *plan;               // host copy (the schedule)
+  const void *d_pos, *d_ext, *d_steps;  // DesPos[n_pos], DesPosExt[n_pos], DesStep[]
+  const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops;
+  uint64_t *W, *A, *blk, *BK;        // workspace: [n_pos][N], [N], chunk sums, [steps][N]
   uint32_t *E;                       // workspace: [N]
   void *sort_ws;                     // workspace of the sort path (keys, values, radix-sort temp)
   uint64_t *d_stats, *d_table;

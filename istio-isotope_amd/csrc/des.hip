@@ -96,8 +96,12 @@ __device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
 
 struct DesK {
   const DesPos *pos;
+  const DesPosExt *ext;
+  const DesStep *steps;
   const uint32_t *child;
-  const uint32_t *level_pos;
+  const uint32_t *level_pos;  // the positions of the launch (fast queue or finish group)
+  const uint32_t *arr_ops;    // BK rows of the launch (step begins)
+  uint64_t *BK;               // [steps][ld]
   uint64_t *W;  // [n_pos][N]
   uint64_t *A;  // [N]
   uint32_t *E;  // [N]
@@ -119,6 +123,14 @@ struct DesK {
   uint64_t *keys;
   uint32_t *vals;
 };
+
+// arrival of position v (pp = pos[v]) for trace t
+__device__ __forceinline__ uint64_t des_arrival(const DesK &k, uint32_t v, const DesPos &pp, uint64_t t) {
+  if (pp.parent == kDesNoParent) return k.A[t];
+  const uint32_t b = k.ext[v].bk_in;
+  return (b == kDesNone ? k.W[(uint64_t)pp.parent * k.ld + t] : k.BK[(uint64_t)b * k.ld + t]) + pp.off;
+}
+
 
 // (B, C) represents x -> max(x + B, C); `then` composes a after b.
 struct MaxPlus {
@@ -348,9 +360,16 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
   const uint64_t N = k.N;
   const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
   uint64_t *mine = k.W + (uint64_t)v * k.ld;
-  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
+  const DesPosExt X = k.ext[v];
+  // arrival: start(parent) + off, or a step begin + H (calls after calls), or A_t (the entry)
+  const uint64_t *par = P.parent == kDesNoParent ? k.A
+                        : X.bk_in == kDesNone    ? k.W + (uint64_t)P.parent * k.ld
+                                                 : k.BK + (uint64_t)X.bk_in * k.ld;
   const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
   const bool leaf = P.flags & kDesFlagLeaf;
+  // several call steps: F = max(BK_last + floor, max F(last step's callees)) + post
+  const uint64_t *base_t = X.bk_last == kDesNone ? mine : k.BK + (uint64_t)X.bk_last * k.ld;
+  const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
   constexpr uint32_t U = 4;  // independent traces per thread per iteration (memory-level parallelism)
   for (uint64_t t0 = tb + threadIdx.x; t0 < te; t0 += U * kDesUpThreads) {
@@ -365,16 +384,20 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
       sto[j] = 0;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < U; ++j) m[j] = S[j] + P.floor;
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint64_t t = t0 + j * kDesUpThreads;
+      m[j] = (X.bk_last == kDesNone ? S[j] : (t < te ? base_t[t] : 0)) + P.floor;
+    }
     if (!leaf) {
       for (uint32_t c = 0; c < P.child_cnt; ++c) {
         const uint64_t *fc = k.W + (uint64_t)k.child[P.child_off + c] * k.ld;
+        const bool in_max = c >= c_max_from;
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j) {
           const uint64_t t = t0 + j * kDesUpThreads;
           const uint64_t f = t < te ? fc[t] : 0;
           const uint64_t tc = f & kMask63;
-          m[j] = tc > m[j] ? tc : m[j];
+          if (in_max) m[j] = tc > m[j] ? tc : m[j];
           sto[j] |= (uint32_t)(f >> 63);
         }
       }
@@ -514,8 +537,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
        i += (uint64_t)gridDim.x * kDesUpThreads) {
     const uint64_t t = i / P;
     const uint32_t v = k.sort_pos[k.svc.pos_off + (uint32_t)(i - t * P)];
-    const DesPos &pp = k.pos[v];
-    k.keys[i] = pp.parent == kDesNoParent ? k.A[t] : k.W[(uint64_t)pp.parent * k.ld + t] + pp.off;
+    k.keys[i] = des_arrival(k, v, k.pos[v], t);
     k.vals[i] = (uint32_t)i;
   }
 }
@@ -603,6 +625,28 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
   }
 }
 
+// ---- step begins (calls after calls): BK rows of one round
+__global__ void __launch_bounds__(kDesUpThreads) des_arrive(DesK k) {
+  const uint32_t b = k.arr_ops[k.level_begin + blockIdx.y];
+  const DesStep st = k.steps[b];
+  const uint64_t N = k.N;
+  const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
+  uint64_t *out = k.BK + (uint64_t)b * k.ld;
+  for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
+    uint64_t v;
+    if (st.prev == kDesNone) {
+      v = k.W[(uint64_t)st.pos * k.ld + t];  // the position's start
+    } else {
+      v = k.BK[(uint64_t)st.prev * k.ld + t] + st.smax;
+      for (uint32_t j = 0; j < st.child_cnt; ++j) {
+        const uint64_t f = k.W[(uint64_t)k.child[st.child_off + j] * k.ld + t] & kMask63;
+        v = f > v ? f : v;
+      }
+    }
+    out[t] = v + st.add;
+  }
+}
+
 }  // namespace dev
 
 static size_t sort_temp_bytes(uint64_t m) {
@@ -618,10 +662,11 @@ static size_t sort_temp_bytes(uint64_t m) {
 uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n) {
   const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  const uint64_t ld = (n + 7) & ~7ull;
   const uint64_t m = (uint64_t)plan.max_sort_pos * n;
   const uint64_t sort = m ? 2 * al(m * 8) + 2 * al(m * 4) + al(sort_temp_bytes(m)) : 0;
-  return al((uint64_t)plan.pos.size() * ((n + 7) & ~7ull) * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8) +
-         sort;
+  return al((uint64_t)plan.pos.size() * ld * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8) +
+         al((uint64_t)plan.steps.size() * ld * 8) + sort;
 }
 
 int des_launch(const DesLaunch &L, void *stream_) {
@@ -629,12 +674,15 @@ int des_launch(const DesLaunch &L, void *stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   DesK k{};
   k.pos = (const DesPos *)L.d_pos;
+  k.ext = (const DesPosExt *)L.d_ext;
+  k.steps = (const DesStep *)L.d_steps;
   k.child = L.d_child;
-  k.level_pos = L.d_level_pos;
+  k.arr_ops = L.d_arr_ops;
   k.W = L.W;
   k.A = L.A;
   k.E = L.E;
   k.blk = L.blk;
+  k.BK = L.BK;
   k.stats = L.d_stats;
   k.table = L.d_table;
   k.records = L.d_records;
@@ -653,8 +701,6 @@ int des_launch(const DesLaunch &L, void *stream_) {
   hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   const DesPlan &pl = *L.plan;
-  // down pass by service level: single-position trace-ordered services scan
-  // in place; the others sort their arrivals first
   const uint64_t m_max = (uint64_t)pl.max_sort_pos * L.n_traces;
   auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   char *sw = (char *)L.sort_ws;
@@ -663,23 +709,38 @@ int des_launch(const DesLaunch &L, void *stream_) {
   uint32_t *vals_b = (uint32_t *)(sw + 2 * al(m_max * 8) + al(m_max * 4));
   void *sort_tmp = sw + 2 * al(m_max * 8) + 2 * al(m_max * 4);
   const size_t sort_tmp_bytes = sort_temp_bytes(m_max);
-  const uint32_t slevels = (uint32_t)pl.fast_off.size() - 1;
   k.sort_pos = L.d_sort_pos;
-  for (uint32_t l = 0; l < slevels; ++l) {
-    const uint32_t nf = pl.fast_off[l + 1] - pl.fast_off[l];
+  // (position or row) x trace-range blocks: enough to fill the chip, >= 256 traces each
+  auto splits_for = [&](uint32_t width) {
+    uint64_t sp = (4096 + width - 1) / width;
+    const uint64_t cap = (L.n_traces + 255) / 256;
+    sp = sp < cap ? sp : cap;
+    return (uint32_t)(sp ? sp : 1);
+  };
+  for (uint32_t r = 0; r < pl.rounds(); ++r) {
+    // 1. step begins (calls after calls)
+    const uint32_t na = pl.arr_off[r + 1] - pl.arr_off[r];
+    if (na) {
+      k.level_begin = pl.arr_off[r];
+      k.splits = splits_for(na);
+      hipLaunchKernelGGL(des_arrive, dim3(k.splits, na), dim3(kDesUpThreads), 0, stream, k);
+    }
+    // 2. queues: single-position trace-ordered services scan in place, the
+    //    others sort their arrivals first
+    const uint32_t nf = pl.fast_off[r + 1] - pl.fast_off[r];
     if (nf) {
       k.level_pos = L.d_fast_pos;
-      const uint32_t n1 = pl.fast_multi[l] - pl.fast_off[l];
+      const uint32_t n1 = pl.fast_multi[r] - pl.fast_off[r];
       if (n1) {
-        k.level_begin = pl.fast_off[l];
+        k.level_begin = pl.fast_off[r];
         hipLaunchKernelGGL(des_down<false>, dim3(n1), dim3(kDesThreads), 0, stream, k);
       }
       if (nf > n1) {
-        k.level_begin = pl.fast_multi[l];
+        k.level_begin = pl.fast_multi[r];
         hipLaunchKernelGGL(des_down<true>, dim3(nf - n1), dim3(kDesThreads), 0, stream, k);
       }
     }
-    for (uint32_t si = pl.sorted_off[l]; si < pl.sorted_off[l + 1]; ++si) {
+    for (uint32_t si = pl.sorted_off[r]; si < pl.sorted_off[r + 1]; ++si) {
       k.svc = pl.sorted[si];
       const uint64_t m = (uint64_t)k.svc.pos_cnt * L.n_traces;
       k.keys = keys_a;
@@ -695,17 +756,14 @@ int des_launch(const DesLaunch &L, void *stream_) {
       k.svals = vals_b;
       hipLaunchKernelGGL(des_down_sorted, dim3(1), dim3(kDesThreads), 0, stream, k);
     }
-  }
-  k.level_pos = L.d_level_pos;
-  const uint32_t levels = (uint32_t)pl.level_off.size() - 1;
-  for (uint32_t l = levels; l-- > 0;) {
-    const uint32_t width = pl.level_off[l + 1] - pl.level_off[l];
-    k.level_begin = pl.level_off[l];
-    // enough (position, trace-range) blocks to fill the chip, >= 256 traces each
-    uint64_t splits = (4096 + width - 1) / width;
-    splits = splits < (L.n_traces + 255) / 256 ? splits : (L.n_traces + 255) / 256;
-    k.splits = (uint32_t)(splits ? splits : 1);
-    hipLaunchKernelGGL(des_up, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+    // 3. finishes, deepest group first
+    k.level_pos = L.d_fin_pos;
+    for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
+      const uint32_t width = pl.fin_off[gi + 1] - pl.fin_off[gi];
+      k.level_begin = pl.fin_off[gi];
+      k.splits = splits_for(width);
+      hipLaunchKernelGGL(des_up, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+    }
   }
   uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
   fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;

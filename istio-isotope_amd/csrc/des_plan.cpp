@@ -1,4 +1,19 @@
 // DES plan builder (des.h); the kernels are in des.hip.
+//
+// The plan unrolls the static walk's invocation tree (one POSITION per
+// invocation, hop order = the draw stream's order) and schedules the exact
+// DES of a batch as ROUNDS; a round runs, in this order,
+//   1. step begins   BK rows of call steps k > 1 (and k = 1 of multi-step
+//                    scripts) whose inputs are settled,
+//   2. queues        the FIFO scan of every service whose arrivals are all
+//                    known (fast path, or sort path),
+//   3. finishes      F of positions whose start and callees are settled,
+//                    deepest first.
+// Every operation goes in the earliest round its inputs allow (longest path
+// over the dependency graph); a dependency cycle — a service invoked both
+// inside a call step and after it within one caller's script — has no
+// schedule and is rejected.  Graphs whose scripts have at most one call step
+// get the shortest schedule: queues by service level, all finishes last.
 #include "des.h"
 
 #include <algorithm>
@@ -8,27 +23,29 @@ namespace {
 
 uint64_t sleep_of(int64_t d) { return d > 0 ? (uint64_t)d : 0; }
 
+// A script as [sleeps] (call step [sleeps])* (DESIGN.md §10.1).
 struct ScriptShape {
-  bool ok = true;     // at most one step contains calls
-  bool leaf = true;   // no call step
-  uint64_t pre = 0, cmax = 0, post = 0, total = 0, hold = 0;
+  uint64_t pre = 0;                  // sleeps before the first call step (leaf: the script time)
+  std::vector<uint64_t> smax, gap;   // per call step: longest concurrent sleep; sleeps after it
+  std::vector<uint32_t> call_step;   // per call command (document order): its call step
+  uint64_t hold = 0;                 // sum of all sleeps (the worker hold time)
+  bool leaf() const { return smax.empty(); }
 };
 
-// Splits a script into [sleeps] [call step] [sleeps].
 ScriptShape shape_of(const Service &s) {
   ScriptShape r;
   for (const Command &c : s.script) {
     uint64_t dur = 0, smax = 0;
-    bool calls = false;
+    uint32_t calls = 0;
     if (c.kind == Command::Sleep) {
       dur = sleep_of(c.sleep_ns);
       r.hold += dur;
     } else if (c.kind == Command::Request) {
-      calls = true;
+      calls = 1;
     } else {
       for (const Command &x : c.commands) {
         if (x.kind == Command::Request) {
-          calls = true;
+          ++calls;
         } else {
           smax = std::max(smax, sleep_of(x.sleep_ns));
           r.hold += sleep_of(x.sleep_ns);
@@ -37,15 +54,14 @@ ScriptShape shape_of(const Service &s) {
       dur = smax;
     }
     if (calls) {
-      if (!r.leaf) r.ok = false;
-      r.leaf = false;
-      r.cmax = smax;
-    } else if (r.leaf) {
+      for (uint32_t i = 0; i < calls; ++i) r.call_step.push_back((uint32_t)r.smax.size());
+      r.smax.push_back(smax);
+      r.gap.push_back(0);
+    } else if (r.smax.empty()) {
       r.pre += dur;
     } else {
-      r.post += dur;
+      r.gap.back() += dur;
     }
-    r.total += dur;
   }
   return r;
 }
@@ -63,8 +79,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   std::vector<char> shaped(n, 0);
   const uint32_t np = p.stream_nodes;
   out.pos.resize(np);
+  out.ext.assign(np, DesPosExt{kDesNone, kDesNone, 0, 0});
   std::vector<std::vector<uint32_t>> kids(np);
-  std::vector<uint32_t> depth(np, 0);
+  std::vector<uint32_t> depth(np, 0), kstep(np, 0);  // kstep: the caller's call step of the position
   std::vector<int32_t> pos_svc(np, -1);
   std::vector<std::vector<uint32_t>> svc_pos(n);
   std::vector<uint32_t> stack;
@@ -75,35 +92,35 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (!shaped[svc]) {
       shape[svc] = shape_of(g.services[svc]);
       shaped[svc] = 1;
-      if (!shape[svc].ok) {
-        err = "service \"" + g.services[svc].name +
-              "\" has more than one step with calls; the DES needs every call sent when the script's call step "
-              "begins (a call after a call waits for the first callee's queueing)";
-        return ISIM_EINVAL;
-      }
       if (std::max<int32_t>(1, g.services[svc].num_replicas) > (int32_t)kDesMaxReplicas) {
         err = "service \"" + g.services[svc].name + "\" has more than 64 replicas (DES limit)";
         return ISIM_EINVAL;
       }
     }
+    const ScriptShape &sh = shape[svc];
     DesPos &ps = out.pos[i];
     ps.parent = stack.empty() ? kDesNoParent : stack.back();
     ps.row = (uint32_t)p.svc_row[svc];
     ps.slot = slot;
     ps.reps = (uint32_t)std::max<int32_t>(1, g.services[svc].num_replicas);
-    ps.hold = shape[svc].hold;
-    ps.floor = shape[svc].leaf ? shape[svc].total : shape[svc].pre + shape[svc].cmax;
-    ps.post = shape[svc].post;
+    ps.hold = sh.hold;
+    // one call step: F = max(S + floor, max_c F_c) + post; several: F =
+    // max(BK_last + floor, max_c(last step) F_c) + post
+    ps.floor = sh.leaf() ? sh.pre : (sh.smax.size() == 1 ? sh.pre + sh.smax[0] : sh.smax.back());
+    ps.post = sh.leaf() ? 0 : sh.gap.back();
     ps.thr = nd.thr;
     ps.flags = (nd.meta & 0x80000000u) ? kDesFlagAlways : 0u;
-    if (shape[svc].leaf) ps.flags |= kDesFlagLeaf;
+    if (sh.leaf()) ps.flags |= kDesFlagLeaf;
     pos_svc[i] = svc;
     svc_pos[svc].push_back(i);
     if (ps.parent != kDesNoParent) {
-      // calls are sent when the caller's call step begins: its pre-call sleeps after its start
-      ps.off = shape[pos_svc[ps.parent]].pre + p.site_hop[p.slot_site[slot]];
-      kids[ps.parent].push_back(i);
-      depth[i] = depth[ps.parent] + 1;
+      const uint32_t par = ps.parent;
+      const ScriptShape &ph = shape[pos_svc[par]];
+      kstep[i] = ph.call_step[kids[par].size()];  // j-th callee = j-th call command (static walk)
+      const uint64_t h = p.site_hop[p.slot_site[slot]];
+      ps.off = kstep[i] == 0 ? ph.pre + h : h;     // step 1: start(parent) + pre + H; later: BK + H
+      kids[par].push_back(i);
+      depth[i] = depth[par] + 1;
     }
     stack.push_back(i);
     for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
@@ -113,73 +130,141 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     out.pos[i].child_cnt = (uint32_t)kids[i].size();
     out.child.insert(out.child.end(), kids[i].begin(), kids[i].end());
   }
-  // up pass: positions by depth
-  const uint32_t levels = np ? 1 + *std::max_element(depth.begin(), depth.end()) : 0;
-  out.level_off.assign(levels + 1, 0);
-  for (uint32_t i = 0; i < np; ++i) out.level_off[depth[i] + 1]++;
-  for (uint32_t l = 0; l < levels; ++l) {
-    out.max_width = std::max(out.max_width, out.level_off[l + 1]);
-    out.level_off[l + 1] += out.level_off[l];
-  }
-  out.level_pos.resize(np);
-  std::vector<uint32_t> fill(out.level_off.begin(), out.level_off.end() - 1);
-  for (uint32_t i = 0; i < np; ++i) out.level_pos[fill[depth[i]]++] = i;
-
-  // down pass: a service's queue needs ALL its arrivals, so services go by
-  // service level (longest call path from the entry; positions in hop order
-  // visit callers before callees, so one sweep settles it)
-  std::vector<uint32_t> slev(n, 0);
+  out.n_levels = np ? 1 + *std::max_element(depth.begin(), depth.end()) : 0;
   {
-    // longest path over the service DAG of the reachable services (Kahn)
-    std::vector<std::vector<int32_t>> out_e(n);
-    std::vector<uint32_t> indeg(n, 0);
-    std::vector<std::pair<int32_t, int32_t>> edges;
-    for (uint32_t i = 0; i < np; ++i)
-      if (out.pos[i].parent != kDesNoParent) edges.push_back({pos_svc[out.pos[i].parent], pos_svc[i]});
-    std::sort(edges.begin(), edges.end());
-    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
-    for (auto &e : edges) {
-      out_e[e.first].push_back(e.second);
-      indeg[e.second]++;
-    }
-    std::vector<int32_t> q{p.entry};
-    for (size_t h = 0; h < q.size(); ++h)
-      for (int32_t c : out_e[q[h]]) {
-        slev[c] = std::max(slev[c], slev[q[h]] + 1);
-        if (--indeg[c] == 0) q.push_back(c);
-      }
+    std::vector<uint32_t> w(out.n_levels, 0);
+    for (uint32_t i = 0; i < np; ++i) out.max_width = std::max(out.max_width, ++w[depth[i]]);
   }
-  // arrivals in trace order (the FIFO scan needs no sort) when the caller's
-  // start times are: a single-replica caller whose own arrivals are in order
+
+  // ---- BK rows: every call step of a multi-step script
+  std::vector<std::vector<uint32_t>> pos_bk(np);  // per position: BK row of each of its call steps
+  for (uint32_t i = 0; i < np; ++i) {
+    const ScriptShape &sh = shape[pos_svc[i]];
+    if (sh.smax.size() < 2) continue;
+    out.general = true;
+    uint32_t c0 = out.pos[i].child_off, cprev = 0, nprev = 0;
+    for (uint32_t k = 0; k < sh.smax.size(); ++k) {
+      DesStep st{};
+      st.pos = i;
+      st.prev = k ? pos_bk[i][k - 1] : kDesNone;
+      st.add = k ? sh.gap[k - 1] : sh.pre;
+      st.smax = k ? sh.smax[k - 1] : 0;
+      st.child_off = cprev;
+      st.child_cnt = nprev;
+      pos_bk[i].push_back((uint32_t)out.steps.size());
+      out.steps.push_back(st);
+      // the callees of step k follow in the children list
+      uint32_t cnt = 0;
+      for (uint32_t j = 0; j < kids[i].size(); ++j) cnt += kstep[kids[i][j]] == k ? 1u : 0u;
+      cprev = c0;
+      nprev = cnt;
+      c0 += cnt;
+    }
+    out.ext[i].bk_last = pos_bk[i].back();
+    out.ext[i].last_child = out.pos[i].child_cnt - nprev;
+  }
+  for (uint32_t i = 0; i < np; ++i) {
+    const uint32_t par = out.pos[i].parent;
+    if (par != kDesNoParent && kstep[i] > 0) out.ext[i].bk_in = pos_bk[par][kstep[i]];
+  }
+
+  // ---- arrivals in trace order (no sort needed): a first-step callee of a
+  // single-replica caller whose own arrivals are in order
   std::vector<char> arr_sorted(np, 1), s_sorted(np, 1);
   for (uint32_t i = 0; i < np; ++i) {
     const uint32_t par = out.pos[i].parent;
-    arr_sorted[i] = par == kDesNoParent ? 1 : s_sorted[par];
+    arr_sorted[i] = par == kDesNoParent ? 1 : (s_sorted[par] && kstep[i] == 0);
     s_sorted[i] = arr_sorted[i] && out.pos[i].reps == 1;
   }
-  uint32_t n_slev = 0;
-  for (int32_t s = 0; s < n; ++s)
-    if (!svc_pos[s].empty()) n_slev = std::max(n_slev, slev[s] + 1);
-  std::vector<std::vector<uint32_t>> fast(n_slev);
-  std::vector<std::vector<int32_t>> srt(n_slev);
+
+  // ---- the schedule: op ids  Q(s) = service s, F(v) = n + v, A(b) = n + np + b
+  const uint32_t nq = (uint32_t)n, nb = (uint32_t)out.steps.size();
+  const uint32_t n_ops = nq + np + nb;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> pred(n_ops);  // (op, weight)
+  auto Q = [&](uint32_t v) { return (uint32_t)pos_svc[v]; };
+  auto F = [&](uint32_t v) { return nq + v; };
+  auto Ab = [&](uint32_t b) { return nq + np + b; };
+  for (uint32_t v = 0; v < np; ++v) {
+    const uint32_t par = out.pos[v].parent;
+    // queue(svc v) after the arrival of v is known
+    if (par != kDesNoParent) {
+      if (kstep[v] == 0) pred[Q(v)].push_back({Q(par), 1});          // start(parent), earlier round
+      else pred[Q(v)].push_back({Ab(out.ext[v].bk_in), 0});          // BK row, same round or later
+    }
+    pred[F(v)].push_back({Q(v), 0});
+    for (uint32_t c : kids[v]) pred[F(v)].push_back({F(c), 0});        // same round: deeper first
+    if (out.ext[v].bk_last != kDesNone) pred[F(v)].push_back({Ab(out.ext[v].bk_last), 0});
+  }
+  for (uint32_t b = 0; b < nb; ++b) {
+    const DesStep &st = out.steps[b];
+    if (st.prev == kDesNone) {
+      pred[Ab(b)].push_back({Q(st.pos), 1});
+    } else {
+      pred[Ab(b)].push_back({Ab(st.prev), 1});  // step begins of one round run in one launch
+      for (uint32_t j = 0; j < st.child_cnt; ++j) pred[Ab(b)].push_back({F(out.child[st.child_off + j]), 1});
+    }
+  }
+  // longest path by relaxation; more passes than ops means a cycle
+  std::vector<uint32_t> rnd(n_ops, 0);
+  std::vector<char> used(n_ops, 0);
+  for (uint32_t v = 0; v < np; ++v) used[Q(v)] = used[F(v)] = 1;
+  for (uint32_t b = 0; b < nb; ++b) used[Ab(b)] = 1;
+  bool changed = true;
+  uint32_t pass = 0;
+  while (changed) {
+    changed = false;
+    if (++pass > n_ops + 2) {
+      err = "a service is called both inside a call step and after it (through one caller's later steps); "
+            "its queue would depend on its own finish: no DES schedule";
+      return ISIM_EINVAL;
+    }
+    for (uint32_t o = 0; o < n_ops; ++o) {
+      if (!used[o]) continue;
+      uint32_t r = 0;
+      for (auto &e : pred[o]) r = std::max(r, rnd[e.first] + e.second);
+      if (r != rnd[o]) {
+        rnd[o] = r;
+        changed = true;
+      }
+    }
+  }
+  uint32_t R = 0;
+  for (uint32_t o = 0; o < n_ops; ++o)
+    if (used[o]) R = std::max(R, rnd[o] + 1);
+  if (!out.general) {
+    // no step begins depend on finishes: all finishes in one last round
+    for (uint32_t v = 0; v < np; ++v) rnd[F(v)] = R;
+    R += 1;
+  }
+  // ---- lay the rounds out
+  std::vector<std::vector<uint32_t>> arr(R), fast(R);
+  std::vector<std::vector<int32_t>> srt(R);
+  std::vector<std::vector<std::vector<uint32_t>>> fin(R, std::vector<std::vector<uint32_t>>(out.n_levels));
+  for (uint32_t b = 0; b < nb; ++b) arr[rnd[Ab(b)]].push_back(b);
   for (int32_t s = 0; s < n; ++s) {
     if (svc_pos[s].empty()) continue;
     bool need = svc_pos[s].size() > 1;
     for (uint32_t v : svc_pos[s]) need = need || !arr_sorted[v];
-    if (need) srt[slev[s]].push_back(s);
-    else fast[slev[s]].push_back(svc_pos[s][0]);
+    if (need) srt[rnd[s]].push_back(s);
+    else fast[rnd[s]].push_back(svc_pos[s][0]);
   }
-  out.fast_off.assign(n_slev + 1, 0);
-  out.fast_multi.assign(n_slev, 0);
-  out.sorted_off.assign(n_slev + 1, 0);
-  for (uint32_t l = 0; l < n_slev; ++l) {
+  for (uint32_t v = 0; v < np; ++v) fin[rnd[F(v)]][depth[v]].push_back(v);
+  out.arr_off.assign(R + 1, 0);
+  out.fast_off.assign(R + 1, 0);
+  out.fast_multi.assign(R, 0);
+  out.sorted_off.assign(R + 1, 0);
+  out.fin_round_off.assign(R + 1, 0);
+  out.fin_off.assign(1, 0);
+  for (uint32_t r = 0; r < R; ++r) {
+    out.arr_ops.insert(out.arr_ops.end(), arr[r].begin(), arr[r].end());
+    out.arr_off[r + 1] = (uint32_t)out.arr_ops.size();
     // single-replica positions first: they run a kernel variant without the routing draw
-    std::stable_partition(fast[l].begin(), fast[l].end(), [&](uint32_t v) { return out.pos[v].reps == 1; });
-    out.fast_multi[l] = out.fast_off[l];
-    for (uint32_t v : fast[l]) out.fast_multi[l] += out.pos[v].reps == 1 ? 1u : 0u;
-    out.fast_pos.insert(out.fast_pos.end(), fast[l].begin(), fast[l].end());
-    out.fast_off[l + 1] = (uint32_t)out.fast_pos.size();
-    for (int32_t s : srt[l]) {
+    std::stable_partition(fast[r].begin(), fast[r].end(), [&](uint32_t v) { return out.pos[v].reps == 1; });
+    out.fast_multi[r] = out.fast_off[r];
+    for (uint32_t v : fast[r]) out.fast_multi[r] += out.pos[v].reps == 1 ? 1u : 0u;
+    out.fast_pos.insert(out.fast_pos.end(), fast[r].begin(), fast[r].end());
+    out.fast_off[r + 1] = (uint32_t)out.fast_pos.size();
+    for (int32_t s : srt[r]) {
       DesSortSvc ss;
       ss.row = (uint32_t)p.svc_row[s];
       ss.reps = (uint32_t)std::max<int32_t>(1, g.services[s].num_replicas);
@@ -190,7 +275,13 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       out.max_sort_pos = std::max(out.max_sort_pos, ss.pos_cnt);
       out.sorted.push_back(ss);
     }
-    out.sorted_off[l + 1] = (uint32_t)out.sorted.size();
+    out.sorted_off[r + 1] = (uint32_t)out.sorted.size();
+    for (uint32_t d = out.n_levels; d-- > 0;) {
+      if (fin[r][d].empty()) continue;
+      out.fin_pos.insert(out.fin_pos.end(), fin[r][d].begin(), fin[r][d].end());
+      out.fin_off.push_back((uint32_t)out.fin_pos.size());
+    }
+    out.fin_round_off[r + 1] = (uint32_t)out.fin_off.size() - 1;
   }
   out.slot_mult = p.stream_mult;
   return ISIM_OK;

@@ -8,8 +8,9 @@
  * A plain sequential discrete-event simulation: one global binary heap of
  * invocation ARRIVE events ordered by (time, trace id, hop id); each replica
  * is a FIFO queue in front of one worker, held for the invocation's hold time
- * (its sleep total); an invocation's script starts when the worker takes it,
- * and its calls are sent when its call step begins.  After the heap drains,
+ * (its sleep total); an invocation's script starts when the worker takes it;
+ * a call step sends its requests when it begins and ends when its last
+ * callee finishes, then the script goes on (any number of call steps).  After the heap drains,
  * each trace's finish times, statuses and stats are computed by recursion
  * over the SERVICE GRAPH (as isim_oracle.c's invoke() does), so this shares
  * no code or layout with the product's position arrays and level scans.
@@ -277,6 +278,80 @@ static uint64_t finish(fstate *f, int32_t s, uint32_t hop, int *err) {
     return T;
 }
 
+/* ---- per-invocation script progress during the simulation: a call step
+ * sends its requests when it begins and ends when its last callee finishes
+ * (the response arrives at the callee's finish); the script then goes on */
+#define NO_PARENT 0xFFFFFFFFu
+typedef struct {
+    uint64_t T, runmax;
+    uint32_t parent, next, step, pending;
+    int32_t svc;
+} istate;
+
+typedef struct {
+    const sctx *c;
+    heap *h;
+    istate *is;      /* [n_traces][nodes] */
+    uint32_t nodes;
+    uint64_t trace_begin;
+} sim;
+
+static int advance(sim *m, uint64_t i, uint32_t hop);
+
+static int notify(sim *m, uint64_t i, uint32_t hop, uint64_t fin) {
+    istate *st = &m->is[i * m->nodes + hop];
+    if (fin > st->runmax) st->runmax = fin;
+    if (--st->pending) return 1;
+    st->T = st->runmax;
+    return advance(m, i, hop);
+}
+
+static int push_call(sim *m, uint64_t i, istate *st, uint32_t hop, const ocmd *x) {
+    const ograph *g = m->c->g;
+    const int32_t cs = g->site_callee[x->site];
+    const uint32_t ch = st->next;
+    st->next += m->c->size[cs];
+    istate *cst = &m->is[i * m->nodes + ch];
+    cst->parent = hop;
+    cst->svc = cs;
+    ev ce = {st->T + g->site_hop[x->site], m->trace_begin + i, ch, cs};
+    st->pending++;
+    return hpush(m->h, ce);
+}
+
+static int advance(sim *m, uint64_t i, uint32_t hop) {
+    const ograph *g = m->c->g;
+    istate *st = &m->is[i * m->nodes + hop];
+    const int32_t s = st->svc;
+    while (st->step < (uint32_t)g->step_len[s]) {
+        const ocmd *x = &g->cmds[g->step_off[s] + st->step];
+        st->step++;
+        if (x->kind == K_SLEEP) {
+            st->T += sl(x->sleep_ns);
+        } else if (x->kind == K_CALL) {
+            st->runmax = st->T;
+            if (!push_call(m, i, st, hop, x)) return 0;
+            return 1;  /* waits for the callee */
+        } else {
+            uint64_t smax = 0;
+            for (int32_t j = 0; j < x->sub_len; ++j) {
+                const ocmd *y = &g->cmds[x->sub_off + j];
+                if (y->kind == K_SLEEP && sl(y->sleep_ns) > smax) smax = sl(y->sleep_ns);
+            }
+            st->runmax = st->T + smax;
+            for (int32_t j = 0; j < x->sub_len; ++j) {
+                const ocmd *y = &g->cmds[x->sub_off + j];
+                if (y->kind == K_CALL && !push_call(m, i, st, hop, y)) return 0;
+            }
+            if (st->pending) return 1;  /* waits for all callees */
+            st->T = st->runmax;
+        }
+    }
+    /* the script has ended: respond to the caller */
+    if (st->parent != NO_PARENT) return notify(m, i, st->parent, st->T);
+    return 1;
+}
+
 uint64_t isim_oracle_des_stats_words(int32_t n_services, int32_t n_sites) {
     return ST_SVC + 2 * (uint64_t)n_services + (uint64_t)n_sites;
 }
@@ -312,6 +387,13 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
         ev e = {now, trace_begin + i, 0, p->entry};
         if (!hpush(&h, e)) return 2;
     }
+    istate *is = (istate *)calloc((size_t)n_traces * nodes, sizeof(istate));
+    if (!is) return 2;
+    for (uint64_t i = 0; i < n_traces; ++i) {
+        is[i * nodes].parent = NO_PARENT;
+        is[i * nodes].svc = p->entry;
+    }
+    sim m = {&c, &h, is, nodes, trace_begin};
     while (h.n) {
         const ev e = hpop(&h);
         const uint64_t i = e.t - trace_begin;
@@ -323,40 +405,15 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
         *b = start + c.hold[s];
         S[i * nodes + e.hop] = start;
         A[i * nodes + e.hop] = e.time;
-        /* the script runs from `start`; calls are sent when their step begins */
-        uint64_t T = start;
-        uint32_t next = e.hop + 1;
-        for (int32_t k = 0; k < g->step_len[s]; ++k) {
-            const ocmd *x = &g->cmds[g->step_off[s] + k];
-            if (x->kind == K_SLEEP) {
-                T += sl(x->sleep_ns);
-            } else if (x->kind == K_CALL) {
-                const int32_t cs = g->site_callee[x->site];
-                ev ce = {T + g->site_hop[x->site], e.t, next, cs};
-                if (!hpush(&h, ce)) return 2;
-                next += c.size[cs];
-                break;  /* DES v1: the only call step (checked by the caller) */
-            } else {
-                int any = 0;
-                for (int32_t j = 0; j < x->sub_len; ++j) {
-                    const ocmd *y = &g->cmds[x->sub_off + j];
-                    if (y->kind != K_CALL) continue;
-                    const int32_t cs = g->site_callee[y->site];
-                    ev ce = {T + g->site_hop[y->site], e.t, next, cs};
-                    if (!hpush(&h, ce)) return 2;
-                    next += c.size[cs];
-                    any = 1;
-                }
-                if (any) break;
-                uint64_t m = 0;
-                for (int32_t j = 0; j < x->sub_len; ++j) {
-                    const ocmd *y = &g->cmds[x->sub_off + j];
-                    if (sl(y->sleep_ns) > m) m = sl(y->sleep_ns);
-                }
-                T += m;
-            }
-        }
+        /* the script runs from `start` */
+        istate *st = &is[i * nodes + e.hop];
+        st->T = start;
+        st->step = 0;
+        st->pending = 0;
+        st->next = e.hop + 1;
+        if (!advance(&m, i, e.hop)) return 2;
     }
+    free(is);
     stats[5] = ~0ull;
     for (uint64_t i = 0; i < n_traces; ++i) {
         fstate f = {&c, S + i * nodes, A + i * nodes, trace_begin + i, stats, des, 0};

@@ -176,3 +176,36 @@ def test_dag_mode_b(gpu):
         s["script"] = [x for x in s["script"] if not (isinstance(x, dict) and x.get("sleep") == "50us")]
         s["errorRate"] = 0.05
     DesCase(doc, 400_000, error_mode=isim.MODE_B).compare(0, 6000)
+
+
+# ---- calls after calls (step begins)
+
+def _sleepy(doc, pre="400us", post="100us"):
+    for s in doc["services"]:
+        s["script"] = [{"sleep": pre}] + s.get("script", []) + ([{"sleep": post}] if post else [])
+    return doc
+
+
+@pytest.mark.parametrize("mean", [300_000, 3_000_000])
+def test_sequential_tree(gpu, mean):
+    DesCase(_sleepy(tree_topology(3, 4, sequential=True)), mean).compare(0, 8000)
+
+
+def test_sequential_realistic(gpu):
+    # the reference generator's default: one call step per child (mode A: in
+    # mode B a 500 would abort the later steps, not a static walk)
+    doc = realistic_topology(150, sleep_ms=(1, 3), error_rate=(0.0, 0.05))
+    DesCase(doc, 2_000_000).compare(3, 6000)
+
+
+def test_mixed_steps_and_replicas(gpu):
+    doc = tree_topology(4, 3)
+    for i, s in enumerate(doc["services"]):
+        calls = [c for st in s.get("script", []) for c in (st if isinstance(st, list) else [st])]
+        if len(calls) == 3:  # [a || b], sleep, c
+            s["script"] = [{"sleep": "200us"}, [calls[0], calls[1], {"sleep": "50us"}], {"sleep": "70us"}, calls[2]]
+        else:
+            s["script"] = [{"sleep": f"{100 + 37 * i}us"}]
+        s["numReplicas"] = 1 + i % 3
+        s["errorRate"] = 0.02
+    DesCase(doc, 500_000).compare(0, 7000)
