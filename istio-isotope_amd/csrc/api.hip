@@ -39,6 +39,8 @@ struct DevState {
   void *d_prog = nullptr;  // Ins[] (interpreters) or Node[] (draw stream)
   uint32_t *d_mult = nullptr;  // draw stream: per-slot call multiplicity
   uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
+  unsigned long long *d_work = nullptr;  // kWorkSlots sets of batch queues, zero between launches
+  uint32_t work_next = 0;                // next queue (launches in flight use distinct queues)
   void *kernel = nullptr;
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
@@ -75,6 +77,7 @@ struct isim_handler {
         (void)hipFree(kv.second.d_prog);
         (void)hipFree(kv.second.d_mult);
         (void)hipFree(kv.second.d_dur);
+        (void)hipFree(kv.second.d_work);
         (void)hipFree(kv.second.d_des_pos);
         (void)hipFree(kv.second.d_des_child);
         (void)hipFree(kv.second.d_des_level);
@@ -174,6 +177,8 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
     HIPCHK(hipMalloc(&st.d_dur, p.slot_dur.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_dur, p.slot_dur.data(), p.slot_dur.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   }
+  HIPCHK(hipMalloc(&st.d_work, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(st.d_work, 0, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   auto res = h->dev.emplace(device, st);
   out = &res.first->second;
   return ISIM_OK;
@@ -370,6 +375,7 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);
+  kp.work = st->d_work + isim::kWorkWords * (__atomic_fetch_add(&st->work_next, 1u, __ATOMIC_RELAXED) % isim::kWorkSlots);
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};

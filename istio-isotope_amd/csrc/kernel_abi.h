@@ -64,7 +64,16 @@ struct KParams {
   uint64_t t_static;        // stream kernel: the (trace-invariant) latency
   uint32_t svc_dur;         // dynamic walks: 1 = record per-service durations
   uint32_t root_dur;        // the entry's duration-table word (row | leaf bucket << 24)
+  unsigned long long *work; // batch queues (kWorkWords): zero at launch, zeroed again by the last wave
 };
+
+// Batch queues of one launch: one counter per XCD (workgroups are dealt to
+// the 8 XCDs round-robin), each on its own 128-B line, then the count of
+// waves done.  kWorkSlots sets of them per device, one per launch in flight.
+constexpr uint32_t kWorkQueues = 8;
+constexpr uint32_t kWorkLine = 16;                    // u64 words per 128-B line
+constexpr uint32_t kWorkWords = (kWorkQueues + 1) * kWorkLine;
+constexpr uint32_t kWorkSlots = 256;
 
 constexpr uint32_t kWgThreads = 1024;                 // max workgroup size (launch bound)
 constexpr uint32_t kLdsAccBytes = 64;                 // WgAcc

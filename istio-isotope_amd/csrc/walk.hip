@@ -1051,7 +1051,21 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
   constexpr uint64_t kBatch = KIND >= 4 ? 64ull * kStreamTPL : 64ull;
   const uint64_t n_batches = (kp.n_traces + kBatch - 1) / kBatch;
   const uint64_t stride = (uint64_t)gridDim.x * waves;
-  for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b += stride) {
+  // Batches: the first wave-stride statically, the rest claimed from the
+  // launch's queues, so waves the SIMD arbiter favours take more batches and
+  // the grid drains within about one batch of the last claim.  Queue q (the
+  // workgroup's XCD; every queue in use has workgroups) deals batches
+  // stride + nq c + q.
+  const uint32_t nq = gridDim.x < kWorkQueues ? gridDim.x : kWorkQueues;
+  const uint32_t q = blockIdx.x % nq;
+  unsigned long long *queue = kp.work + q * kWorkLine;
+  auto claim = [&]() -> uint64_t {
+    unsigned long long v = 0;
+    if (lane_id() == 0) v = atomicAdd(queue, 1ull);
+    const uint64_t c = (uint64_t)rfl((uint32_t)(v >> 32)) << 32 | rfl((uint32_t)v);
+    return stride + c * nq + q;
+  };
+  for (uint64_t b = (uint64_t)blockIdx.x * waves + wave; b < n_batches; b = claim()) {
     if constexpr (KIND >= 4) {
       const uint64_t base = b * 64 * kStreamTPL;
       CNode4 *st = (CNode4 *)(const __attribute__((address_space(1))) Ins *)prog;
@@ -1067,6 +1081,10 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
     else walk_dynamic<MODEB, TT>(c, kp.trace_begin, kp.n_traces, b * 64, lstk, hstk);
   }
 
+  // every wave has stopped claiming once all have counted out: the last one re-arms the queue
+  if (lane_id() == 0 && atomicAdd(kp.work + kWorkQueues * kWorkLine, 1ull) == stride - 1) {
+    for (uint32_t i = 0; i <= kWorkQueues; ++i) atomicExch(kp.work + i * kWorkLine, 0ull);
+  }
   __syncthreads();
   // ---- flush workgroup accumulators to HBM
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);

@@ -154,3 +154,41 @@ def test_mode_b_stack_depths(gpu, depth, kind):
     assert c.handler.info.max_depth == depth
     assert c.handler.launch_info(0)["kernel_kind"] == kind
     c.compare(5, 3000)
+
+
+# ---- batch queues: past the first wave-stride, waves claim batches from
+# per-XCD queues (walk.hip); each launch re-arms its queue set on exit
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_batch_queue_claims(gpu, kernel):
+    # more batches than resident waves (stream: 128 traces per batch,
+    # interpreter: 64), so most batches are claimed from the queues
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
+             isim.SimParams(flags=KERNELS[kernel]))
+    li = c.handler.launch_info(0)
+    per = 128 if li["kernel_kind"] >= 4 else 64
+    n = 3 * li["max_blocks"] * li["wg_threads"] // 64 * per + 4097
+    c.compare(11, n)
+
+
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_batch_queue_rearms(gpu, kernel):
+    import torch
+    c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
+             isim.SimParams(flags=KERNELS[kernel]))
+    li = c.handler.launch_info(0)
+    per = 128 if li["kernel_kind"] >= 4 else 64
+    n = 2 * li["max_blocks"] * li["wg_threads"] // 64 * per + 999
+    _, one = c.gpu(0, n, records=False)
+    dev = torch.device("cuda", 0)
+    st = torch.zeros(c.handler.stats_words, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    k = 300  # more launches than queue sets (kWorkSlots): every set is reused
+    for _ in range(k):
+        c.handler.serve_device(0, n, 0, st.data_ptr(), s)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy().view(np.uint64)
+    f1, fk = c.handler.fold(one), c.handler.fold(got)
+    assert fk["n_traces"] == k * n and f1["n_traces"] == n
+    assert fk["sum_latency"] == k * f1["sum_latency"] and fk["n_500"] == k * f1["n_500"]
+    assert np.array_equal(fk["site_calls"], k * f1["site_calls"])

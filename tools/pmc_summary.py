@@ -31,6 +31,19 @@ def counters(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}, meta
 
 
+CUS, WAVES_PER_CU = 256, 32  # MI355X: 8 XCDs x 32 CUs; 8 waves/SIMD x 4 SIMDs
+
+
+def occupancy(wave_cycles, grbm_gui_active, xcds=8):
+    """Mean resident waves per CU over the dispatch against the gfx950 limit
+    of 32: SQ_WAVE_CYCLES counts quad-cycles summed over every wave
+    (MI355X_MICROARCH.md, s_memtime vs SQ PMC units), GRBM_GUI_ACTIVE the
+    dispatch's cycles summed over the 8 XCDs (ibid., DVFS give-back)."""
+    waves = 4 * wave_cycles / (grbm_gui_active / xcds) / CUS
+    return {"mean_waves_per_cu": waves, "peak_waves_per_cu": WAVES_PER_CU, "frac": waves / WAVES_PER_CU,
+            "formula": "4*SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE/8) / 256 CUs"}
+
+
 def main(src, rnd):
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
@@ -79,6 +92,7 @@ def main(src, rnd):
         "waves": sq1["SQ_WAVES"],
         "grbm_gui_active": sq2["GRBM_GUI_ACTIVE"],
         "effective_clock_ghz": sq2["GRBM_GUI_ACTIVE"] / xcds / kernel_ns,
+        "occupancy": occupancy(sq1["SQ_WAVE_CYCLES"], sq2["GRBM_GUI_ACTIVE"]),
     }
     with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
