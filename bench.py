@@ -183,13 +183,14 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
     # finalize / records ~60 B per trace
     alg_bytes = B * (40 * npos + 8 * (npos - 1) + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = occupancy = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary_c5.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("batch") == B:
                 traffic = pmc.get("hbm_bytes_per_step")
+                occupancy = pmc.get("occupancy")
         except Exception:
             traffic = None
     rows = d.fold(table.cpu().numpy().view(np.uint64))
@@ -210,6 +211,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "des_* (arrivals, down and up passes of all levels, finalize) per step",
                      "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+        "occupancy": {"peak_waves_per_cu": 32, "measured": occupancy},
         "mean_latency_ns": folded["sum_latency"] / total,
         "mean_queue_wait_ns": mean_wait,
         "hop_visits_per_s": value * folded["sum_hops"] / total,
@@ -318,12 +320,15 @@ def main():
     alg_bytes = B * (0 if args.no_records else 16) + prog_bytes + info.stats_words * 8
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
+    occupancy = {"launched_waves_per_cu": launch["blocks_per_cu"] * launch["wg_threads"] // 64,
+                 "peak_waves_per_cu": 32, "measured": None}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("config") == args.config and pmc.get("batch") == B:
                 traffic = pmc.get("hbm_bytes_per_launch")
+                occupancy["measured"] = pmc.get("occupancy")
         except Exception:
             traffic = None
 
@@ -350,6 +355,7 @@ def main():
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
         "compute_roofline": compute_roofline(stream, info, B, kern_ms),
+        "occupancy": occupancy,
         "hop_visits_per_s": value * hops_per_trace,
         "n_500_frac": folded["n_500"] / total,
     }

@@ -572,6 +572,8 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   ws += al(((n_traces + 8191) / 8192 + 1) * 8);
   L.BK = (uint64_t *)ws;
   ws += al((uint64_t)d.steps.size() * ((n_traces + 7) & ~7ull) * 8);
+  L.chain = ws;
+  ws += al(isim::des_chain_bytes(d, n_traces));
   L.sort_ws = ws;
   L.d_stats = d_stats;
   L.d_table = d_des_table;

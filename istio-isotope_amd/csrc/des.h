@@ -22,6 +22,7 @@ constexpr uint32_t kDesNoParent = 0xFFFFFFFFu;
 constexpr uint32_t kDesMaxReplicas = 64;  // per-replica carries of a leaf position live in LDS
 constexpr uint32_t kDesFlagAlways = 1u;   // errorRate 1
 constexpr uint32_t kDesFlagLeaf = 2u;     // no call step
+constexpr uint32_t kDesFlagFused = 4u;    // fast-path leaf: finished by its queue pass (no up pass)
 
 // One invocation position of the unrolled tree (64 bytes, device layout).
 struct DesPos {
@@ -82,7 +83,9 @@ struct DesPlan {
   // the schedule: rounds of (step begins, queues, finishes)
   std::vector<uint32_t> arr_ops, arr_off;        // BK rows computed in round r
   std::vector<uint32_t> fast_pos, fast_off;      // single-position trace-ordered services
-  std::vector<uint32_t> fast_multi;              // [rounds]: first multi-replica position
+  // [rounds][5]: a round's fast positions by kernel variant (des_down<MULTI, FUSED>):
+  // [v][0..1) single replica, [1..2) fused single, [2..3) replicas, [3..4) fused replicas
+  std::vector<uint32_t> fast_split;
   std::vector<DesSortSvc> sorted;                // sort-path services
   std::vector<uint32_t> sorted_off;
   std::vector<uint32_t> sort_pos;                // positions of the sort-path services
@@ -100,6 +103,7 @@ struct DesLaunch {
   uint64_t *W, *A, *blk, *BK;        // workspace: [n_pos][N], [N], chunk sums, [steps][N]
   uint32_t *E;                       // workspace: [N]
   void *sort_ws;                     // workspace of the sort path (keys, values, radix-sort temp)
+  void *chain;                       // workspace: chained-scan states of the down pass (des_chain_bytes)
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;         // may be null
   uint64_t n_traces, trace_begin, mean_ns, seed;
@@ -109,6 +113,9 @@ struct DesLaunch {
 // Workspace bytes for a batch of n traces (W, A, E, chunk sums, sort path; 256-B aligned parts).
 uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n);
 int des_launch(const DesLaunch &L, void *stream);
+// Chained-scan workspace of the down pass: a ticket counter per launch, then
+// one 32-byte state per (position, chunk of kChainChunk traces); zeroed per batch.
+uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n);
 
 // Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is
 // outside the DES class.

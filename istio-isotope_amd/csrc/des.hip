@@ -39,6 +39,14 @@ constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per arriva
 #endif
 constexpr uint32_t kDownPer = ISIM_DES_DOWN_PER;        // traces per thread in the down passes
 constexpr uint32_t kDownChunk = kDownPer * kDesThreads;
+#ifndef ISIM_DES_CHAIN_THREADS
+#define ISIM_DES_CHAIN_THREADS 1024
+#endif
+constexpr uint32_t kChainThreads = ISIM_DES_CHAIN_THREADS;  // chained down pass: workgroup size
+constexpr uint32_t kChainChunk = kDownPer * kChainThreads;  // traces per chunk
+#ifndef ISIM_DES_CHAIN_BELOW
+#define ISIM_DES_CHAIN_BELOW 512  // positions per launch below which the chained scan is used
+#endif
 constexpr uint32_t kDesUpThreads = 256;
 constexpr uint64_t kMask63 = (1ull << 63) - 1;
 
@@ -84,14 +92,21 @@ __device__ __forceinline__ uint64_t des_exp_q24(uint32_t u) {
   return (uint64_t)(24 * kLn2Q24 - ((int64_t)e * kLn2Q24 + lnm));
 }
 
+// Prometheus duration bucket (prometheus/handler.go:26-35): the first edge
+// >= t.  The edges are whole milliseconds in six arithmetic runs (7..12 by 1,
+// 14..20 by 2, 25..50 by 5, 60..100 by 10, 120..200 by 20, 250..500 by 50), so
+// with m = ceil(t / 1 ms) (t <= e ms  <=>  m <= e) the bucket is the run's
+// base + ceil((m - run start) / step): ~20 integer ops instead of 32 compares.
 __device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
-  constexpr uint32_t edges_ms[32] = {7,  8,  9,  10, 11,  12,  14,  16,  18,  20,  25,  30,  35,  40,  45,  50,
-                                     60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
-  uint32_t b = 32;
-#pragma unroll
-  for (int i = 31; i >= 0; --i)
-    if (t <= (uint64_t)edges_ms[i] * 1000000ull) b = (uint32_t)i;
-  return b;
+  if (t > 500000000ull) return 32;
+  const uint32_t m = ((uint32_t)t + 999999u) / 1000000u;
+  const uint32_t lo = m <= 12 ? 7 : m <= 20 ? 12 : m <= 50 ? 20 : m <= 100 ? 50 : m <= 200 ? 100 : 200;
+  const uint32_t base = m <= 12 ? 0 : m <= 20 ? 5 : m <= 50 ? 9 : m <= 100 ? 15 : m <= 200 ? 20 : 25;
+  const uint32_t d = m <= 12 ? 1 : m <= 20 ? 2 : m <= 50 ? 5 : m <= 100 ? 10 : m <= 200 ? 20 : 50;
+  // ceil(65536 / d): exact quotients for numerators below 2^9
+  const uint32_t M = m <= 12 ? 65536 : m <= 20 ? 32768 : m <= 50 ? 13108 : m <= 100 ? 6554 : m <= 200 ? 3277 : 1311;
+  const uint32_t n = m > lo ? m - lo : 0;
+  return base + (((n + d - 1) * M) >> 16);
 }
 
 struct DesK {
@@ -122,6 +137,10 @@ struct DesK {
   const uint32_t *svals;
   uint64_t *keys;
   uint32_t *vals;
+  // chained down pass
+  struct ChainState *chain;
+  uint32_t *chain_ticket;  // this launch's ticket counter
+  uint32_t n_chunks;
 };
 
 // arrival of position v (pp = pos[v]) for trace t
@@ -143,6 +162,7 @@ __device__ __forceinline__ MaxPlus mp_then(MaxPlus first, MaxPlus second) {
 
 // Inclusive block scan of MaxPlus over kDesThreads threads (wave shuffles +
 // one LDS pass over the 16 wave totals).
+template <uint32_t NT = kDesThreads>
 __device__ __forceinline__ MaxPlus mp_block_scan(MaxPlus v, MaxPlus *wtot) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -155,15 +175,15 @@ __device__ __forceinline__ MaxPlus mp_block_scan(MaxPlus v, MaxPlus *wtot) {
   if (lane == 63) wtot[wave] = v;
   __syncthreads();
   if (wave == 0) {
-    MaxPlus w = lane < kDesThreads / 64 ? wtot[lane] : MaxPlus{0, 0};
+    MaxPlus w = lane < NT / 64 ? wtot[lane] : MaxPlus{0, 0};
 #pragma unroll
-    for (uint32_t d = 1; d < kDesThreads / 64; d <<= 1) {
+    for (uint32_t d = 1; d < NT / 64; d <<= 1) {
       MaxPlus o;
       o.B = __shfl_up(w.B, d, 64);
       o.C = __shfl_up(w.C, d, 64);
       if (lane >= d) w = mp_then(o, w);
     }
-    if (lane < kDesThreads / 64) wtot[lane] = w;
+    if (lane < NT / 64) wtot[lane] = w;
   }
   __syncthreads();
   if (wave > 0) v = mp_then(wtot[wave - 1], v);
@@ -242,18 +262,98 @@ __global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
     if (base + i < k.N) k.A[base + i] += off;
 }
 
+// hist[bin] += 1 for every lane with bin != kNoBin, one LDS atomic per
+// distinct bin of the wave (durations of one position mostly share a bin).
+// Call with the whole wave converged.
+constexpr uint32_t kNoBin = 0xFFFFFFFFu;
+__device__ __forceinline__ void hist_add_wave(uint32_t *hist, uint32_t bin) {
+  uint64_t pending = __ballot(bin != kNoBin);
+  while (pending) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)leader);
+    const uint64_t m = __ballot(bin == b);
+    if ((threadIdx.x & 63u) == leader) atomicAdd(&hist[b], (uint32_t)__builtin_popcountll(m));
+    pending &= ~m;
+  }
+}
+
+// A fused leaf (kDesFlagFused) finishes in its queue pass: F = S + script
+// time, its own error status (drawn with the loads), the duration F - a into
+// the LDS histogram.
+__device__ __forceinline__ uint32_t des_own_status(const DesK &k, uint32_t v, const DesPos &P, uint64_t t) {
+  if (P.flags & kDesFlagAlways) return 1u;
+  if (!P.thr) return 0u;
+  return des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint64_t des_leaf_finish(const DesK &k, const DesPos &P, uint64_t t, uint64_t S,
+                                                    uint64_t a, uint32_t st, uint32_t &bin, uint64_t &d0,
+                                                    uint64_t &d1, uint64_t &n5) {
+  const uint64_t F = S + P.floor;
+  const uint64_t dur = F - a;
+  if (st) atomicAdd(k.E + t, 1u);
+  n5 += st;
+  d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
+  d0 += st ? 0 : dur;
+  bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+  return F | ((uint64_t)st << 63);
+}
+
+// per-service duration statistics of a workgroup: LDS histogram + sums -> the
+// service's table row, 500s -> the call site's callee-500 counter
+template <uint32_t NT>
+__device__ __forceinline__ void des_flush_durations(const DesK &k, const DesPos &P, const uint32_t *hist,
+                                                    uint64_t d0, uint64_t d1, uint64_t n5, uint64_t *red) {
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    d0 += __shfl_xor(d0, d, 64);
+    d1 += __shfl_xor(d1, d, 64);
+    n5 += __shfl_xor(n5, d, 64);
+  }
+  constexpr uint32_t W = NT / 64;
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = d0;
+    red[W + (threadIdx.x >> 6)] = d1;
+    red[2 * W + (threadIdx.x >> 6)] = n5;
+  }
+  __syncthreads();
+  unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += NT)
+    if (hist[i]) atomicAdd(row + i, (unsigned long long)hist[i]);
+  if (threadIdx.x == 0) {
+    uint64_t s0 = 0, s1 = 0, e = 0;
+#pragma unroll 2
+    for (uint32_t i = 0; i < W; ++i) {
+      s0 += red[i];
+      s1 += red[W + i];
+      e += red[2 * W + i];
+    }
+    if (s0) atomicAdd(row + 2 * ISIM_N_PROM, (unsigned long long)s0);
+    if (s1) atomicAdd(row + 2 * ISIM_N_PROM + 1, (unsigned long long)s1);
+    if (e && P.slot != kSlotRoot)
+      atomicAdd((unsigned long long *)(k.stats + ISIM_ST_SITES + k.n_slots + P.slot), (unsigned long long)e);
+  }
+}
+
 // ---- down pass: FIFO start times, one workgroup per position of the level
-template <bool MULTI>  // MULTI: the service has replicas (routing draw per trace)
+// MULTI: the service has replicas (routing draw per trace); FUSED: leaves
+// finished here (kDesFlagFused)
+template <bool MULTI, bool FUSED>
 __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   __shared__ MaxPlus wtot[kDesThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
   __shared__ uint64_t red[2 * kDesThreads / 64];
   __shared__ MaxPlus xs[kDesThreads];
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint64_t red3[3 * kDesThreads / 64];
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
   const DesPos P = k.pos[v];
   const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
+  if constexpr (FUSED)
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
   __syncthreads();
+  uint64_t d0 = 0, d1 = 0, n5 = 0;
   const uint64_t N = k.N;
   const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
   const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
@@ -276,12 +376,14 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
 #pragma unroll
       for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
     }
+    uint32_t stm = 0;  // fused leaves: own error statuses, bit i
 #pragma unroll
     for (uint32_t i = 0; i < kDownPer; ++i) {
       if constexpr (MULTI)
         rr[i] = base + i < N ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
       else
         rr[i] = 0u;
+      if constexpr (FUSED) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
     }
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
@@ -307,6 +409,15 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
           wsum += w;
           wmax = w > wmax ? w : wmax;
           x = S + P.hold;
+        }
+      }
+      if constexpr (FUSED) {
+#pragma unroll
+        for (uint32_t i = 0; i < kDownPer; ++i) {
+          uint32_t bin = kNoBin;
+          if (base + i < N && rr[i] == r)
+            Sv[i] = des_leaf_finish(k, P, base + i, Sv[i], a[i], (stm >> i) & 1u, bin, d0, d1, n5);
+          hist_add_wave(hist, bin);
         }
       }
       if (reps == 1 && base + kDownPer <= N) {
@@ -337,6 +448,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t s = 0, m = 0;
+#pragma unroll 2
     for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
       s += red[i];
       m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
@@ -347,6 +459,194 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
     atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
     atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(N * P.hold));
   }
+  if constexpr (FUSED) des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red3);
+}
+
+// ---- down pass, single-replica services: one workgroup per (position,
+// chunk of kDownChunk traces), chunks of a position chained by a decoupled
+// look-back over their max-plus maps, so a position's queue is scanned by
+// many workgroups at once.  Workgroups take tickets in launch order
+// (position-major, chunk-minor), so every chunk they wait on has started.
+struct ChainState {
+  uint64_t B, C;   // the chunk's max-plus map (flag >= 1)
+  uint64_t P;      // the queue's carry after the chunk (flag 2)
+  uint32_t flag, pad;
+};
+static_assert(sizeof(ChainState) == 32, "ChainState is 32 bytes");
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_flag(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool FUSED>
+__global__ void __launch_bounds__(kChainThreads, 8) des_down_chain(DesK k) {
+  __shared__ MaxPlus wtot[kChainThreads / 64];
+  __shared__ MaxPlus xs[kChainThreads];
+  __shared__ uint64_t red[2 * kChainThreads / 64];
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint64_t red3[3 * kChainThreads / 64];
+  __shared__ uint32_t s_ticket;
+  __shared__ uint64_t s_carry;
+  if (threadIdx.x == 0) s_ticket = atomicAdd(k.chain_ticket, 1u);
+  if constexpr (FUSED)
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kChainThreads) hist[i] = 0;
+  __syncthreads();
+  const uint32_t ticket = s_ticket;
+  const uint32_t chunk = ticket % k.n_chunks;
+  const uint32_t v = k.level_pos[k.level_begin + ticket / k.n_chunks];
+  const DesPos P = k.pos[v];
+  const uint64_t N = k.N;
+  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
+  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
+  uint64_t *out = k.W + (uint64_t)v * k.ld;
+  ChainState *cs = k.chain + (uint64_t)v * k.n_chunks;
+  const uint64_t base = (uint64_t)chunk * kChainChunk + (uint64_t)threadIdx.x * kDownPer;
+  uint64_t a[kDownPer];
+  if (base + kDownPer <= N) {
+    const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(par + base);
+#pragma unroll
+    for (uint32_t i = 0; i < kDownPer / 2; ++i) {
+      const ulonglong2 x = q[i];
+      a[2 * i] = x.x + off;
+      a[2 * i + 1] = x.y + off;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
+  }
+  uint32_t stm = 0;
+  if constexpr (FUSED) {
+#pragma unroll
+    for (uint32_t i = 0; i < kDownPer; ++i) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
+  }
+  MaxPlus f{0, 0};
+#pragma unroll
+  for (uint32_t i = 0; i < kDownPer; ++i)
+    if (base + i < N) f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
+  const MaxPlus inc = mp_block_scan<kChainThreads>(f, wtot);
+  xs[threadIdx.x] = inc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    // wave 0: publish this chunk's map, then look back (64 chunks per step)
+    // for the carry into it.  Hand-offs between workgroups (other XCDs
+    // included) use sc1 stores drained before the flag store and sc1 loads
+    // (no L2 writeback / invalidate).
+    const uint32_t lane = threadIdx.x;
+    const MaxPlus agg = xs[kChainThreads - 1];
+    if (chunk > 0 && lane == 0) {
+      st_relaxed(&cs[chunk].B, agg.B);
+      st_relaxed(&cs[chunk].C, agg.C);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_flag(&cs[chunk].flag, 1u);
+    }
+    uint64_t cin = 0;  // chunk 0 starts from an idle worker
+    if (chunk > 0) {
+      MaxPlus tot{0, 0};  // maps of the windows already passed (applied last)
+      int64_t top = (int64_t)chunk - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t j = top - (int64_t)lane;  // lane 0 = the nearest chunk
+        const uint32_t fl = j >= 0 ? ld_flag(&cs[j].flag) : 2u;  // j < 0: the idle start, prefix 0
+        const uint64_t m0 = __ballot(fl == 0), m2 = __ballot(fl == 2);
+        const uint32_t f2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+        const uint64_t below = f2 >= 64 ? ~0ull : ((1ull << f2) - 1);
+        if (m0 & below) {  // a chunk this one needs has not published yet
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 26)) break;  // never expected: tickets order the chunks
+          continue;
+        }
+        MaxPlus m{0, 0};
+        uint64_t pv = 0;
+        if (lane < f2 && j >= 0) m = MaxPlus{ld_relaxed(&cs[j].B), ld_relaxed(&cs[j].C)};
+        if (lane == f2 && j >= 0) pv = ld_relaxed(&cs[j].P);
+        // the window's maps, the farthest (highest lane) applied first
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+          const MaxPlus o{__shfl_xor(m.B, d, 64), __shfl_xor(m.C, d, 64)};
+          m = (lane & d) ? mp_then(m, o) : mp_then(o, m);
+        }
+        tot = mp_then(m, tot);
+        if (f2 < 64) {
+          const uint64_t x = __shfl(pv, f2, 64);
+          cin = x + tot.B > tot.C ? x + tot.B : tot.C;
+          break;
+        }
+        top -= 64;
+      }
+    }
+    if (lane == 0) {
+      const uint64_t pout = cin + agg.B > agg.C ? cin + agg.B : agg.C;
+      st_relaxed(&cs[chunk].P, pout);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_flag(&cs[chunk].flag, 2u);
+      s_carry = cin;
+    }
+  }
+  __syncthreads();
+  const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
+  const uint64_t cin = s_carry;
+  uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+  uint64_t Sv[kDownPer];
+  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kDownPer; ++i) {
+    Sv[i] = 0;
+    uint32_t bin = kNoBin;
+    if (base + i < N) {
+      const uint64_t S = x > a[i] ? x : a[i];
+      const uint64_t w = S - a[i];
+      wsum += w;
+      wmax = w > wmax ? w : wmax;
+      x = S + P.hold;
+      Sv[i] = FUSED ? des_leaf_finish(k, P, base + i, S, a[i], (stm >> i) & 1u, bin, d0, d1, n5) : S;
+    }
+    if constexpr (FUSED) hist_add_wave(hist, bin);
+  }
+  if (base + kDownPer <= N) {
+    ulonglong2 *q = reinterpret_cast<ulonglong2 *>(out + base);
+#pragma unroll
+    for (uint32_t i = 0; i < kDownPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kDownPer; ++i)
+      if (base + i < N) out[base + i] = Sv[i];
+  }
+#pragma unroll
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d, 64);
+    const uint64_t o = __shfl_xor(wmax, d, 64);
+    wmax = o > wmax ? o : wmax;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = wsum;
+    red[kChainThreads / 64 + (threadIdx.x >> 6)] = wmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t s = 0, m = 0;
+#pragma unroll 2
+    for (uint32_t i = 0; i < kChainThreads / 64; ++i) {
+      s += red[i];
+      m = red[kChainThreads / 64 + i] > m ? red[kChainThreads / 64 + i] : m;
+    }
+    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
+    if (chunk == 0) {
+      atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)N);
+      atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(N * P.hold));
+    }
+    if (s) atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
+    if (m) atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
+  }
+  if constexpr (FUSED) des_flush_durations<kChainThreads>(k, P, hist, d0, d1, n5, red3);
 }
 
 // ---- up pass: finish times, statuses, per-service durations
@@ -405,7 +705,8 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
 #pragma unroll
     for (uint32_t j = 0; j < U; ++j) {
       const uint64_t t = t0 + j * kDesUpThreads;
-      if (t >= te) continue;
+      uint32_t bin = kNoBin;
+      if (t < te) {
       const uint64_t F = leaf ? m[j] : m[j] + P.post;
       uint32_t own = 0;
       if (P.flags & kDesFlagAlways) own = 1;
@@ -420,37 +721,12 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
       } else {
         dsum0 += dur;
       }
-      atomicAdd(&hist[st * ISIM_N_PROM + des_prom_bucket(dur)], 1u);
+      bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+      }
+      hist_add_wave(hist, bin);
     }
   }
-#pragma unroll
-  for (uint32_t d = 32; d > 0; d >>= 1) {
-    dsum0 += __shfl_xor(dsum0, d, 64);
-    dsum1 += __shfl_xor(dsum1, d, 64);
-    n500 += __shfl_xor(n500, d, 64);
-  }
-  constexpr uint32_t W = kDesUpThreads / 64;
-  if ((threadIdx.x & 63u) == 0) {
-    red[threadIdx.x >> 6] = dsum0;
-    red[W + (threadIdx.x >> 6)] = dsum1;
-    red[2 * W + (threadIdx.x >> 6)] = n500;
-  }
-  __syncthreads();
-  unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
-  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads)
-    if (hist[i]) atomicAdd(row + i, (unsigned long long)hist[i]);
-  if (threadIdx.x == 0) {
-    uint64_t s0 = 0, s1 = 0, e = 0;
-    for (uint32_t i = 0; i < W; ++i) {
-      s0 += red[i];
-      s1 += red[W + i];
-      e += red[2 * W + i];
-    }
-    if (s0) atomicAdd(row + 2 * ISIM_N_PROM, (unsigned long long)s0);
-    if (s1) atomicAdd(row + 2 * ISIM_N_PROM + 1, (unsigned long long)s1);
-    if (e && P.slot != kSlotRoot)
-      atomicAdd((unsigned long long *)(k.stats + ISIM_ST_SITES + k.n_slots + P.slot), (unsigned long long)e);
-  }
+  des_flush_durations<kDesUpThreads>(k, P, hist, dsum0, dsum1, n500, red);
 }
 
 // ---- finalize: records and the latency statistics
@@ -613,6 +889,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t s = 0, m = 0;
+#pragma unroll 2
     for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
       s += red[i];
       m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
@@ -666,7 +943,14 @@ uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n) {
   const uint64_t m = (uint64_t)plan.max_sort_pos * n;
   const uint64_t sort = m ? 2 * al(m * 8) + 2 * al(m * 4) + al(sort_temp_bytes(m)) : 0;
   return al((uint64_t)plan.pos.size() * ld * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8) +
-         al((uint64_t)plan.steps.size() * ld * 8) + sort;
+         al((uint64_t)plan.steps.size() * ld * 8) + al(des_chain_bytes(plan, n)) + sort;
+}
+
+static uint64_t chain_tickets(const DesPlan &plan) { return 4ull * plan.rounds(); }
+
+uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n) {
+  const uint64_t chunks = (n + dev::kChainChunk - 1) / dev::kChainChunk;
+  return ((chain_tickets(plan) * 4 + 255) & ~255ull) + (uint64_t)plan.pos.size() * chunks * sizeof(dev::ChainState);
 }
 
 int des_launch(const DesLaunch &L, void *stream_) {
@@ -697,6 +981,11 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.modeb = L.modeb;
   k.n_blk = (uint32_t)((L.n_traces + kDesChunk - 1) / kDesChunk);
   if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
+  const uint64_t tk_bytes = (chain_tickets(*L.plan) * 4 + 255) & ~255ull;
+  if (hipMemsetAsync(L.chain, 0, des_chain_bytes(*L.plan, L.n_traces), stream) != hipSuccess) return 1;
+  uint32_t *tickets = (uint32_t *)L.chain;
+  k.chain = (ChainState *)((char *)L.chain + tk_bytes);
+  k.n_chunks = (uint32_t)((L.n_traces + kChainChunk - 1) / kChainChunk);
   hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
@@ -727,17 +1016,22 @@ int des_launch(const DesLaunch &L, void *stream_) {
     }
     // 2. queues: single-position trace-ordered services scan in place, the
     //    others sort their arrivals first
-    const uint32_t nf = pl.fast_off[r + 1] - pl.fast_off[r];
-    if (nf) {
-      k.level_pos = L.d_fast_pos;
-      const uint32_t n1 = pl.fast_multi[r] - pl.fast_off[r];
-      if (n1) {
-        k.level_begin = pl.fast_off[r];
-        hipLaunchKernelGGL(des_down<false>, dim3(n1), dim3(kDesThreads), 0, stream, k);
-      }
-      if (nf > n1) {
-        k.level_begin = pl.fast_multi[r];
-        hipLaunchKernelGGL(des_down<true>, dim3(nf - n1), dim3(kDesThreads), 0, stream, k);
+    k.level_pos = L.d_fast_pos;
+    // single-replica groups narrower than the chip take the chained scan
+    // (many workgroups per position); wide groups and replicated services
+    // one workgroup per position
+    static void (*const down[4])(DesK) = {des_down<false, false>, des_down<false, true>, des_down<true, false>,
+                                         des_down<true, true>};
+    static void (*const chain[2])(DesK) = {des_down_chain<false>, des_down_chain<true>};
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t b = pl.fast_split[5 * r + j], e = pl.fast_split[5 * r + j + 1];
+      if (e == b) continue;
+      k.level_begin = b;
+      if (j < 2 && e - b < ISIM_DES_CHAIN_BELOW) {
+        k.chain_ticket = tickets + 4 * r + j;
+        hipLaunchKernelGGL(chain[j], dim3((e - b) * k.n_chunks), dim3(kChainThreads), 0, stream, k);
+      } else {
+        hipLaunchKernelGGL(down[j], dim3(e - b), dim3(kDesThreads), 0, stream, k);
       }
     }
     for (uint32_t si = pl.sorted_off[r]; si < pl.sorted_off[r + 1]; ++si) {

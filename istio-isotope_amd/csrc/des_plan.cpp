@@ -245,23 +245,39 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (svc_pos[s].empty()) continue;
     bool need = svc_pos[s].size() > 1;
     for (uint32_t v : svc_pos[s]) need = need || !arr_sorted[v];
-    if (need) srt[rnd[s]].push_back(s);
-    else fast[rnd[s]].push_back(svc_pos[s][0]);
+    if (need) {
+      srt[rnd[s]].push_back(s);
+    } else {
+      const uint32_t v = svc_pos[s][0];
+      fast[rnd[s]].push_back(v);
+      // a leaf's finish needs only its start: the queue pass writes F (every
+      // reader of F(v) runs in a later stage of Q(v)'s round or later)
+      if (out.pos[v].flags & kDesFlagLeaf) out.pos[v].flags |= kDesFlagFused;
+    }
   }
-  for (uint32_t v = 0; v < np; ++v) fin[rnd[F(v)]][depth[v]].push_back(v);
+  for (uint32_t v = 0; v < np; ++v)
+    if (!(out.pos[v].flags & kDesFlagFused)) fin[rnd[F(v)]][depth[v]].push_back(v);
   out.arr_off.assign(R + 1, 0);
   out.fast_off.assign(R + 1, 0);
-  out.fast_multi.assign(R, 0);
+  out.fast_split.assign(5 * R, 0);
   out.sorted_off.assign(R + 1, 0);
   out.fin_round_off.assign(R + 1, 0);
   out.fin_off.assign(1, 0);
   for (uint32_t r = 0; r < R; ++r) {
     out.arr_ops.insert(out.arr_ops.end(), arr[r].begin(), arr[r].end());
     out.arr_off[r + 1] = (uint32_t)out.arr_ops.size();
-    // single-replica positions first: they run a kernel variant without the routing draw
-    std::stable_partition(fast[r].begin(), fast[r].end(), [&](uint32_t v) { return out.pos[v].reps == 1; });
-    out.fast_multi[r] = out.fast_off[r];
-    for (uint32_t v : fast[r]) out.fast_multi[r] += out.pos[v].reps == 1 ? 1u : 0u;
+    // grouped by kernel variant: single replica (no routing draw) or not, fused leaf or not
+    auto variant = [&](uint32_t v) {
+      return (out.pos[v].reps > 1 ? 2u : 0u) + ((out.pos[v].flags & kDesFlagFused) ? 1u : 0u);
+    };
+    std::stable_sort(fast[r].begin(), fast[r].end(),
+                     [&](uint32_t a, uint32_t b) { return variant(a) < variant(b); });
+    uint32_t at = out.fast_off[r];
+    for (uint32_t j = 0; j < 4; ++j) {
+      out.fast_split[5 * r + j] = at;
+      for (uint32_t v : fast[r]) at += variant(v) == j ? 1u : 0u;
+    }
+    out.fast_split[5 * r + 4] = at;
     out.fast_pos.insert(out.fast_pos.end(), fast[r].begin(), fast[r].end());
     out.fast_off[r + 1] = (uint32_t)out.fast_pos.size();
     for (int32_t s : srt[r]) {

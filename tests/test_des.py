@@ -48,6 +48,32 @@ def test_exp_q24_is_exponential():
     assert np.max(np.abs(e - exact)) < 2e-5
 
 
+def test_piecewise_duration_bucket():
+    # des.hip des_prom_bucket: the 32 Prometheus duration edges are six
+    # arithmetic runs of whole milliseconds; its closed form (restated here)
+    # equals the first-edge->=t search for every t (the GPU tables are
+    # checked bit-exact against the oracle in test_des_gpu.py)
+    from isim.prometheus import DURATION_BUCKETS
+    edges = [round(e * 1000) for e in DURATION_BUCKETS]
+
+    def search(t):
+        return next((i for i, e in enumerate(edges) if t <= e * 1_000_000), 32)
+
+    def closed(t):
+        if t > 500_000_000:
+            return 32
+        m = (t + 999_999) // 1_000_000
+        lo, base, d = next(r for r in ((12, 7, 0, 1), (20, 12, 5, 2), (50, 20, 9, 5), (100, 50, 15, 10),
+                                       (200, 100, 20, 20), (10 ** 9, 200, 25, 50)) if m <= r[0])[1:]
+        n = max(0, m - lo)
+        return base + (((n + d - 1) * -(-65536 // d)) >> 16)
+
+    rng = np.random.default_rng(5)
+    ts = [max(0, e * 1_000_000 + dd) for e in range(0, 505) for dd in (-1, 0, 1, 499_999, 999_999)]
+    ts += rng.integers(0, 600_000_000, 20000).tolist()
+    assert all(search(t) == closed(t) for t in ts)
+
+
 def canonical_concurrent(sleep="300us"):
     """example-topologies/canonical.yaml with every service's calls in one
     concurrent step (a and b are then invoked twice per trace: a DAG)."""

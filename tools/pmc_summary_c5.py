@@ -15,6 +15,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import occupancy  # noqa: E402
 
 
 def per_run(path, counter):
@@ -29,7 +31,9 @@ def main(src, rnd):
     dst = os.path.join(ROOT, "profiles", rnd, "c5")
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-    for p in ("fetch", "write"):
+    for p in ("fetch", "write", "sq"):
+        if not os.path.exists(os.path.join(src, p, "run_counter_collection.csv")):
+            continue
         shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
     line = [l for l in open(os.path.join(src, "stats.log")) if l.startswith("{")][-1]
     open(os.path.join(dst, "bench_under_rocprof.json"), "w").write(line)
@@ -53,6 +57,10 @@ def main(src, rnd):
         "hbm_bytes_note": "gfx950 correction: FETCH_SIZE doubled; WRITE_SIZE as-is; summed over every des_* "
                           "dispatch of a step",
     }
+    sq = os.path.join(src, "sq", "run_counter_collection.csv")
+    if os.path.exists(sq):
+        # dispatch-time-weighted over every des_* dispatch (pmc_summary.occupancy)
+        out["occupancy"] = occupancy(per_run(sq, "SQ_WAVE_CYCLES"), per_run(sq, "GRBM_GUI_ACTIVE"))
     json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_summary_c5.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
