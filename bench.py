@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
+                    "64-bit only when a batch's latencies reach 2^31 ns)")
     ap.add_argument("--mean-interarrival-ns", type=int, default=6_000_000,
                     help="c5 (DES): mean gap of the open-loop Poisson arrivals")
     ap.add_argument("--mode", default="A", choices=["A", "B"])
@@ -143,25 +145,41 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
+    # 32-bit rows unless a batch's latencies reach 2^31 ns (isim.h ISIM_ST_DES_RETRY): then 64-bit rows
+    wide = [bool(args.wide_rows)]
+
     def step(s):
         begin = shard_begin(rank, world, s, B)
         d.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), table.data_ptr(),
-                       ws.data_ptr(), wsb, sptr)
+                       ws.data_ptr(), wsb, sptr, wide=wide[0])
+
+    def retried():
+        t = stats[isim.native.ST_DES_RETRY:isim.native.ST_DES_RETRY + 1].clone()
+        if world > 1:
+            dist.all_reduce(t)
+        return int(t.item()) > 0
 
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
-    stats.zero_()
-    table.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step(args.warmup + i)
-        ev[i][1].record(stream)
+    if retried():
+        wide[0] = True
+    for attempt in range(2):
+        stats.zero_()
+        table.zero_()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            ev[i][0].record(stream)
+            step(args.warmup + i)
+            ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        if wide[0] or not retried():
+            break
+        wide[0] = True  # a timed batch overflowed the 32-bit rows: time the run again with 64-bit rows
     if world > 1:
         merge_stats(stats)
     torch.cuda.synchronize()
@@ -178,10 +196,14 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
     assert folded["n_traces"] == total, (folded["n_traces"], total)
     value = total / elapsed
     npos = d.info.n_positions
-    # algorithmic bytes of one step: down pass 16 B and up
-    # pass 24 B per (position, trace), 8 B per (child edge, trace), arrivals /
-    # finalize / records ~60 B per trace
-    alg_bytes = B * (40 * npos + 8 * (npos - 1) + 44 + (0 if args.no_records else 16))
+    # algorithmic bytes of one step, R = row bytes (4 or 8):
+    # queue pass 2R per (position, trace) (arrival row read, start / fused
+    # finish written), up pass 3R per (non-fused position, trace) (start,
+    # arrival row, finish) + R per (child edge, trace); arrivals / finalize /
+    # records ~60 B per trace
+    R = 8 if wide[0] else 4
+    nf = d.info.n_fused
+    alg_bytes = B * (R * (2 * npos + 3 * (npos - nf) + (npos - 1)) + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = occupancy = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary_c5.json")
@@ -206,6 +228,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
                        mean_interarrival_ns=args.mean_interarrival_ns,
                        parallelism=f"replicas x{world}", records=not args.no_records,
                        des_levels=d.info.n_levels, des_max_width=d.info.max_width,
+                       des_fused_leaves=d.info.n_fused, des_rows="u64" if wide[0] else "u32",
                        workspace_bytes=wsb),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

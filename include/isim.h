@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 3
+#define ISIM_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -101,6 +101,8 @@ typedef struct {
 #define ISIM_ST_N_500 4
 #define ISIM_ST_NOT_MIN_LATENCY 5 /* ~min latency (so min and max both merge with MAX) */
 #define ISIM_ST_MAX_LATENCY 6
+#define ISIM_ST_DES_RETRY 7       /* DES batches NOT accumulated: a latency reached 2^31 ns in 32-bit rows;
+                                     rerun them with ISIM_DES_FLAG_WIDE (isim_serve_des does) */
 #define ISIM_ST_PROM 8            /* [2][33] latency histogram, Prometheus duration buckets
                                      (prometheus/handler.go:26-31), index [status500][bucket] */
 #define ISIM_N_PROM 33
@@ -233,13 +235,17 @@ ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *st
  * handler.go:37-79) starts when the worker takes it.  Statuses, hops and
  * call counters are those of the static walk; latencies and the per-service
  * durations include queueing.  Exact (bit-identical to the sequential
- * event-driven oracle) for the DES v1 graph class: static walks whose
- * services are invoked at most once per trace, whose scripts have at most
- * one step with calls, and whose multi-replica services are leaves
- * (isim_des_info_get returns ISIM_EINVAL with the reason otherwise). */
+ * event-driven oracle) for the DES graph class of DESIGN.md §10.1: static
+ * walks of at most 2^24 invocations and 64 replicas per service whose
+ * call-step schedule is acyclic (isim_des_info_get returns ISIM_EINVAL with
+ * the reason otherwise).  Times are kept per trace relative to its arrival:
+ * in 32-bit rows by default; a batch with a latency of 2^31 ns (2.1 s) or
+ * more is then not accumulated (ISIM_ST_DES_RETRY counts it) and must be
+ * rerun with ISIM_DES_FLAG_WIDE (64-bit rows). */
+#define ISIM_DES_FLAG_WIDE 1u    /* 64-bit rows: any latency */
 typedef struct {
   uint64_t mean_interarrival_ns; /* 1 .. 2^34: mean gap of the exponential arrivals */
-  uint32_t flags;                /* must be 0 */
+  uint32_t flags;                /* 0 or ISIM_DES_FLAG_WIDE */
   uint32_t reserved;             /* must be 0 */
 } isim_des_params;
 
@@ -248,10 +254,12 @@ typedef struct {
   int32_t n_levels;              /* depth of the invocation tree */
   int32_t max_width;             /* widest level */
   int32_t table_rows;            /* rows of the DES table (reachable services) */
+  int32_t n_fused;               /* leaf positions finished in their queue pass (no up pass) */
+  int32_t reserved;
 } isim_des_info;
 
 ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);
-/* Device workspace a batch of n_traces needs (8 B per invocation per trace + 20 B per trace). */
+/* Device workspace a batch of n_traces needs (either row width: 8 B per invocation per trace + ~40 B per trace). */
 ISIM_API int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes);
 /* One DES batch (trace ids [trace_begin, trace_begin+n_traces), arrivals from
  * time 0, all replicas idle) on the current device, asynchronously on

@@ -520,13 +520,14 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   out->n_levels = (int32_t)h->des.n_levels;
   out->max_width = (int32_t)h->des.max_width;
   out->table_rows = (int32_t)h->prog.row_svc.size();
+  for (const auto &q : h->des.pos) out->n_fused += (q.flags & isim::kDesFlagFused) ? 1 : 0;
   return ISIM_OK;
 }
 
 int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
   if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
   if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
-  *bytes = isim::des_workspace_bytes(h->des, n_traces);
+  *bytes = isim::des_workspace_bytes(h->des, n_traces, stats_words(h), h->prog.row_svc.size());
   return ISIM_OK;
 }
 
@@ -536,7 +537,8 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   if (!h || !dp || !d_stats || !d_des_table) return fail(ISIM_EINVAL, "null argument");
   if (dp->mean_interarrival_ns == 0 || dp->mean_interarrival_ns > (1ull << 34))
     return fail(ISIM_EINVAL, "mean_interarrival_ns must be in [1, 2^34]");
-  if (dp->reserved != 0 || dp->flags != 0) return fail(ISIM_EINVAL, "isim_des_params.flags/reserved must be 0");
+  if (dp->reserved != 0 || (dp->flags & ~ISIM_DES_FLAG_WIDE) != 0)
+    return fail(ISIM_EINVAL, "isim_des_params.flags must be 0 or ISIM_DES_FLAG_WIDE, reserved 0");
   if (n_traces == 0) return ISIM_OK;
   if (n_traces > (1ull << 31)) return fail(ISIM_EINVAL, "n_traces above 2^31 per DES batch");
   int device = 0;
@@ -545,14 +547,13 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   int rc = des_prepare(h, device, st);
   if (rc != ISIM_OK) return rc;
   const isim::DesPlan &d = h->des;
-  const uint32_t np = (uint32_t)d.pos.size();
   if (n_traces * (uint64_t)std::max<uint32_t>(1, d.max_sort_pos) > 0xFFFFFFFFull)
     return fail(ISIM_EINVAL, "n_traces x positions of one service above 2^32 per DES batch");
-  if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(d, n_traces))
+  const uint64_t words = stats_words(h);
+  const uint32_t rows = (uint32_t)h->prog.row_svc.size();
+  if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(d, n_traces, words, rows))
     return fail(ISIM_EINVAL, "DES workspace smaller than isim_des_workspace_bytes()");
-  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-  char *ws = (char *)d_workspace;
-  isim::DesLaunch L;
+  isim::DesLaunch L{};
   L.plan = &d;
   L.d_pos = st->d_des_pos;
   L.d_ext = st->d_des_ext;
@@ -562,19 +563,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.d_arr_ops = st->d_des_arr;
   L.d_fast_pos = st->d_des_fast;
   L.d_sort_pos = st->d_des_sort;
-  L.W = (uint64_t *)ws;
-  ws += al((uint64_t)np * ((n_traces + 7) & ~7ull) * 8);
-  L.A = (uint64_t *)ws;
-  ws += al(n_traces * 8);
-  L.E = (uint32_t *)ws;
-  ws += al(n_traces * 4);
-  L.blk = (uint64_t *)ws;
-  ws += al(((n_traces + 8191) / 8192 + 1) * 8);
-  L.BK = (uint64_t *)ws;
-  ws += al((uint64_t)d.steps.size() * ((n_traces + 7) & ~7ull) * 8);
-  L.chain = ws;
-  ws += al(isim::des_chain_bytes(d, n_traces));
-  L.sort_ws = ws;
+  L.d_mult = st->d_des_mult;
   L.d_stats = d_stats;
   L.d_table = d_des_table;
   L.d_records = d_records;
@@ -582,17 +571,14 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.trace_begin = trace_begin;
   L.mean_ns = dp->mean_interarrival_ns;
   L.seed = h->params.seed;
-  L.n_pos = np;
+  L.stats_words = words;
+  L.table_rows = rows;
+  L.n_pos = (uint32_t)d.pos.size();
   L.n_slots = (uint32_t)h->prog.n_slots;
   L.modeb = h->params.error_mode == ISIM_MODE_B ? 1u : 0u;
+  L.wide = (dp->flags & ISIM_DES_FLAG_WIDE) != 0;
+  isim::des_carve(L, d_workspace);
   if (isim::des_launch(L, hip_stream) != 0) return fail(ISIM_EHIP, "DES kernel launch failed");
-  if (h->prog.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
-    uint32_t n_slots = (uint32_t)h->prog.n_slots;
-    const uint32_t *mult = st->d_des_mult;
-    void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};
-    HIPCHK(hipLaunchKernel(isim::stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args2, 0,
-                           (hipStream_t)hip_stream));
-  }
   return ISIM_OK;
 }
 
@@ -605,7 +591,7 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
   HIPCHK(hipSetDevice(device));
   const uint64_t words = stats_words(h);
   const uint64_t tab_words = (uint64_t)h->prog.row_svc.size() * ISIM_DES_ROW_WORDS;
-  const uint64_t ws_bytes = isim::des_workspace_bytes(h->des, n_traces);
+  const uint64_t ws_bytes = isim::des_workspace_bytes(h->des, n_traces, words, h->prog.row_svc.size());
   uint64_t *d_stats = nullptr, *d_tab = nullptr;
   void *d_ws = nullptr;
   isim_trace_rec *d_rec = nullptr;
@@ -622,12 +608,25 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
       rc = fail(ISIM_EHIP, "hipMalloc(records) failed");
       break;
     }
-    if (hipMemsetAsync(d_stats, 0, words * 8, s) != hipSuccess ||
-        hipMemsetAsync(d_tab, 0, tab_words * 8 + 8, s) != hipSuccess) {
-      rc = fail(ISIM_EHIP, "hipMemset failed");
-      break;
+    // 32-bit rows first; a batch they cannot hold (ISIM_ST_DES_RETRY) again with 64-bit rows
+    isim_des_params p = *dp;
+    for (int pass = 0; pass < 2; ++pass) {
+      if (hipMemsetAsync(d_stats, 0, words * 8, s) != hipSuccess ||
+          hipMemsetAsync(d_tab, 0, tab_words * 8 + 8, s) != hipSuccess) {
+        rc = fail(ISIM_EHIP, "hipMemset failed");
+        break;
+      }
+      rc = isim_serve_des_device(h, &p, trace_begin, n_traces, d_rec, d_stats, d_tab, d_ws, ws_bytes + 8, s);
+      if (rc != ISIM_OK || (p.flags & ISIM_DES_FLAG_WIDE)) break;
+      uint64_t retry = 0;
+      if (hipMemcpyAsync(&retry, d_stats + ISIM_ST_DES_RETRY, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        rc = fail(ISIM_EHIP, "DES retry check failed");
+        break;
+      }
+      if (!retry) break;
+      p.flags |= ISIM_DES_FLAG_WIDE;
     }
-    rc = isim_serve_des_device(h, dp, trace_begin, n_traces, d_rec, d_stats, d_tab, d_ws, ws_bytes + 8, s);
     if (rc != ISIM_OK) break;
     if (h_stats && hipMemcpyAsync(h_stats, d_stats, words * 8, hipMemcpyDeviceToHost, s) != hipSuccess) {
       rc = fail(ISIM_EHIP, "copy stats failed");

@@ -100,21 +100,33 @@ struct DesLaunch {
   const DesPlan *plan;               // host copy (the schedule)
   const void *d_pos, *d_ext, *d_steps;  // DesPos[n_pos], DesPosExt[n_pos], DesStep[]
   const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops;
-  uint64_t *W, *A, *blk, *BK;        // workspace: [n_pos][N], [N], chunk sums, [steps][N]
-  uint32_t *E;                       // workspace: [N]
-  void *sort_ws;                     // workspace of the sort path (keys, values, radix-sort temp)
-  void *chain;                       // workspace: chained-scan states of the down pass (des_chain_bytes)
+  const uint32_t *d_mult;            // per slot: calls per trace (executed-call counters)
+  // workspace parts (des_carve)
+  void *W, *BK;                      // rows [n_pos][ld], [steps][ld] of u32 (narrow) or u64
+  uint64_t *A, *blk;                 // [N] arrival times, chunk sums
+  uint32_t *E;                       // [N] per-trace 500 count
+  void *chain;                       // chained-scan states of the down pass (des_chain_bytes)
+  uint32_t *ovf;                     // narrow rows: overflow flag
+  uint64_t *stage;                   // narrow rows: staged stats (stats_words) + table
+  void *sort_ws;                     // sort path (keys, values, radix-sort temp)
+  // caller buffers
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;         // may be null
   uint64_t n_traces, trace_begin, mean_ns, seed;
+  uint64_t stats_words;
+  uint32_t table_rows;
   uint32_t n_pos, n_slots, modeb;
+  bool wide;                         // u64 rows (ISIM_DES_FLAG_WIDE); else u32 rows + overflow retry
 };
 
-// Workspace bytes for a batch of n traces (W, A, E, chunk sums, sort path; 256-B aligned parts).
-uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n);
+// Workspace bytes for a batch of n traces (every part 256-B aligned; rows
+// sized for u64 so one workspace serves both row widths).
+uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n, uint64_t stats_words, uint64_t table_rows);
+// Points L's workspace parts into `workspace` (L.plan, n_traces, stats_words, table_rows set).
+void des_carve(DesLaunch &L, void *workspace);
 int des_launch(const DesLaunch &L, void *stream);
 // Chained-scan workspace of the down pass: a ticket counter per launch, then
-// one 32-byte state per (position, chunk of kChainChunk traces); zeroed per batch.
+// one 32-byte state per (position, chunk of 4096 traces); zeroed per batch.
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n);
 
 // Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is

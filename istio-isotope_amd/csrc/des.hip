@@ -3,22 +3,29 @@
 //
 //   arrivals   A[t] = sum of exponential inter-arrival times (Philox draw,
 //              integer inverse CDF) — a block scan + a scan of block sums
-//   down pass  per level, one workgroup per position v: the replica queue of
-//              v's service is FIFO over its arrivals a(v,t) = S(parent,t) +
-//              off(v), which are in trace order, so the start
-//              times are one max-plus scan over t:  fin_t = max(fin_{t-1},
-//              a_t) + hold,  S_t = fin_t - hold  (per replica for leaves with
-//              numReplicas > 1).  W[v][t] = S.
-//   up pass    per level from the deepest, (position, trace-range) blocks:
-//              finish F = max(S + floor, max_c F(c)) + post, status (own
-//              Philox error draw; mode B ORs the children's), duration
-//              F - a(v,t) into the per-service histogram.  W[v][t] = F | st<<63.
-//   finalize   latency F(entry) - A[t], records and the stats header.
+//   down pass  per queue round: the replica queue of a position's service is
+//              FIFO over its arrivals a(v,t) = S(parent,t) + off(v), which are
+//              in trace order, so the start times are one
+//              max-plus scan over t:  fin_t = max(fin_{t-1}, a_t) + hold,
+//              S_t = fin_t - hold (per replica for replicated services).
+//              Wide groups: one workgroup per position; narrow groups: chunks
+//              of a position chained by a decoupled look-back.  Leaves finish
+//              here (F = S + script time, status, duration).
+//   up pass    finish groups from the deepest, (position, trace-range)
+//              blocks: F = max(S + floor, max_c F(c)) + post, status (own
+//              Philox draw; mode B ORs the children's), duration F - a(v,t)
+//              into the per-service histogram.
+//   finalize   latency F(entry), records and the stats header.
 //
-// HBM layout: W is [position][trace] u64 so every pass reads and writes
-// whole cache lines of consecutive traces; A (u64) and E (u32, per-trace 500
-// count) are [trace].  All bytes per (position, trace): down 8 R + 8 W, up
-// 8 R (S) + 8 R (parent S) + 8 R per child + 8 W.
+// Rows W[position][trace] (and the step-begin rows BK) hold times RELATIVE to
+// the trace's arrival A_t: every value of trace t lies in [0, latency_t].
+// Narrow rows are u32 (status in bit 31), so a batch whose latencies stay
+// below 2^31 ns (2.1 s) moves 4 B per value; a value that does not fit sets
+// the overflow flag, the batch's statistics (staged in the workspace) are
+// then dropped and ISIM_ST_DES_RETRY counts it, to be rerun with u64 rows
+// (ISIM_DES_FLAG_WIDE; isim_serve_des does that itself).  Bytes per
+// (position, trace), narrow: queue pass 4 R + 4 W (+ A_t from L2), up pass
+// 4 R (S) + 4 R (arrival row) + 4 R per child + 4 W.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,26 +36,18 @@
 #include "kernel_abi.h"
 
 namespace isim {
+void *stream_calls_kernel();
 namespace dev {
 
-constexpr uint32_t kDesPer = 8;                   // traces per thread in the down pass / arrivals
+constexpr uint32_t kDesPer = 8;                   // traces per thread in the arrivals
 constexpr uint32_t kDesThreads = 1024;
 constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per arrivals chunk
-#ifndef ISIM_DES_DOWN_PER
-#define ISIM_DES_DOWN_PER 4
-#endif
-constexpr uint32_t kDownPer = ISIM_DES_DOWN_PER;        // traces per thread in the down passes
-constexpr uint32_t kDownChunk = kDownPer * kDesThreads;
-#ifndef ISIM_DES_CHAIN_THREADS
-#define ISIM_DES_CHAIN_THREADS 1024
-#endif
-constexpr uint32_t kChainThreads = ISIM_DES_CHAIN_THREADS;  // chained down pass: workgroup size
-constexpr uint32_t kChainChunk = kDownPer * kChainThreads;  // traces per chunk
+constexpr uint32_t kPer = 4;                           // consecutive traces per thread in the row passes
+constexpr uint32_t kDownChunk = kPer * kDesThreads;    // traces per down-pass chunk
 #ifndef ISIM_DES_CHAIN_BELOW
 #define ISIM_DES_CHAIN_BELOW 512  // positions per launch below which the chained scan is used
 #endif
 constexpr uint32_t kDesUpThreads = 256;
-constexpr uint64_t kMask63 = (1ull << 63) - 1;
 
 __constant__ int32_t c_ln[257] = {
 #include "des_ln_table.inc"
@@ -109,6 +108,8 @@ __device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
   return base + (((n + d - 1) * M) >> 16);
 }
 
+struct ChainState;
+
 struct DesK {
   const DesPos *pos;
   const DesPosExt *ext;
@@ -116,16 +117,17 @@ struct DesK {
   const uint32_t *child;
   const uint32_t *level_pos;  // the positions of the launch (fast queue or finish group)
   const uint32_t *arr_ops;    // BK rows of the launch (step begins)
-  uint64_t *BK;               // [steps][ld]
-  uint64_t *W;  // [n_pos][N]
-  uint64_t *A;  // [N]
-  uint32_t *E;  // [N]
+  void *BK;                   // [steps][ld] row type T
+  void *W;                    // [n_pos][ld] row type T
+  uint64_t *A;                // [N] absolute arrival times
+  uint32_t *E;                // [N] per-trace 500 count
   uint64_t *blk;
-  uint64_t *stats;
-  uint64_t *table;  // [rows][ISIM_DES_ROW_WORDS]
+  uint64_t *stats;            // narrow rows: the staging copy (des_commit)
+  uint64_t *table;            // [rows][ISIM_DES_ROW_WORDS] (staged likewise)
   isim_trace_rec *records;
+  uint32_t *ovf;              // narrow rows: a value reached 2^31
   uint64_t N, trace_begin, mean_ns;
-  uint64_t ld;  // row stride of W in traces: N rounded up to 8 (64-B aligned rows)
+  uint64_t ld;                // row stride in traces: N rounded up to 16 (64-B aligned rows)
   uint32_t k0, k1;
   uint32_t n_pos, n_slots;
   uint32_t level_begin, splits;
@@ -138,18 +140,97 @@ struct DesK {
   uint64_t *keys;
   uint32_t *vals;
   // chained down pass
-  struct ChainState *chain;
-  uint32_t *chain_ticket;  // this launch's ticket counter
+  ChainState *chain;
+  uint32_t *chain_ticket;     // this launch's ticket counter
   uint32_t n_chunks;
 };
 
-// arrival of position v (pp = pos[v]) for trace t
-__device__ __forceinline__ uint64_t des_arrival(const DesK &k, uint32_t v, const DesPos &pp, uint64_t t) {
-  if (pp.parent == kDesNoParent) return k.A[t];
-  const uint32_t b = k.ext[v].bk_in;
-  return (b == kDesNone ? k.W[(uint64_t)pp.parent * k.ld + t] : k.BK[(uint64_t)b * k.ld + t]) + pp.off;
+// ---- rows: u32 (narrow) or u64, times relative to A_t, status in the top bit
+template <typename T>
+struct Row {
+  static constexpr uint32_t kTop = 8 * sizeof(T) - 1;
+  static constexpr uint64_t kSt = 1ull << kTop;
+  static constexpr uint64_t kMask = kSt - 1;
+  // narrow rows hold values below 2^31 (the status bit stays free)
+  __device__ static bool fits(uint64_t v) { return sizeof(T) == 8 || v < kSt; }
+};
+
+template <typename T>
+__device__ __forceinline__ T *row(void *base, uint64_t ld, uint32_t r) {
+  return reinterpret_cast<T *>(base) + (uint64_t)r * ld;
 }
 
+// four consecutive values at a 16-B aligned index
+template <typename T>
+__device__ __forceinline__ void load4(const T *p, uint64_t (&x)[kPer]) {
+  if constexpr (sizeof(T) == 4) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    x[0] = v.x;
+    x[1] = v.y;
+    x[2] = v.z;
+    x[3] = v.w;
+  } else {
+    const ulonglong2 a = reinterpret_cast<const ulonglong2 *>(p)[0];
+    const ulonglong2 b = reinterpret_cast<const ulonglong2 *>(p)[1];
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = b.x;
+    x[3] = b.y;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4(T *p, const uint64_t (&x)[kPer]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<uint4 *>(p) = make_uint4((uint32_t)x[0], (uint32_t)x[1], (uint32_t)x[2], (uint32_t)x[3]);
+  } else {
+    reinterpret_cast<ulonglong2 *>(p)[0] = make_ulonglong2(x[0], x[1]);
+    reinterpret_cast<ulonglong2 *>(p)[1] = make_ulonglong2(x[2], x[3]);
+  }
+}
+// values [base, base+4) of a row, zero past n (vector load when whole)
+template <typename T>
+__device__ __forceinline__ void load4n(const T *p, uint64_t base, uint64_t n, uint64_t (&x)[kPer]) {
+  if (base + kPer <= n) {
+    load4<T>(p + base, x);
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) x[i] = base + i < n ? (uint64_t)p[base + i] : 0;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4n(T *p, uint64_t base, uint64_t n, const uint64_t (&x)[kPer]) {
+  if (base + kPer <= n) {
+    store4<T>(p + base, x);
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i)
+      if (base + i < n) p[base + i] = (T)x[i];
+  }
+}
+__device__ __forceinline__ void load4a(const uint64_t *p, uint64_t base, uint64_t n, uint64_t (&x)[kPer]) {
+  load4n<uint64_t>(p, base, n, x);
+}
+
+__device__ __forceinline__ void flag_overflow(const DesK &k, bool bad) {
+  if (bad) atomicOr(k.ovf, 1u);
+}
+
+// relative arrival of position v (pp = pos[v]) for trace t
+template <typename T>
+__device__ __forceinline__ uint64_t des_arrival(const DesK &k, uint32_t v, const DesPos &pp, uint64_t t) {
+  if (pp.parent == kDesNoParent) return 0;
+  const uint32_t b = k.ext[v].bk_in;
+  const T *r = b == kDesNone ? row<T>(k.W, k.ld, pp.parent) : row<T>(k.BK, k.ld, b);
+  return (uint64_t)r[t] + pp.off;
+}
+
+// the row a position's arrivals are read from (null: the entry, arrival 0)
+template <typename T>
+__device__ __forceinline__ const T *arrival_row(const DesK &k, uint32_t v, const DesPos &pp) {
+  if (pp.parent == kDesNoParent) return nullptr;
+  const uint32_t b = k.ext[v].bk_in;
+  return b == kDesNone ? row<T>(k.W, k.ld, pp.parent) : row<T>(k.BK, k.ld, b);
+}
 
 // (B, C) represents x -> max(x + B, C); `then` composes a after b.
 struct MaxPlus {
@@ -277,26 +358,13 @@ __device__ __forceinline__ void hist_add_wave(uint32_t *hist, uint32_t bin) {
   }
 }
 
-// A fused leaf (kDesFlagFused) finishes in its queue pass: F = S + script
-// time, its own error status (drawn with the loads), the duration F - a into
-// the LDS histogram.
+// A leaf finished in its queue pass (kDesFlagFused): F = S + script time, its
+// own error status (drawn with the loads), the duration F - a into the LDS
+// histogram.
 __device__ __forceinline__ uint32_t des_own_status(const DesK &k, uint32_t v, const DesPos &P, uint64_t t) {
   if (P.flags & kDesFlagAlways) return 1u;
   if (!P.thr) return 0u;
   return des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr ? 1u : 0u;
-}
-
-__device__ __forceinline__ uint64_t des_leaf_finish(const DesK &k, const DesPos &P, uint64_t t, uint64_t S,
-                                                    uint64_t a, uint32_t st, uint32_t &bin, uint64_t &d0,
-                                                    uint64_t &d1, uint64_t &n5) {
-  const uint64_t F = S + P.floor;
-  const uint64_t dur = F - a;
-  if (st) atomicAdd(k.E + t, 1u);
-  n5 += st;
-  d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
-  d0 += st ? 0 : dur;
-  bin = st * ISIM_N_PROM + des_prom_bucket(dur);
-  return F | ((uint64_t)st << 63);
 }
 
 // per-service duration statistics of a workgroup: LDS histogram + sums -> the
@@ -317,9 +385,9 @@ __device__ __forceinline__ void des_flush_durations(const DesK &k, const DesPos 
     red[2 * W + (threadIdx.x >> 6)] = n5;
   }
   __syncthreads();
-  unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
+  unsigned long long *trow = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += NT)
-    if (hist[i]) atomicAdd(row + i, (unsigned long long)hist[i]);
+    if (hist[i]) atomicAdd(trow + i, (unsigned long long)hist[i]);
   if (threadIdx.x == 0) {
     uint64_t s0 = 0, s1 = 0, e = 0;
 #pragma unroll 2
@@ -328,113 +396,17 @@ __device__ __forceinline__ void des_flush_durations(const DesK &k, const DesPos 
       s1 += red[W + i];
       e += red[2 * W + i];
     }
-    if (s0) atomicAdd(row + 2 * ISIM_N_PROM, (unsigned long long)s0);
-    if (s1) atomicAdd(row + 2 * ISIM_N_PROM + 1, (unsigned long long)s1);
+    if (s0) atomicAdd(trow + 2 * ISIM_N_PROM, (unsigned long long)s0);
+    if (s1) atomicAdd(trow + 2 * ISIM_N_PROM + 1, (unsigned long long)s1);
     if (e && P.slot != kSlotRoot)
       atomicAdd((unsigned long long *)(k.stats + ISIM_ST_SITES + k.n_slots + P.slot), (unsigned long long)e);
   }
 }
 
-// ---- down pass: FIFO start times, one workgroup per position of the level
-// MULTI: the service has replicas (routing draw per trace); FUSED: leaves
-// finished here (kDesFlagFused)
-template <bool MULTI, bool FUSED>
-__global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
-  __shared__ MaxPlus wtot[kDesThreads / 64];
-  __shared__ uint64_t carry[kDesMaxReplicas];
-  __shared__ uint64_t red[2 * kDesThreads / 64];
-  __shared__ MaxPlus xs[kDesThreads];
-  __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint64_t red3[3 * kDesThreads / 64];
-  const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
-  const DesPos P = k.pos[v];
-  const uint32_t reps = MULTI ? P.reps : 1u;
-  if (threadIdx.x < reps) carry[threadIdx.x] = 0;
-  if constexpr (FUSED)
-    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
-  __syncthreads();
-  uint64_t d0 = 0, d1 = 0, n5 = 0;
-  const uint64_t N = k.N;
-  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
-  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
-  uint64_t *out = k.W + (uint64_t)v * k.ld;
-  uint64_t wsum = 0, wmax = 0;
-  for (uint64_t c0 = 0; c0 < N; c0 += kDownChunk) {
-    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDownPer;
-    uint64_t a[kDownPer];
-    uint32_t rr[kDownPer];
-    if (base + kDownPer <= N) {
-      // 8 consecutive traces = 64 B per thread: four 16-B loads (rows are 64-B aligned)
-      const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(par + base);
-#pragma unroll
-      for (uint32_t i = 0; i < kDownPer / 2; ++i) {
-        const ulonglong2 x = q[i];
-        a[2 * i] = x.x + off;
-        a[2 * i + 1] = x.y + off;
-      }
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
-    }
-    uint32_t stm = 0;  // fused leaves: own error statuses, bit i
-#pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i) {
-      if constexpr (MULTI)
-        rr[i] = base + i < N ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
-      else
-        rr[i] = 0u;
-      if constexpr (FUSED) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
-    }
-    for (uint32_t r = 0; r < reps; ++r) {
-      MaxPlus f{0, 0};
-#pragma unroll
-      for (uint32_t i = 0; i < kDownPer; ++i)
-        if (base + i < N && rr[i] == r) f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
-      const MaxPlus inc = mp_block_scan(f, wtot);
-      // exclusive prefix = the previous thread's inclusive one
-      xs[threadIdx.x] = inc;
-      __syncthreads();
-      const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
-      const uint64_t cin = carry[r];
-      uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-      uint64_t Sv[kDownPer];
-#pragma unroll
-      for (uint32_t i = 0; i < kDownPer; ++i) {
-        const uint64_t t = base + i;
-        Sv[i] = 0;
-        if (t < N && rr[i] == r) {
-          const uint64_t S = x > a[i] ? x : a[i];
-          Sv[i] = S;
-          const uint64_t w = S - a[i];
-          wsum += w;
-          wmax = w > wmax ? w : wmax;
-          x = S + P.hold;
-        }
-      }
-      if constexpr (FUSED) {
-#pragma unroll
-        for (uint32_t i = 0; i < kDownPer; ++i) {
-          uint32_t bin = kNoBin;
-          if (base + i < N && rr[i] == r)
-            Sv[i] = des_leaf_finish(k, P, base + i, Sv[i], a[i], (stm >> i) & 1u, bin, d0, d1, n5);
-          hist_add_wave(hist, bin);
-        }
-      }
-      if (reps == 1 && base + kDownPer <= N) {
-        ulonglong2 *q = reinterpret_cast<ulonglong2 *>(out + base);
-#pragma unroll
-        for (uint32_t i = 0; i < kDownPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
-      } else {
-#pragma unroll
-        for (uint32_t i = 0; i < kDownPer; ++i)
-          if (base + i < N && rr[i] == r) out[base + i] = Sv[i];
-      }
-      __syncthreads();
-      if (threadIdx.x == kDesThreads - 1) carry[r] = x;
-      __syncthreads();
-    }
-  }
-  // per-position queue statistics (the service's row: one position per service)
+// queue statistics of a workgroup -> the service's table row
+template <uint32_t NT>
+__device__ __forceinline__ void des_flush_waits(const DesK &k, uint32_t trow_idx, uint64_t wsum, uint64_t wmax,
+                                                uint64_t count, uint64_t hold_sum, uint64_t *red) {
 #pragma unroll
   for (uint32_t d = 32; d > 0; d >>= 1) {
     wsum += __shfl_xor(wsum, d, 64);
@@ -443,30 +415,157 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   }
   if ((threadIdx.x & 63u) == 0) {
     red[threadIdx.x >> 6] = wsum;
-    red[kDesThreads / 64 + (threadIdx.x >> 6)] = wmax;
+    red[NT / 64 + (threadIdx.x >> 6)] = wmax;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t s = 0, m = 0;
 #pragma unroll 2
-    for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
+    for (uint32_t i = 0; i < NT / 64; ++i) {
       s += red[i];
-      m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
+      m = red[NT / 64 + i] > m ? red[NT / 64 + i] : m;
     }
-    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
-    atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)N);
-    atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
-    atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
-    atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(N * P.hold));
+    unsigned long long *trow = (unsigned long long *)(k.table + (uint64_t)trow_idx * ISIM_DES_ROW_WORDS);
+    if (count) atomicAdd(trow + ISIM_DES_COUNT, (unsigned long long)count);
+    if (hold_sum) atomicAdd(trow + ISIM_DES_SUM_HOLD, (unsigned long long)hold_sum);
+    if (s) atomicAdd(trow + ISIM_DES_SUM_WAIT, (unsigned long long)s);
+    if (m) atomicMax(trow + ISIM_DES_MAX_WAIT, (unsigned long long)m);
   }
-  if constexpr (FUSED) des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red3);
 }
 
-// ---- down pass, single-replica services: one workgroup per (position,
-// chunk of kDownChunk traces), chunks of a position chained by a decoupled
-// look-back over their max-plus maps, so a position's queue is scanned by
-// many workgroups at once.  Workgroups take tickets in launch order
-// (position-major, chunk-minor), so every chunk they wait on has started.
+// The queue of one chunk of 4 traces per thread, once the carry into the
+// thread is known: S = max(x, a) per trace (absolute), the stored value
+// (S or, fused, F | status, relative to A_t), waits and durations.
+template <typename T, bool FUSED>
+__device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uint64_t base, uint64_t N,
+                                             uint64_t x, const uint64_t (&a)[kPer], const uint64_t (&At)[kPer],
+                                             uint32_t mask, uint32_t stm, uint64_t (&out)[kPer], uint32_t *hist,
+                                             uint64_t &wsum, uint64_t &wmax, uint64_t &d0, uint64_t &d1,
+                                             uint64_t &n5, bool &bad) {
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    uint32_t bin = kNoBin;
+    if (base + i < N && ((mask >> i) & 1u)) {
+      const uint64_t S = x > a[i] ? x : a[i];
+      const uint64_t w = S - a[i];
+      wsum += w;
+      wmax = w > wmax ? w : wmax;
+      x = S + P.hold;
+      uint64_t val = S - At[i];
+      if constexpr (FUSED) {
+        const uint64_t F = val + P.floor;
+        const uint32_t st = (stm >> i) & 1u;
+        const uint64_t dur = w + P.floor;  // F - a
+        if (st) atomicAdd(k.E + base + i, 1u);
+        n5 += st;
+        d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
+        d0 += st ? 0 : dur;
+        bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+        bad |= !Row<T>::fits(F);
+        val = F | ((uint64_t)st << Row<T>::kTop);
+      } else {
+        bad |= !Row<T>::fits(val);
+      }
+      out[i] = val;
+    }
+    if constexpr (FUSED) hist_add_wave(hist, bin);
+  }
+}
+
+// this thread's 4 traces: relative arrivals + A_t -> absolute arrivals a, A_t
+template <typename T>
+__device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint64_t off, uint64_t base,
+                                              uint64_t N, uint64_t (&a)[kPer], uint64_t (&At)[kPer]) {
+  load4a(k.A, base, N, At);
+  if (par) {
+    uint64_t r[kPer];
+    load4n<T>(par, base, N, r);
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) a[i] = At[i] + r[i] + off;
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) a[i] = At[i];
+  }
+}
+
+// ---- queue pass, one workgroup per position (wide groups; replicated
+// services: per-replica scans, the routing draw per trace)
+template <typename T, bool MULTI, bool FUSED>
+__global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
+  __shared__ MaxPlus wtot[kDesThreads / 64];
+  __shared__ uint64_t carry[kDesMaxReplicas];
+  __shared__ uint64_t red[3 * kDesThreads / 64];
+  __shared__ MaxPlus xs[kDesThreads];
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
+  const DesPos P = k.pos[v];
+  const uint32_t reps = MULTI ? P.reps : 1u;
+  if (threadIdx.x < reps) carry[threadIdx.x] = 0;
+  if constexpr (FUSED)
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
+  __syncthreads();
+  const uint64_t N = k.N;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
+  T *out = row<T>(k.W, k.ld, v);
+  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
+  bool bad = false;
+  for (uint64_t c0 = 0; c0 < N; c0 += kDownChunk) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+    uint64_t a[kPer], At[kPer], o[kPer] = {0, 0, 0, 0};
+    load_arrivals<T>(k, par, off, base, N, a, At);
+    uint32_t rr[kPer];
+    uint32_t stm = 0;  // fused leaves: own error statuses, bit i
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      if constexpr (MULTI)
+        rr[i] = base + i < N ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
+      else
+        rr[i] = 0u;
+      if constexpr (FUSED) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
+    }
+    for (uint32_t r = 0; r < reps; ++r) {
+      MaxPlus f{0, 0};
+      uint32_t mask = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i)
+        if (base + i < N && rr[i] == r) {
+          f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
+          mask |= 1u << i;
+        }
+      const MaxPlus inc = mp_block_scan(f, wtot);
+      // exclusive prefix = the previous thread's inclusive one
+      xs[threadIdx.x] = inc;
+      __syncthreads();
+      const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
+      const uint64_t cin = carry[r];
+      const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+      queue_finish<T, FUSED>(k, P, base, N, x, a, At, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+      __syncthreads();  // every thread has read carry[r]
+      if (threadIdx.x == kDesThreads - 1) {
+        uint64_t xe = x;
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i)
+          if ((mask >> i) & 1u) xe = (xe > a[i] ? xe : a[i]) + P.hold;
+        carry[r] = xe;
+      }
+      __syncthreads();
+    }
+    store4n<T>(out, base, N, o);
+  }
+  flag_overflow(k, bad);
+  des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
+  if constexpr (FUSED) {
+    __syncthreads();
+    des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red);
+  }
+}
+
+// ---- queue pass, single-replica services of narrow groups: one workgroup
+// per (position, chunk of kDownChunk traces), chunks of a position chained by
+// a decoupled look-back over their max-plus maps.  Workgroups take tickets in
+// launch order (position-major, chunk-minor), so every chunk they wait on
+// has started.
 struct ChainState {
   uint64_t B, C;   // the chunk's max-plus map (flag >= 1)
   uint64_t P;      // the queue's carry after the chunk (flag 2)
@@ -487,52 +586,44 @@ __device__ __forceinline__ void st_flag(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool FUSED>
-__global__ void __launch_bounds__(kChainThreads, 8) des_down_chain(DesK k) {
-  __shared__ MaxPlus wtot[kChainThreads / 64];
-  __shared__ MaxPlus xs[kChainThreads];
-  __shared__ uint64_t red[2 * kChainThreads / 64];
+template <typename T, bool FUSED>
+__global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
+  __shared__ MaxPlus wtot[kDesThreads / 64];
+  __shared__ MaxPlus xs[kDesThreads];
+  __shared__ uint64_t red[3 * kDesThreads / 64];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint64_t red3[3 * kChainThreads / 64];
   __shared__ uint32_t s_ticket;
   __shared__ uint64_t s_carry;
   if (threadIdx.x == 0) s_ticket = atomicAdd(k.chain_ticket, 1u);
   if constexpr (FUSED)
-    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kChainThreads) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
   __syncthreads();
   const uint32_t ticket = s_ticket;
   const uint32_t chunk = ticket % k.n_chunks;
   const uint32_t v = k.level_pos[k.level_begin + ticket / k.n_chunks];
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
-  const uint64_t *par = P.parent == kDesNoParent ? k.A : k.W + (uint64_t)P.parent * k.ld;
-  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
-  uint64_t *out = k.W + (uint64_t)v * k.ld;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
+  T *out = row<T>(k.W, k.ld, v);
   ChainState *cs = k.chain + (uint64_t)v * k.n_chunks;
-  const uint64_t base = (uint64_t)chunk * kChainChunk + (uint64_t)threadIdx.x * kDownPer;
-  uint64_t a[kDownPer];
-  if (base + kDownPer <= N) {
-    const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(par + base);
-#pragma unroll
-    for (uint32_t i = 0; i < kDownPer / 2; ++i) {
-      const ulonglong2 x = q[i];
-      a[2 * i] = x.x + off;
-      a[2 * i + 1] = x.y + off;
-    }
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i) a[i] = base + i < N ? par[base + i] + off : 0;
-  }
+  const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
+  uint64_t a[kPer], At[kPer];
+  load_arrivals<T>(k, par, off, base, N, a, At);
   uint32_t stm = 0;
   if constexpr (FUSED) {
 #pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
+    for (uint32_t i = 0; i < kPer; ++i) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
   }
   MaxPlus f{0, 0};
+  uint32_t mask = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < kDownPer; ++i)
-    if (base + i < N) f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
-  const MaxPlus inc = mp_block_scan<kChainThreads>(f, wtot);
+  for (uint32_t i = 0; i < kPer; ++i)
+    if (base + i < N) {
+      f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
+      mask |= 1u << i;
+    }
+  const MaxPlus inc = mp_block_scan(f, wtot);
   xs[threadIdx.x] = inc;
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -541,7 +632,7 @@ __global__ void __launch_bounds__(kChainThreads, 8) des_down_chain(DesK k) {
     // included) use sc1 stores drained before the flag store and sc1 loads
     // (no L2 writeback / invalidate).
     const uint32_t lane = threadIdx.x;
-    const MaxPlus agg = xs[kChainThreads - 1];
+    const MaxPlus agg = xs[kDesThreads - 1];
     if (chunk > 0 && lane == 0) {
       st_relaxed(&cs[chunk].B, agg.B);
       st_relaxed(&cs[chunk].C, agg.C);
@@ -594,62 +685,23 @@ __global__ void __launch_bounds__(kChainThreads, 8) des_down_chain(DesK k) {
   __syncthreads();
   const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
   const uint64_t cin = s_carry;
-  uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-  uint64_t Sv[kDownPer];
+  const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+  uint64_t o[kPer] = {0, 0, 0, 0};
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kDownPer; ++i) {
-    Sv[i] = 0;
-    uint32_t bin = kNoBin;
-    if (base + i < N) {
-      const uint64_t S = x > a[i] ? x : a[i];
-      const uint64_t w = S - a[i];
-      wsum += w;
-      wmax = w > wmax ? w : wmax;
-      x = S + P.hold;
-      Sv[i] = FUSED ? des_leaf_finish(k, P, base + i, S, a[i], (stm >> i) & 1u, bin, d0, d1, n5) : S;
-    }
-    if constexpr (FUSED) hist_add_wave(hist, bin);
+  bool bad = false;
+  queue_finish<T, FUSED>(k, P, base, N, x, a, At, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+  store4n<T>(out, base, N, o);
+  flag_overflow(k, bad);
+  des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
+  if constexpr (FUSED) {
+    __syncthreads();
+    des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red);
   }
-  if (base + kDownPer <= N) {
-    ulonglong2 *q = reinterpret_cast<ulonglong2 *>(out + base);
-#pragma unroll
-    for (uint32_t i = 0; i < kDownPer / 2; ++i) q[i] = make_ulonglong2(Sv[2 * i], Sv[2 * i + 1]);
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i)
-      if (base + i < N) out[base + i] = Sv[i];
-  }
-#pragma unroll
-  for (uint32_t d = 32; d > 0; d >>= 1) {
-    wsum += __shfl_xor(wsum, d, 64);
-    const uint64_t o = __shfl_xor(wmax, d, 64);
-    wmax = o > wmax ? o : wmax;
-  }
-  if ((threadIdx.x & 63u) == 0) {
-    red[threadIdx.x >> 6] = wsum;
-    red[kChainThreads / 64 + (threadIdx.x >> 6)] = wmax;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t s = 0, m = 0;
-#pragma unroll 2
-    for (uint32_t i = 0; i < kChainThreads / 64; ++i) {
-      s += red[i];
-      m = red[kChainThreads / 64 + i] > m ? red[kChainThreads / 64 + i] : m;
-    }
-    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS);
-    if (chunk == 0) {
-      atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)N);
-      atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(N * P.hold));
-    }
-    if (s) atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
-    if (m) atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
-  }
-  if constexpr (FUSED) des_flush_durations<kChainThreads>(k, P, hist, d0, d1, n5, red3);
 }
 
-// ---- up pass: finish times, statuses, per-service durations
+// ---- up pass: finish times, statuses, per-service durations.
+// (position, trace-range) blocks; 4 consecutive traces per thread.
+template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
@@ -658,78 +710,82 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.y];
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
-  const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
-  uint64_t *mine = k.W + (uint64_t)v * k.ld;
+  // trace range: split boundaries on multiples of 16 (aligned vector accesses)
+  const uint64_t tb = blockIdx.x ? (N * blockIdx.x / k.splits) & ~15ull : 0;
+  const uint64_t te = blockIdx.x + 1 == k.splits ? N : (N * (blockIdx.x + 1) / k.splits) & ~15ull;
+  T *mine = row<T>(k.W, k.ld, v);
   const DesPosExt X = k.ext[v];
-  // arrival: start(parent) + off, or a step begin + H (calls after calls), or A_t (the entry)
-  const uint64_t *par = P.parent == kDesNoParent ? k.A
-                        : X.bk_in == kDesNone    ? k.W + (uint64_t)P.parent * k.ld
-                                                 : k.BK + (uint64_t)X.bk_in * k.ld;
-  const uint64_t off = P.parent == kDesNoParent ? 0 : P.off;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
   const bool leaf = P.flags & kDesFlagLeaf;
   // several call steps: F = max(BK_last + floor, max F(last step's callees)) + post
-  const uint64_t *base_t = X.bk_last == kDesNone ? mine : k.BK + (uint64_t)X.bk_last * k.ld;
+  const T *base_t = X.bk_last == kDesNone ? nullptr : row<T>(k.BK, k.ld, X.bk_last);
   const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
-  constexpr uint32_t U = 4;  // independent traces per thread per iteration (memory-level parallelism)
-  for (uint64_t t0 = tb + threadIdx.x; t0 < te; t0 += U * kDesUpThreads) {
-    uint64_t S[U], a[U], m[U];
-    uint32_t sto[U];
+  bool bad = false;
+  for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
+    uint64_t S[kPer], a[kPer], m[kPer];
+    uint32_t sto = 0;  // children's 500s, bit i
+    load4n<T>(mine, b0, te, S);
+    if (par) {
+      load4n<T>(par, b0, te, a);
 #pragma unroll
-    for (uint32_t j = 0; j < U; ++j) {
-      const uint64_t t = t0 + j * kDesUpThreads;
-      const bool ok = t < te;
-      S[j] = ok ? mine[t] : 0;
-      a[j] = ok ? par[t] + off : 0;
-      sto[j] = 0;
+      for (uint32_t i = 0; i < kPer; ++i) a[i] += off;
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) a[i] = 0;
+    }
+    if (base_t) load4n<T>(base_t, b0, te, m);
+    else {
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) m[i] = S[i];
     }
 #pragma unroll
-    for (uint32_t j = 0; j < U; ++j) {
-      const uint64_t t = t0 + j * kDesUpThreads;
-      m[j] = (X.bk_last == kDesNone ? S[j] : (t < te ? base_t[t] : 0)) + P.floor;
-    }
+    for (uint32_t i = 0; i < kPer; ++i) m[i] += P.floor;
     if (!leaf) {
       for (uint32_t c = 0; c < P.child_cnt; ++c) {
-        const uint64_t *fc = k.W + (uint64_t)k.child[P.child_off + c] * k.ld;
+        uint64_t f[kPer];
+        load4n<T>(row<T>(k.W, k.ld, k.child[P.child_off + c]), b0, te, f);
         const bool in_max = c >= c_max_from;
 #pragma unroll
-        for (uint32_t j = 0; j < U; ++j) {
-          const uint64_t t = t0 + j * kDesUpThreads;
-          const uint64_t f = t < te ? fc[t] : 0;
-          const uint64_t tc = f & kMask63;
-          if (in_max) m[j] = tc > m[j] ? tc : m[j];
-          sto[j] |= (uint32_t)(f >> 63);
+        for (uint32_t i = 0; i < kPer; ++i) {
+          const uint64_t tc = f[i] & Row<T>::kMask;
+          if (in_max) m[i] = tc > m[i] ? tc : m[i];
+          sto |= (uint32_t)(f[i] >> Row<T>::kTop) << i;
         }
       }
     }
+    uint64_t o[kPer];
 #pragma unroll
-    for (uint32_t j = 0; j < U; ++j) {
-      const uint64_t t = t0 + j * kDesUpThreads;
+    for (uint32_t i = 0; i < kPer; ++i) {
+      const uint64_t t = b0 + i;
       uint32_t bin = kNoBin;
+      o[i] = 0;
       if (t < te) {
-      const uint64_t F = leaf ? m[j] : m[j] + P.post;
-      uint32_t own = 0;
-      if (P.flags & kDesFlagAlways) own = 1;
-      else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
-      const uint32_t st = k.modeb ? (own | sto[j]) : own;
-      const uint64_t dur = F - a[j];
-      mine[t] = F | ((uint64_t)st << 63);
-      if (st) {
-        atomicAdd(k.E + t, 1u);
-        n500 += 1;
-        dsum1 += dur;
-      } else {
-        dsum0 += dur;
-      }
-      bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+        const uint64_t F = leaf ? m[i] : m[i] + P.post;
+        uint32_t own = 0;
+        if (P.flags & kDesFlagAlways) own = 1;
+        else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
+        const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
+        const uint64_t dur = F - a[i];
+        bad |= !Row<T>::fits(F);
+        o[i] = F | ((uint64_t)st << Row<T>::kTop);
+        if (st) atomicAdd(k.E + t, 1u);
+        n500 += st;
+        dsum1 += st ? dur : 0;
+        dsum0 += st ? 0 : dur;
+        bin = st * ISIM_N_PROM + des_prom_bucket(dur);
       }
       hist_add_wave(hist, bin);
     }
+    store4n<T>(mine, b0, te, o);
   }
+  flag_overflow(k, bad);
   des_flush_durations<kDesUpThreads>(k, P, hist, dsum0, dsum1, n500, red);
 }
 
 // ---- finalize: records and the latency statistics
+template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
   __shared__ uint64_t red[5 * kDesUpThreads / 64];
@@ -737,14 +793,17 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads) hl[i] = 0;
   __syncthreads();
   const uint64_t N = k.N;
+  // an overflowed narrow batch is dropped (des_commit): records untouched
+  const bool keep = sizeof(T) == 8 || *k.ovf == 0;
+  const T *F0 = row<T>(k.W, k.ld, 0);  // position 0: the entry
   uint64_t sl = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * kDesUpThreads + threadIdx.x; t < N;
        t += (uint64_t)gridDim.x * kDesUpThreads) {
-    const uint64_t F = k.W[t];  // position 0 (the entry)
-    const uint32_t st = (uint32_t)(F >> 63);
-    const uint64_t L = (F & kMask63) - k.A[t];
+    const uint64_t F = F0[t];
+    const uint32_t st = (uint32_t)(F >> Row<T>::kTop);
+    const uint64_t L = F & Row<T>::kMask;  // relative to the trace's arrival: the latency
     const uint32_t e = k.E[t];
-    if (k.records) {
+    if (k.records && keep) {
       isim_trace_rec r;
       r.latency_ns = L;
       r.hops = k.n_pos;
@@ -804,8 +863,9 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
 }
 
 // ---- sort path: arrivals of all positions of one service,
-// item i = t * P + j (j = the position's rank in hop order), so a stable sort
-// by arrival time leaves ties in (t, hop) order
+// item i = t * P + j (j = the position's rank in hop order), keyed by the
+// absolute arrival, so a stable sort leaves ties in (t, hop) order
+template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
   const uint32_t P = k.svc.pos_cnt;
   const uint64_t M = k.N * P;
@@ -813,12 +873,13 @@ __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
        i += (uint64_t)gridDim.x * kDesUpThreads) {
     const uint64_t t = i / P;
     const uint32_t v = k.sort_pos[k.svc.pos_off + (uint32_t)(i - t * P)];
-    k.keys[i] = des_arrival(k, v, k.pos[v], t);
+    k.keys[i] = k.A[t] + des_arrival<T>(k, v, k.pos[v], t);
     k.vals[i] = (uint32_t)i;
   }
 }
 
 // FIFO scan of one sort-path service over its sorted arrivals (one workgroup)
+template <typename T>
 __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
   __shared__ MaxPlus wtot[kDesThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
@@ -830,12 +891,13 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
   __syncthreads();
   uint64_t wsum = 0, wmax = 0;
+  bool bad = false;
   for (uint64_t c0 = 0; c0 < M; c0 += kDownChunk) {
-    const uint64_t base = c0 + (uint64_t)threadIdx.x * kDownPer;
-    uint64_t a[kDownPer], tt[kDownPer];
-    uint32_t vv[kDownPer], rr[kDownPer];
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+    uint64_t a[kPer], tt[kPer];
+    uint32_t vv[kPer], rr[kPer];
 #pragma unroll
-    for (uint32_t i = 0; i < kDownPer; ++i) {
+    for (uint32_t i = 0; i < kPer; ++i) {
       const uint64_t q = base + i;
       a[i] = 0;
       tt[i] = 0;
@@ -852,7 +914,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
 #pragma unroll
-      for (uint32_t i = 0; i < kDownPer; ++i)
+      for (uint32_t i = 0; i < kPer; ++i)
         if (base + i < M && rr[i] == r) f = mp_then(f, MaxPlus{sv.hold, a[i] + sv.hold});
       const MaxPlus inc = mp_block_scan(f, wtot);
       xs[threadIdx.x] = inc;
@@ -861,10 +923,12 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
       const uint64_t cin = carry[r];
       uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
 #pragma unroll
-      for (uint32_t i = 0; i < kDownPer; ++i) {
+      for (uint32_t i = 0; i < kPer; ++i) {
         if (base + i < M && rr[i] == r) {
           const uint64_t S = x > a[i] ? x : a[i];
-          k.W[(uint64_t)vv[i] * k.ld + tt[i]] = S;
+          const uint64_t rel = S - k.A[tt[i]];
+          bad |= !Row<T>::fits(rel);
+          row<T>(k.W, k.ld, vv[i])[tt[i]] = (T)rel;
           const uint64_t w = S - a[i];
           wsum += w;
           wmax = w > wmax ? w : wmax;
@@ -876,51 +940,60 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
       __syncthreads();
     }
   }
-#pragma unroll
-  for (uint32_t d = 32; d > 0; d >>= 1) {
-    wsum += __shfl_xor(wsum, d, 64);
-    const uint64_t o = __shfl_xor(wmax, d, 64);
-    wmax = o > wmax ? o : wmax;
-  }
-  if ((threadIdx.x & 63u) == 0) {
-    red[threadIdx.x >> 6] = wsum;
-    red[kDesThreads / 64 + (threadIdx.x >> 6)] = wmax;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t s = 0, m = 0;
-#pragma unroll 2
-    for (uint32_t i = 0; i < kDesThreads / 64; ++i) {
-      s += red[i];
-      m = red[kDesThreads / 64 + i] > m ? red[kDesThreads / 64 + i] : m;
-    }
-    unsigned long long *row = (unsigned long long *)(k.table + (uint64_t)sv.row * ISIM_DES_ROW_WORDS);
-    atomicAdd(row + ISIM_DES_COUNT, (unsigned long long)M);
-    atomicAdd(row + ISIM_DES_SUM_WAIT, (unsigned long long)s);
-    atomicMax(row + ISIM_DES_MAX_WAIT, (unsigned long long)m);
-    atomicAdd(row + ISIM_DES_SUM_HOLD, (unsigned long long)(M * sv.hold));
-  }
+  flag_overflow(k, bad);
+  des_flush_waits<kDesThreads>(k, sv.row, wsum, wmax, M, M * sv.hold, red);
 }
 
 // ---- step begins (calls after calls): BK rows of one round
+template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_arrive(DesK k) {
   const uint32_t b = k.arr_ops[k.level_begin + blockIdx.y];
   const DesStep st = k.steps[b];
   const uint64_t N = k.N;
   const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
-  uint64_t *out = k.BK + (uint64_t)b * k.ld;
+  T *out = row<T>(k.BK, k.ld, b);
+  bool bad = false;
   for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
     uint64_t v;
     if (st.prev == kDesNone) {
-      v = k.W[(uint64_t)st.pos * k.ld + t];  // the position's start
+      v = row<T>(k.W, k.ld, st.pos)[t];  // the position's start
     } else {
-      v = k.BK[(uint64_t)st.prev * k.ld + t] + st.smax;
+      v = (uint64_t)row<T>(k.BK, k.ld, st.prev)[t] + st.smax;
       for (uint32_t j = 0; j < st.child_cnt; ++j) {
-        const uint64_t f = k.W[(uint64_t)k.child[st.child_off + j] * k.ld + t] & kMask63;
+        const uint64_t f = row<T>(k.W, k.ld, k.child[st.child_off + j])[t] & Row<T>::kMask;
         v = f > v ? f : v;
       }
     }
-    out[t] = v + st.add;
+    v += st.add;
+    bad |= !Row<T>::fits(v);
+    out[t] = (T)v;
+  }
+  flag_overflow(k, bad);
+}
+
+// ---- narrow rows: merge the staged statistics into the caller's buffers,
+// or count the batch in ISIM_ST_DES_RETRY when a value overflowed
+__global__ void __launch_bounds__(256) des_commit(const uint64_t *__restrict__ stage, uint64_t *stats,
+                                                  uint64_t *table, uint64_t stats_words, uint64_t table_words,
+                                                  const uint32_t *ovf) {
+  if (*ovf) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long *)(stats + ISIM_ST_DES_RETRY), 1ull);
+    return;
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < stats_words + table_words;
+       i += (uint64_t)gridDim.x * 256) {
+    const uint64_t x = stage[i];
+    if (!x) continue;
+    if (i < stats_words) {
+      unsigned long long *p = (unsigned long long *)(stats + i);
+      if (i == ISIM_ST_NOT_MIN_LATENCY || i == ISIM_ST_MAX_LATENCY) atomicMax(p, (unsigned long long)x);
+      else atomicAdd(p, (unsigned long long)x);
+    } else {
+      const uint64_t j = i - stats_words;
+      unsigned long long *p = (unsigned long long *)(table + j);
+      if (j % ISIM_DES_ROW_WORDS == ISIM_DES_MAX_WAIT) atomicMax(p, (unsigned long long)x);
+      else atomicAdd(p, (unsigned long long)x);
+    }
   }
 }
 
@@ -934,69 +1007,59 @@ static size_t sort_temp_bytes(uint64_t m) {
   return bytes;
 }
 
-// Host launcher: the whole DES of one batch on `stream` (no allocation, no
-// host synchronisation).
-uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n) {
-  const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
-  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-  const uint64_t ld = (n + 7) & ~7ull;
-  const uint64_t m = (uint64_t)plan.max_sort_pos * n;
-  const uint64_t sort = m ? 2 * al(m * 8) + 2 * al(m * 4) + al(sort_temp_bytes(m)) : 0;
-  return al((uint64_t)plan.pos.size() * ld * 8) + al(n * 8) + al(n * 4) + al((nblk + 1) * 8) +
-         al((uint64_t)plan.steps.size() * ld * 8) + al(des_chain_bytes(plan, n)) + sort;
-}
-
+static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
+static uint64_t row_ld(uint64_t n) { return (n + 15) & ~15ull; }
 static uint64_t chain_tickets(const DesPlan &plan) { return 4ull * plan.rounds(); }
 
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n) {
-  const uint64_t chunks = (n + dev::kChainChunk - 1) / dev::kChainChunk;
-  return ((chain_tickets(plan) * 4 + 255) & ~255ull) + (uint64_t)plan.pos.size() * chunks * sizeof(dev::ChainState);
+  const uint64_t chunks = (n + dev::kDownChunk - 1) / dev::kDownChunk;
+  return al256(chain_tickets(plan) * 4) + (uint64_t)plan.pos.size() * chunks * sizeof(dev::ChainState);
 }
 
-int des_launch(const DesLaunch &L, void *stream_) {
+// Workspace parts, in order (256-B aligned): W and BK rows sized for u64,
+// A, E, chunk sums, chain states, overflow flag, staged stats + table, sort path.
+uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n, uint64_t stats_words, uint64_t table_rows) {
+  const uint64_t nblk = (n + dev::kDesChunk - 1) / dev::kDesChunk;
+  const uint64_t ld = row_ld(n);
+  const uint64_t m = (uint64_t)plan.max_sort_pos * n;
+  const uint64_t sort = m ? 2 * al256(m * 8) + 2 * al256(m * 4) + al256(sort_temp_bytes(m)) : 0;
+  return al256((uint64_t)plan.pos.size() * ld * 8) + al256((uint64_t)plan.steps.size() * ld * 8) + al256(n * 8) +
+         al256(n * 4) + al256((nblk + 1) * 8) + al256(des_chain_bytes(plan, n)) + 256 +
+         al256((stats_words + table_rows * ISIM_DES_ROW_WORDS) * 8) + sort;
+}
+
+void des_carve(DesLaunch &L, void *workspace) {
+  const DesPlan &plan = *L.plan;
+  const uint64_t n = L.n_traces, ld = row_ld(n);
+  char *ws = (char *)workspace;
+  auto take = [&](uint64_t bytes) {
+    char *p = ws;
+    ws += al256(bytes);
+    return p;
+  };
+  L.W = take((uint64_t)plan.pos.size() * ld * 8);
+  L.BK = take((uint64_t)plan.steps.size() * ld * 8);
+  L.A = (uint64_t *)take(n * 8);
+  L.E = (uint32_t *)take(n * 4);
+  L.blk = (uint64_t *)take(((n + dev::kDesChunk - 1) / dev::kDesChunk + 1) * 8);
+  L.chain = take(des_chain_bytes(plan, n));
+  L.ovf = (uint32_t *)take(4);
+  L.stage = (uint64_t *)take((L.stats_words + (uint64_t)L.table_rows * ISIM_DES_ROW_WORDS) * 8);
+  L.sort_ws = ws;
+}
+
+// The rounds of one batch with row type T: step begins,
+// queues (fast: in place; sort path: radix sort first), finishes.
+template <typename T>
+static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStream_t stream) {
   using namespace dev;
-  hipStream_t stream = (hipStream_t)stream_;
-  DesK k{};
-  k.pos = (const DesPos *)L.d_pos;
-  k.ext = (const DesPosExt *)L.d_ext;
-  k.steps = (const DesStep *)L.d_steps;
-  k.child = L.d_child;
-  k.arr_ops = L.d_arr_ops;
-  k.W = L.W;
-  k.A = L.A;
-  k.E = L.E;
-  k.blk = L.blk;
-  k.BK = L.BK;
-  k.stats = L.d_stats;
-  k.table = L.d_table;
-  k.records = L.d_records;
-  k.N = L.n_traces;
-  k.ld = (L.n_traces + 7) & ~7ull;
-  k.trace_begin = L.trace_begin;
-  k.mean_ns = L.mean_ns;
-  k.k0 = (uint32_t)L.seed;
-  k.k1 = (uint32_t)(L.seed >> 32);
-  k.n_pos = L.n_pos;
-  k.n_slots = L.n_slots;
-  k.modeb = L.modeb;
-  k.n_blk = (uint32_t)((L.n_traces + kDesChunk - 1) / kDesChunk);
-  if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
-  const uint64_t tk_bytes = (chain_tickets(*L.plan) * 4 + 255) & ~255ull;
-  if (hipMemsetAsync(L.chain, 0, des_chain_bytes(*L.plan, L.n_traces), stream) != hipSuccess) return 1;
-  uint32_t *tickets = (uint32_t *)L.chain;
-  k.chain = (ChainState *)((char *)L.chain + tk_bytes);
-  k.n_chunks = (uint32_t)((L.n_traces + kChainChunk - 1) / kChainChunk);
-  hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
-  hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
-  hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   const DesPlan &pl = *L.plan;
   const uint64_t m_max = (uint64_t)pl.max_sort_pos * L.n_traces;
-  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
   char *sw = (char *)L.sort_ws;
-  uint64_t *keys_a = (uint64_t *)sw, *keys_b = (uint64_t *)(sw + al(m_max * 8));
-  uint32_t *vals_a = (uint32_t *)(sw + 2 * al(m_max * 8));
-  uint32_t *vals_b = (uint32_t *)(sw + 2 * al(m_max * 8) + al(m_max * 4));
-  void *sort_tmp = sw + 2 * al(m_max * 8) + 2 * al(m_max * 4);
+  uint64_t *keys_a = (uint64_t *)sw, *keys_b = (uint64_t *)(sw + al256(m_max * 8));
+  uint32_t *vals_a = (uint32_t *)(sw + 2 * al256(m_max * 8));
+  uint32_t *vals_b = (uint32_t *)(sw + 2 * al256(m_max * 8) + al256(m_max * 4));
+  void *sort_tmp = sw + 2 * al256(m_max * 8) + 2 * al256(m_max * 4);
   const size_t sort_tmp_bytes = sort_temp_bytes(m_max);
   k.sort_pos = L.d_sort_pos;
   // (position or row) x trace-range blocks: enough to fill the chip, >= 256 traces each
@@ -1006,30 +1069,28 @@ int des_launch(const DesLaunch &L, void *stream_) {
     sp = sp < cap ? sp : cap;
     return (uint32_t)(sp ? sp : 1);
   };
+  static void (*const down[4])(DesK) = {des_down<T, false, false>, des_down<T, false, true>,
+                                       des_down<T, true, false>, des_down<T, true, true>};
+  static void (*const chain[2])(DesK) = {des_down_chain<T, false>, des_down_chain<T, true>};
   for (uint32_t r = 0; r < pl.rounds(); ++r) {
     // 1. step begins (calls after calls)
     const uint32_t na = pl.arr_off[r + 1] - pl.arr_off[r];
     if (na) {
       k.level_begin = pl.arr_off[r];
       k.splits = splits_for(na);
-      hipLaunchKernelGGL(des_arrive, dim3(k.splits, na), dim3(kDesUpThreads), 0, stream, k);
+      hipLaunchKernelGGL(des_arrive<T>, dim3(k.splits, na), dim3(kDesUpThreads), 0, stream, k);
     }
-    // 2. queues: single-position trace-ordered services scan in place, the
-    //    others sort their arrivals first
+    // 2. queues.  Single-replica groups narrower than the chip take the
+    //    chained scan (many workgroups per position); wide groups and
+    //    replicated services one workgroup per position.
     k.level_pos = L.d_fast_pos;
-    // single-replica groups narrower than the chip take the chained scan
-    // (many workgroups per position); wide groups and replicated services
-    // one workgroup per position
-    static void (*const down[4])(DesK) = {des_down<false, false>, des_down<false, true>, des_down<true, false>,
-                                         des_down<true, true>};
-    static void (*const chain[2])(DesK) = {des_down_chain<false>, des_down_chain<true>};
     for (uint32_t j = 0; j < 4; ++j) {
       const uint32_t b = pl.fast_split[5 * r + j], e = pl.fast_split[5 * r + j + 1];
       if (e == b) continue;
       k.level_begin = b;
       if (j < 2 && e - b < ISIM_DES_CHAIN_BELOW) {
         k.chain_ticket = tickets + 4 * r + j;
-        hipLaunchKernelGGL(chain[j], dim3((e - b) * k.n_chunks), dim3(kChainThreads), 0, stream, k);
+        hipLaunchKernelGGL(chain[j], dim3((e - b) * k.n_chunks), dim3(kDesThreads), 0, stream, k);
       } else {
         hipLaunchKernelGGL(down[j], dim3(e - b), dim3(kDesThreads), 0, stream, k);
       }
@@ -1041,14 +1102,14 @@ int des_launch(const DesLaunch &L, void *stream_) {
       k.vals = vals_a;
       uint64_t g = (m + kDesUpThreads - 1) / kDesUpThreads;
       g = g < 4096 ? g : 4096;
-      hipLaunchKernelGGL(des_sort_keys, dim3((uint32_t)g), dim3(kDesUpThreads), 0, stream, k);
+      hipLaunchKernelGGL(des_sort_keys<T>, dim3((uint32_t)g), dim3(kDesUpThreads), 0, stream, k);
       size_t tb = sort_tmp_bytes;
       if (rocprim::radix_sort_pairs(sort_tmp, tb, keys_a, keys_b, vals_a, vals_b, (size_t)m, 0, 64, stream) !=
           hipSuccess)
         return 1;
       k.skeys = keys_b;
       k.svals = vals_b;
-      hipLaunchKernelGGL(des_down_sorted, dim3(1), dim3(kDesThreads), 0, stream, k);
+      hipLaunchKernelGGL(des_down_sorted<T>, dim3(1), dim3(kDesThreads), 0, stream, k);
     }
     // 3. finishes, deepest group first
     k.level_pos = L.d_fin_pos;
@@ -1056,12 +1117,79 @@ int des_launch(const DesLaunch &L, void *stream_) {
       const uint32_t width = pl.fin_off[gi + 1] - pl.fin_off[gi];
       k.level_begin = pl.fin_off[gi];
       k.splits = splits_for(width);
-      hipLaunchKernelGGL(des_up, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+      hipLaunchKernelGGL(des_up<T>, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
     }
   }
   uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
   fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;
-  hipLaunchKernelGGL(des_finalize, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
+  hipLaunchKernelGGL(des_finalize<T>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
+  return 0;
+}
+
+// Host launcher: the whole DES of one batch on `stream` (no allocation, no
+// host synchronisation).
+int des_launch(const DesLaunch &L, void *stream_) {
+  using namespace dev;
+  hipStream_t stream = (hipStream_t)stream_;
+  const bool narrow = !L.wide;
+  const uint64_t table_words = (uint64_t)L.table_rows * ISIM_DES_ROW_WORDS;
+  DesK k{};
+  k.pos = (const DesPos *)L.d_pos;
+  k.ext = (const DesPosExt *)L.d_ext;
+  k.steps = (const DesStep *)L.d_steps;
+  k.child = L.d_child;
+  k.arr_ops = L.d_arr_ops;
+  k.W = L.W;
+  k.BK = L.BK;
+  k.A = L.A;
+  k.E = L.E;
+  k.blk = L.blk;
+  k.ovf = L.ovf;
+  // narrow rows: statistics go to the staging copy, merged by des_commit
+  k.stats = narrow ? L.stage : L.d_stats;
+  k.table = narrow ? L.stage + L.stats_words : L.d_table;
+  k.records = L.d_records;
+  k.N = L.n_traces;
+  k.ld = row_ld(L.n_traces);
+  k.trace_begin = L.trace_begin;
+  k.mean_ns = L.mean_ns;
+  k.k0 = (uint32_t)L.seed;
+  k.k1 = (uint32_t)(L.seed >> 32);
+  k.n_pos = L.n_pos;
+  k.n_slots = L.n_slots;
+  k.modeb = L.modeb;
+  k.n_blk = (uint32_t)((L.n_traces + kDesChunk - 1) / kDesChunk);
+  k.n_chunks = (uint32_t)((L.n_traces + kDownChunk - 1) / kDownChunk);
+  const uint64_t tk_bytes = al256(chain_tickets(*L.plan) * 4);
+  uint32_t *tickets = (uint32_t *)L.chain;
+  k.chain = (ChainState *)((char *)L.chain + tk_bytes);
+  if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
+  if (hipMemsetAsync(L.chain, 0, des_chain_bytes(*L.plan, L.n_traces), stream) != hipSuccess) return 1;
+  if (narrow) {
+    if (hipMemsetAsync(L.ovf, 0, 4, stream) != hipSuccess) return 1;
+    if (hipMemsetAsync(L.stage, 0, (L.stats_words + table_words) * 8, stream) != hipSuccess) return 1;
+  }
+  hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
+  hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
+  hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
+  const int rc = narrow ? des_rounds<uint32_t>(L, k, tickets, stream) : des_rounds<uint64_t>(L, k, tickets, stream);
+  if (rc) return rc;
+  if (L.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
+    uint32_t n_slots = L.n_slots;
+    uint64_t n = L.n_traces;
+    const uint32_t *mult = L.d_mult;
+    uint64_t *st = k.stats;
+    void *args[] = {&mult, &n_slots, &n, &st};
+    if (hipLaunchKernel(stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args, 0, stream) !=
+        hipSuccess)
+      return 1;
+  }
+  if (narrow) {
+    uint64_t g = (L.stats_words + table_words + 255) / 256;
+    g = g < 1024 ? g : 1024;
+    hipLaunchKernelGGL(des_commit, dim3((uint32_t)(g ? g : 1)), dim3(256), 0, stream, L.stage, L.d_stats,
+                       L.d_table, L.stats_words, table_words, (const uint32_t *)L.ovf);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -9,8 +9,13 @@ open-loop mode) issues requests at exponential gaps; each replica of a
 service (numReplicas, convert/pkg/graph/svc/service.go:30-31) is a FIFO queue
 in front of one worker.  Statuses/hops/counters are the static walk's;
 latencies and per-service durations include queueing.  Runs on the GPU
-through libisim (isim_serve_des*); graphs outside the DES v1 class raise
+through libisim (isim_serve_des*); graphs outside the DES class raise
 IsimError(EINVAL) with the reason.
+
+Rows are 32-bit by default (times relative to each trace's arrival); a
+device batch with a latency of 2^31 ns or more is not accumulated and is
+counted in stats[ST_DES_RETRY] — rerun it with ``wide=True``.  ``serve``
+does that itself.
 """
 from __future__ import annotations
 
@@ -42,20 +47,24 @@ class DesHandler:
         native.check(native.load().isim_des_workspace_bytes(self.handler._h, n_traces, C.byref(out)))
         return int(out.value)
 
-    def serve(self, trace_begin: int, n_traces: int, device: int = 0, records: bool = True):
+    def serve(self, trace_begin: int, n_traces: int, device: int = 0, records: bool = True, wide: bool = False):
         """Synchronous: (records or None, stats, DES table)."""
         stats = self.handler.new_stats()
         table = self.new_table()
         recs = np.zeros(n_traces, REC_DTYPE) if records else None
+        p = native.DesParams(self.params.mean_interarrival_ns, native.DES_FLAG_WIDE if wide else 0, 0)
         native.check(native.load().isim_serve_des(
-            self.handler._h, device, C.byref(self.params), trace_begin, n_traces,
+            self.handler._h, device, C.byref(p), trace_begin, n_traces,
             recs.ctypes.data if records and n_traces else None, stats.ctypes.data, table.ctypes.data))
         return recs, stats, table
 
     def serve_device(self, trace_begin: int, n_traces: int, d_records: int, d_stats: int, d_table: int,
-                     d_workspace: int, workspace_bytes: int, stream: int = 0) -> None:
+                     d_workspace: int, workspace_bytes: int, stream: int = 0, wide: bool = False) -> None:
+        p = self.params
+        if wide:
+            p = native.DesParams(p.mean_interarrival_ns, native.DES_FLAG_WIDE, 0)
         native.check(native.load().isim_serve_des_device(
-            self.handler._h, C.byref(self.params), trace_begin, n_traces, d_records or None, d_stats, d_table,
+            self.handler._h, C.byref(p), trace_begin, n_traces, d_records or None, d_stats, d_table,
             d_workspace, workspace_bytes, stream or None))
 
     def fold(self, table: np.ndarray) -> np.ndarray:

@@ -22,13 +22,14 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 3  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 4  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
 ST_NOT_MIN_LATENCY, ST_MAX_LATENCY = 5, 6
+ST_DES_RETRY = 7  # DES batches not accumulated (32-bit rows overflowed): rerun with DES_FLAG_WIDE
 N_PROM, N_LOG2 = 33, 64
 ST_PROM = 8
 ST_LOG2 = ST_PROM + 2 * N_PROM
@@ -37,6 +38,7 @@ SVC_DUR_WORDS = 2 * N_PROM + 2
 # DES table row (isim.h ISIM_DES_*)
 DES_COUNT, DES_SUM_WAIT, DES_MAX_WAIT, DES_SUM_HOLD = SVC_DUR_WORDS, SVC_DUR_WORDS + 1, SVC_DUR_WORDS + 2, SVC_DUR_WORDS + 3
 DES_ROW_WORDS = SVC_DUR_WORDS + 4
+DES_FLAG_WIDE = 1  # isim_des_params.flags: 64-bit rows
 
 
 class IsimError(RuntimeError):
@@ -76,7 +78,7 @@ class DesParams(C.Structure):
 
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
-                ("table_rows", C.c_int32)]
+                ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("reserved", C.c_int32)]
 
 
 # every function declared in include/isim.h: name -> (restype, argtypes)

@@ -104,9 +104,10 @@ def test_config5_slice(gpu):
     c.compare(0, 256)
 
 
-def test_device_entry_accumulates(gpu):
+@pytest.mark.parametrize("wide", [False, True])
+def test_device_entry_accumulates(gpu, wide):
     import torch
-    c = DesCase(_sleepy_tree(3, 3), 900_000)
+    c = DesCase(_sleepy_tree(3, 3), 3_000_000)  # latencies well below 2^31 ns
     n = 5000
     dev = torch.device("cuda", 0)
     rec = torch.zeros(n * 2, dtype=torch.int64, device=dev)
@@ -116,7 +117,8 @@ def test_device_entry_accumulates(gpu):
     ws = torch.empty(wsb // 8 + 1, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     for half in (0, 1):  # two batches accumulate into the same stats/table
-        c.d.serve_device(half * n, n, rec.data_ptr(), st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s)
+        c.d.serve_device(half * n, n, rec.data_ptr(), st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s,
+                         wide=wide)
     torch.cuda.synchronize()
     _, s0, t0 = c.d.serve(0, n, records=False)
     _, s1, t1 = c.d.serve(n, n, records=False)
@@ -209,3 +211,53 @@ def test_mixed_steps_and_replicas(gpu):
         s["numReplicas"] = 1 + i % 3
         s["errorRate"] = 0.02
     DesCase(doc, 500_000).compare(0, 7000)
+
+
+# ---- row widths: 32-bit rows relative to each trace's
+# arrival, 64-bit rows on request or when a latency reaches 2^31 ns
+
+def test_narrow_equals_wide(gpu):
+    c = DesCase(realistic_topology(300, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.05)), 900_000)
+    r1, s1, t1 = c.d.serve(5, 6000)
+    r2, s2, t2 = c.d.serve(5, 6000, wide=True)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(t1, t2)
+    assert s1[isim.native.ST_DES_RETRY] == 0
+
+
+def _overloaded():
+    # 5 ms of service per trace every ~100 us: the queue grows ~5 ms per
+    # trace, so late traces wait for tens of seconds (> 2^31 ns)
+    doc = tree_topology(2, 2)
+    for s in doc["services"]:
+        s["script"] = [{"sleep": "5ms"}] + s.get("script", [])
+    return doc
+
+
+def test_overflow_retries_wide(gpu):
+    import torch
+    c = DesCase(_overloaded(), 100_000)
+    n = 3000
+    recs, stats, rows = c.compare(0, n)  # the synchronous entry reruns the batch with 64-bit rows
+    assert int(stats[isim.native.ST_MAX_LATENCY]) >= 1 << 31 and stats[isim.native.ST_DES_RETRY] == 0
+    # the device entry drops the batch and counts it
+    dev = torch.device("cuda", 0)
+    st = torch.zeros(c.h.stats_words, dtype=torch.int64, device=dev)
+    tab = torch.zeros(max(1, c.d.table_words), dtype=torch.int64, device=dev)
+    rec = torch.full((2 * n,), -1, dtype=torch.int64, device=dev)
+    wsb = c.d.workspace_bytes(n)
+    ws = torch.empty(wsb // 8 + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    c.d.serve_device(0, n, rec.data_ptr(), st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy().view(np.uint64)
+    assert got[isim.native.ST_DES_RETRY] == 1
+    got[isim.native.ST_DES_RETRY] = 0
+    assert got.sum() == 0 and tab.sum().item() == 0 and (rec == -1).all().item()
+    # wide rows on the same buffers: the oracle's numbers
+    c.d.serve_device(0, n, rec.data_ptr(), st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s, wide=True)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy().view(np.uint64).copy()
+    assert got[isim.native.ST_DES_RETRY] == 1  # the earlier drop stays counted
+    got[isim.native.ST_DES_RETRY] = 0
+    assert np.array_equal(got, stats)
+    assert np.array_equal(c.d.fold(tab.cpu().numpy().view(np.uint64)), rows)
