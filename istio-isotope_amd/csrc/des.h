@@ -108,6 +108,7 @@ struct DesLaunch {
   void *chain;                       // chained-scan states of the down pass (des_chain_bytes)
   uint32_t *ovf;                     // narrow rows: overflow flag
   uint64_t *stage;                   // narrow rows: staged stats (stats_words) + table
+  uint32_t *stbits;                  // own error status bits [n_pos][words of 32 traces]
   void *sort_ws;                     // sort path (keys, values, radix-sort temp)
   // caller buffers
   uint64_t *d_stats, *d_table;

@@ -126,6 +126,8 @@ struct DesK {
   uint64_t *table;            // [rows][ISIM_DES_ROW_WORDS] (staged likewise)
   isim_trace_rec *records;
   uint32_t *ovf;              // narrow rows: a value reached 2^31
+  const uint32_t *stbits;     // own error status of (position, trace): bit t%32 of word [v][t/32]
+  uint32_t st_wpr;            // words per status row
   uint64_t N, trace_begin, mean_ns;
   uint64_t ld;                // row stride in traces: N rounded up to 16 (64-B aligned rows)
   uint32_t k0, k1;
@@ -343,28 +345,67 @@ __global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
     if (base + i < k.N) k.A[base + i] += off;
 }
 
-// hist[bin] += 1 for every lane with bin != kNoBin, one LDS atomic per
-// distinct bin of the wave (durations of one position mostly share a bin).
-// Call with the whole wave converged.
+// hist[bin[i]] += 1 for the (up to) 4 bins of every lane (kNoBin: none).
+// The durations of one position mostly share a bin: the wave counts the bins
+// equal to its first lane's first bin with ballots and adds them with one LDS
+// atomic; the rest go one atomic each.  Call with the wave converged.
 constexpr uint32_t kNoBin = 0xFFFFFFFFu;
-__device__ __forceinline__ void hist_add_wave(uint32_t *hist, uint32_t bin) {
-  uint64_t pending = __ballot(bin != kNoBin);
-  while (pending) {
-    const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)leader);
-    const uint64_t m = __ballot(bin == b);
-    if ((threadIdx.x & 63u) == leader) atomicAdd(&hist[b], (uint32_t)__builtin_popcountll(m));
-    pending &= ~m;
+__device__ __forceinline__ void hist_add4(uint32_t *hist, const uint32_t (&bin)[4]) {
+  const uint32_t first = bin[0] != kNoBin ? bin[0] : bin[1] != kNoBin ? bin[1] : bin[2] != kNoBin ? bin[2] : bin[3];
+  const uint64_t any = __ballot(first != kNoBin);
+  if (!any) return;
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)first, (int)__builtin_ctzll(any));
+  uint32_t n = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    n += (uint32_t)__builtin_popcountll(__ballot(bin[i] == b0));
+    if (bin[i] != kNoBin && bin[i] != b0) atomicAdd(&hist[bin[i]], 1u);
   }
+  if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(any)) atomicAdd(&hist[b0], n);
 }
 
-// A leaf finished in its queue pass (kDesFlagFused): F = S + script time, its
-// own error status (drawn with the loads), the duration F - a into the LDS
-// histogram.
-__device__ __forceinline__ uint32_t des_own_status(const DesK &k, uint32_t v, const DesPos &P, uint64_t t) {
-  if (P.flags & kDesFlagAlways) return 1u;
-  if (!P.thr) return 0u;
-  return des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr ? 1u : 0u;
+// own error statuses of traces [base, base+4) of position v (base % 4 == 0),
+// bit i; the status pass zeroes bits past N
+__device__ __forceinline__ uint32_t des_status4(const DesK &k, uint32_t v, uint64_t base) {
+  return (k.stbits[(uint64_t)v * k.st_wpr + (base >> 5)] >> (base & 31u)) & 0xFu;
+}
+
+// ---- status pass: the own error status of every (position, trace).  The
+// four positions 4g..4g+3 share Philox block (t, g, 0, 0) (word j for
+// position 4g+j, as in the walks), so one block per (group, trace) instead of
+// one per (position, trace).  One thread: a group x 32 consecutive traces.
+__global__ void __launch_bounds__(256) des_status(DesK k) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t ng = (k.n_pos + 3) / 4;
+  const uint64_t g = tid / k.st_wpr, w = tid - g * k.st_wpr;
+  if (g >= ng) return;
+  uint32_t thr[4], always[4], live[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t v = (uint32_t)g * 4 + j;
+    live[j] = v < k.n_pos;
+    const DesPos &P = k.pos[live[j] ? v : 0];
+    thr[j] = live[j] ? P.thr : 0u;
+    always[j] = live[j] && (P.flags & kDesFlagAlways);
+  }
+  uint32_t bits[4] = {0, 0, 0, 0};
+  const uint32_t any = thr[0] | thr[1] | thr[2] | thr[3];
+  for (uint32_t b = 0; b < 32; ++b) {
+    const uint64_t t = w * 32 + b;
+    if (t >= k.N) break;
+    if (any) {
+      uint32_t c[4] = {(uint32_t)(k.trace_begin + t), (uint32_t)((k.trace_begin + t) >> 32), (uint32_t)g, 0u};
+      des_philox(c, k.k0, k.k1);
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) bits[j] |= (uint32_t)(always[j] || (thr[j] && c[j] < thr[j])) << b;
+    } else {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) bits[j] |= always[j] << b;
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    if (live[j]) const_cast<uint32_t *>(k.stbits)[(g * 4 + j) * k.st_wpr + w] = bits[j];
 }
 
 // per-service duration statistics of a workgroup: LDS histogram + sums -> the
@@ -442,9 +483,9 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
                                              uint32_t mask, uint32_t stm, uint64_t (&out)[kPer], uint32_t *hist,
                                              uint64_t &wsum, uint64_t &wmax, uint64_t &d0, uint64_t &d1,
                                              uint64_t &n5, bool &bad) {
+  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
-    uint32_t bin = kNoBin;
     if (base + i < N && ((mask >> i) & 1u)) {
       const uint64_t S = x > a[i] ? x : a[i];
       const uint64_t w = S - a[i];
@@ -460,7 +501,7 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
         n5 += st;
         d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
         d0 += st ? 0 : dur;
-        bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+        bin[i] = st * ISIM_N_PROM + des_prom_bucket(dur);
         bad |= !Row<T>::fits(F);
         val = F | ((uint64_t)st << Row<T>::kTop);
       } else {
@@ -468,8 +509,8 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
       }
       out[i] = val;
     }
-    if constexpr (FUSED) hist_add_wave(hist, bin);
   }
+  if constexpr (FUSED) hist_add4(hist, bin);
 }
 
 // this thread's 4 traces: relative arrivals + A_t -> absolute arrivals a, A_t
@@ -515,14 +556,13 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
     uint64_t a[kPer], At[kPer], o[kPer] = {0, 0, 0, 0};
     load_arrivals<T>(k, par, off, base, N, a, At);
     uint32_t rr[kPer];
-    uint32_t stm = 0;  // fused leaves: own error statuses, bit i
+    const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;  // fused leaves: own error statuses, bit i
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
       if constexpr (MULTI)
         rr[i] = base + i < N ? des_draw(k.trace_begin + base + i, v, 0x80000002u, 0, k.k0, k.k1) % reps : 0u;
       else
         rr[i] = 0u;
-      if constexpr (FUSED) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
     }
     for (uint32_t r = 0; r < reps; ++r) {
       MaxPlus f{0, 0};
@@ -610,11 +650,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
   uint64_t a[kPer], At[kPer];
   load_arrivals<T>(k, par, off, base, N, a, At);
-  uint32_t stm = 0;
-  if constexpr (FUSED) {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) stm |= (base + i < N ? des_own_status(k, v, P, base + i) : 0u) << i;
-  }
+  const uint32_t stm = FUSED && base < N ? des_status4(k, v, base) : 0u;
   MaxPlus f{0, 0};
   uint32_t mask = 0;
 #pragma unroll
@@ -756,16 +792,15 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
       }
     }
     uint64_t o[kPer];
+    const uint32_t stm = des_status4(k, v, b0);
+    uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
       const uint64_t t = b0 + i;
-      uint32_t bin = kNoBin;
       o[i] = 0;
       if (t < te) {
         const uint64_t F = leaf ? m[i] : m[i] + P.post;
-        uint32_t own = 0;
-        if (P.flags & kDesFlagAlways) own = 1;
-        else if (P.thr) own = des_draw(k.trace_begin + t, v >> 2, 0u, v & 3u, k.k0, k.k1) < P.thr;
+        const uint32_t own = (stm >> i) & 1u;
         const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
         const uint64_t dur = F - a[i];
         bad |= !Row<T>::fits(F);
@@ -774,10 +809,10 @@ __global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
         n500 += st;
         dsum1 += st ? dur : 0;
         dsum0 += st ? 0 : dur;
-        bin = st * ISIM_N_PROM + des_prom_bucket(dur);
+        bin[i] = st * ISIM_N_PROM + des_prom_bucket(dur);
       }
-      hist_add_wave(hist, bin);
     }
+    hist_add4(hist, bin);
     store4n<T>(mine, b0, te, o);
   }
   flag_overflow(k, bad);
@@ -1010,6 +1045,7 @@ static size_t sort_temp_bytes(uint64_t m) {
 static uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 static uint64_t row_ld(uint64_t n) { return (n + 15) & ~15ull; }
 static uint64_t chain_tickets(const DesPlan &plan) { return 4ull * plan.rounds(); }
+static uint64_t status_wpr(uint64_t n) { return (((n + 31) / 32) + 15) & ~15ull; }
 
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n) {
   const uint64_t chunks = (n + dev::kDownChunk - 1) / dev::kDownChunk;
@@ -1025,7 +1061,8 @@ uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n, uint64_t stats_wor
   const uint64_t sort = m ? 2 * al256(m * 8) + 2 * al256(m * 4) + al256(sort_temp_bytes(m)) : 0;
   return al256((uint64_t)plan.pos.size() * ld * 8) + al256((uint64_t)plan.steps.size() * ld * 8) + al256(n * 8) +
          al256(n * 4) + al256((nblk + 1) * 8) + al256(des_chain_bytes(plan, n)) + 256 +
-         al256((stats_words + table_rows * ISIM_DES_ROW_WORDS) * 8) + sort;
+         al256((stats_words + table_rows * ISIM_DES_ROW_WORDS) * 8) +
+         al256((uint64_t)plan.pos.size() * status_wpr(n) * 4) + sort;
 }
 
 void des_carve(DesLaunch &L, void *workspace) {
@@ -1045,6 +1082,7 @@ void des_carve(DesLaunch &L, void *workspace) {
   L.chain = take(des_chain_bytes(plan, n));
   L.ovf = (uint32_t *)take(4);
   L.stage = (uint64_t *)take((L.stats_words + (uint64_t)L.table_rows * ISIM_DES_ROW_WORDS) * 8);
+  L.stbits = (uint32_t *)take((uint64_t)plan.pos.size() * status_wpr(n) * 4);
   L.sort_ws = ws;
 }
 
@@ -1145,6 +1183,8 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.E = L.E;
   k.blk = L.blk;
   k.ovf = L.ovf;
+  k.stbits = L.stbits;
+  k.st_wpr = (uint32_t)status_wpr(L.n_traces);
   // narrow rows: statistics go to the staging copy, merged by des_commit
   k.stats = narrow ? L.stage : L.d_stats;
   k.table = narrow ? L.stage + L.stats_words : L.d_table;
@@ -1172,6 +1212,10 @@ int des_launch(const DesLaunch &L, void *stream_) {
   hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
+  {
+    const uint64_t threads = (uint64_t)((L.n_pos + 3) / 4) * k.st_wpr;
+    hipLaunchKernelGGL(des_status, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, k);
+  }
   const int rc = narrow ? des_rounds<uint32_t>(L, k, tickets, stream) : des_rounds<uint64_t>(L, k, tickets, stream);
   if (rc) return rc;
   if (L.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
