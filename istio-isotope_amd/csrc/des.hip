@@ -45,9 +45,13 @@ constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per arriva
 constexpr uint32_t kPer = 4;                           // consecutive traces per thread in the row passes
 constexpr uint32_t kDownChunk = kPer * kDesThreads;    // traces per down-pass chunk
 #ifndef ISIM_DES_CHAIN_BELOW
-#define ISIM_DES_CHAIN_BELOW 512  // positions per launch below which the chained scan is used
+#define ISIM_DES_CHAIN_BELOW 256  // positions per launch below which the chained scan is used
 #endif
 constexpr uint32_t kDesUpThreads = 256;
+#ifndef ISIM_DES_DOWN_THREADS
+#define ISIM_DES_DOWN_THREADS 512
+#endif
+constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-position queue pass
 
 __constant__ int32_t c_ln[257] = {
 #include "des_ln_table.inc"
@@ -532,18 +536,18 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 // ---- queue pass, one workgroup per position (wide groups; replicated
 // services: per-replica scans, the routing draw per trace)
 template <typename T, bool MULTI, bool FUSED>
-__global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
-  __shared__ MaxPlus wtot[kDesThreads / 64];
+__global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
+  __shared__ MaxPlus wtot[kDownThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
-  __shared__ uint64_t red[3 * kDesThreads / 64];
-  __shared__ MaxPlus xs[kDesThreads];
+  __shared__ uint64_t red[3 * kDownThreads / 64];
+  __shared__ MaxPlus xs[kDownThreads];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
   const DesPos P = k.pos[v];
   const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
   if constexpr (FUSED)
-    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
   __syncthreads();
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
@@ -551,7 +555,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
   T *out = row<T>(k.W, k.ld, v);
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
-  for (uint64_t c0 = 0; c0 < N; c0 += kDownChunk) {
+  for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
     const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
     uint64_t a[kPer], At[kPer], o[kPer] = {0, 0, 0, 0};
     load_arrivals<T>(k, par, off, base, N, a, At);
@@ -573,7 +577,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
           f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
           mask |= 1u << i;
         }
-      const MaxPlus inc = mp_block_scan(f, wtot);
+      const MaxPlus inc = mp_block_scan<kDownThreads>(f, wtot);
       // exclusive prefix = the previous thread's inclusive one
       xs[threadIdx.x] = inc;
       __syncthreads();
@@ -582,7 +586,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
       const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
       queue_finish<T, FUSED>(k, P, base, N, x, a, At, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
       __syncthreads();  // every thread has read carry[r]
-      if (threadIdx.x == kDesThreads - 1) {
+      if (threadIdx.x == kDownThreads - 1) {
         uint64_t xe = x;
 #pragma unroll
         for (uint32_t i = 0; i < kPer; ++i)
@@ -594,10 +598,10 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down(DesK k) {
     store4n<T>(out, base, N, o);
   }
   flag_overflow(k, bad);
-  des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
+  des_flush_waits<kDownThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
-    des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red);
+    des_flush_durations<kDownThreads>(k, P, hist, d0, d1, n5, red);
   }
 }
 
@@ -738,7 +742,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
 // ---- up pass: finish times, statuses, per-service durations.
 // (position, trace-range) blocks; 4 consecutive traces per thread.
 template <typename T>
-__global__ void __launch_bounds__(kDesUpThreads) des_up(DesK k) {
+__global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hist[i] = 0;
@@ -1130,7 +1134,7 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
         k.chain_ticket = tickets + 4 * r + j;
         hipLaunchKernelGGL(chain[j], dim3((e - b) * k.n_chunks), dim3(kDesThreads), 0, stream, k);
       } else {
-        hipLaunchKernelGGL(down[j], dim3(e - b), dim3(kDesThreads), 0, stream, k);
+        hipLaunchKernelGGL(down[j], dim3(e - b), dim3(kDownThreads), 0, stream, k);
       }
     }
     for (uint32_t si = pl.sorted_off[r]; si < pl.sorted_off[r + 1]; ++si) {
