@@ -48,7 +48,8 @@ def main(src, rnd):
     out = {
         "round": int(rnd.lstrip("r")), "config": "c5", "batch": bench["config"]["traces_per_rank_per_step"],
         "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --config c5 ; PMC passes --pmc FETCH_SIZE "
-                   "| WRITE_SIZE (bench.py --config c5 --steps 2 --warmup 1 --no-cpu)",
+                   "| WRITE_SIZE | SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE "
+                   "(bench.py --config c5 --steps 2 --warmup 1 --no-cpu)",
         "des_kernel_ns_per_step": des_ns / n_steps,
         "des_calls": calls,
         "fetch_size_kb_per_step": fetch, "write_size_kb_per_step": write,
