@@ -93,6 +93,9 @@ def main(src, rnd):
         "grbm_gui_active": sq2["GRBM_GUI_ACTIVE"],
         "effective_clock_ghz": sq2["GRBM_GUI_ACTIVE"] / xcds / kernel_ns,
         "occupancy": occupancy(sq1["SQ_WAVE_CYCLES"], sq2["GRBM_GUI_ACTIVE"]),
+        # a CU issues at most one wave64 VALU instruction per cycle (4 SIMDs x 16 lanes, 4 passes)
+        "valu_issue_frac": sq1["SQ_INSTS_VALU"] / (sq2["GRBM_GUI_ACTIVE"] / xcds * CUS),
+        "salu_issue_frac": sq1["SQ_INSTS_SALU"] / (sq2["GRBM_GUI_ACTIVE"] / xcds * CUS),
     }
     with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
