@@ -51,7 +51,7 @@ struct DevState {
   // DES (config 5): the plan uploaded on first use
   void *d_des_pos = nullptr;
   uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
-  uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr;
+  uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr, *d_des_zero = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
 };
 
@@ -83,6 +83,7 @@ struct isim_handler {
         (void)hipFree(kv.second.d_des_level);
         (void)hipFree(kv.second.d_des_mult);
         (void)hipFree(kv.second.d_des_fast);
+        (void)hipFree(kv.second.d_des_zero);
         (void)hipFree(kv.second.d_des_sort);
         (void)hipFree(kv.second.d_des_arr);
         (void)hipFree(kv.second.d_des_ext);
@@ -503,7 +504,8 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
       !up(&st->d_des_steps, d.steps.data(), d.steps.size() * sizeof(isim::DesStep)) ||
       !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4) ||
       !up((void **)&st->d_des_fast, d.fast_pos.data(), d.fast_pos.size() * 4) ||
-      !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4))
+      !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4) ||
+      !up((void **)&st->d_des_zero, d.zero_pos.data(), d.zero_pos.size() * 4))
     return fail(ISIM_EHIP, "DES plan upload failed");
   return ISIM_OK;
 }
@@ -562,6 +564,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.d_fin_pos = st->d_des_level;
   L.d_arr_ops = st->d_des_arr;
   L.d_fast_pos = st->d_des_fast;
+  L.d_zero_pos = st->d_des_zero;
   L.d_sort_pos = st->d_des_sort;
   L.d_mult = st->d_des_mult;
   L.d_stats = d_stats;

@@ -86,6 +86,7 @@ struct DesPlan {
   // [rounds][5]: a round's fast positions by kernel variant (des_down<MULTI, FUSED>):
   // [v][0..1) single replica, [1..2) fused single, [2..3) replicas, [3..4) fused replicas
   std::vector<uint32_t> fast_split;
+  std::vector<uint32_t> zero_pos, zero_off;      // positions of zero-hold services: start = arrival
   std::vector<DesSortSvc> sorted;                // sort-path services
   std::vector<uint32_t> sorted_off;
   std::vector<uint32_t> sort_pos;                // positions of the sort-path services
@@ -99,7 +100,7 @@ struct DesPlan {
 struct DesLaunch {
   const DesPlan *plan;               // host copy (the schedule)
   const void *d_pos, *d_ext, *d_steps;  // DesPos[n_pos], DesPosExt[n_pos], DesStep[]
-  const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops;
+  const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops, *d_zero_pos;
   const uint32_t *d_mult;            // per slot: calls per trace (executed-call counters)
   // workspace parts (des_carve)
   void *W, *BK;                      // rows [n_pos][ld], [steps][ld] of u32 (narrow) or u64

@@ -1010,6 +1010,29 @@ __global__ void __launch_bounds__(kDesUpThreads) des_arrive(DesK k) {
   flag_overflow(k, bad);
 }
 
+// ---- zero-hold services: no queue, start = arrival (relative), per
+// (position, trace-range) block; the queue statistics: N invocations, no wait
+template <typename T>
+__global__ void __launch_bounds__(kDesUpThreads) des_zero(DesK k) {
+  const uint32_t v = k.level_pos[k.level_begin + blockIdx.y];
+  const DesPos P = k.pos[v];
+  const uint64_t N = k.N;
+  const uint64_t tb = N * blockIdx.x / k.splits, te = N * (blockIdx.x + 1) / k.splits;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
+  T *out = row<T>(k.W, k.ld, v);
+  bool bad = false;
+  for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
+    const uint64_t a = par ? (uint64_t)par[t] + off : 0;
+    bad |= !Row<T>::fits(a);
+    out[t] = (T)a;
+  }
+  flag_overflow(k, bad);
+  if (threadIdx.x == 0 && te > tb)
+    atomicAdd((unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS + ISIM_DES_COUNT),
+              (unsigned long long)(te - tb));
+}
+
 // ---- narrow rows: merge the staged statistics into the caller's buffers,
 // or count the batch in ISIM_ST_DES_RETRY when a value overflowed
 __global__ void __launch_bounds__(256) des_commit(const uint64_t *__restrict__ stage, uint64_t *stats,
@@ -1122,7 +1145,15 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       k.splits = splits_for(na);
       hipLaunchKernelGGL(des_arrive<T>, dim3(k.splits, na), dim3(kDesUpThreads), 0, stream, k);
     }
-    // 2. queues.  Single-replica groups narrower than the chip take the
+    // 2. queues.  Zero-hold services: start = arrival.
+    const uint32_t nz = pl.zero_off[r + 1] - pl.zero_off[r];
+    if (nz) {
+      k.level_pos = L.d_zero_pos;
+      k.level_begin = pl.zero_off[r];
+      k.splits = splits_for(nz);
+      hipLaunchKernelGGL(des_zero<T>, dim3(k.splits, nz), dim3(kDesUpThreads), 0, stream, k);
+    }
+    //    Single-replica groups narrower than the chip take the
     //    chained scan (many workgroups per position); wide groups and
     //    replicated services one workgroup per position.
     k.level_pos = L.d_fast_pos;

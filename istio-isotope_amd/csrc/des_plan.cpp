@@ -10,9 +10,10 @@
 //   3. finishes      F of positions whose start and callees are settled,
 //                    deepest first.
 // Every operation goes in the earliest round its inputs allow (longest path
-// over the dependency graph); a dependency cycle — a service invoked both
-// inside a call step and after it within one caller's script — has no
-// schedule and is rejected.  Graphs whose scripts have at most one call step
+// over the dependency graph); a dependency cycle — a service with a nonzero
+// hold invoked both inside a call step and after it within one caller's
+// script — has no schedule and is rejected.  Zero-hold services (no sleeps)
+// never queue: each of their positions starts at its arrival, one op each.  Graphs whose scripts have at most one call step
 // get the shortest schedule: queues by service level, all finishes last.
 #include "des.h"
 
@@ -92,7 +93,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (!shaped[svc]) {
       shape[svc] = shape_of(g.services[svc]);
       shaped[svc] = 1;
-      if (std::max<int32_t>(1, g.services[svc].num_replicas) > (int32_t)kDesMaxReplicas) {
+      // a zero-hold service never makes an invocation wait (start = arrival):
+      // its replicas do not matter
+      if (shape[svc].hold > 0 && std::max<int32_t>(1, g.services[svc].num_replicas) > (int32_t)kDesMaxReplicas) {
         err = "service \"" + g.services[svc].name + "\" has more than 64 replicas (DES limit)";
         return ISIM_EINVAL;
       }
@@ -174,14 +177,18 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   for (uint32_t i = 0; i < np; ++i) {
     const uint32_t par = out.pos[i].parent;
     arr_sorted[i] = par == kDesNoParent ? 1 : (s_sorted[par] && kstep[i] == 0);
-    s_sorted[i] = arr_sorted[i] && out.pos[i].reps == 1;
+    s_sorted[i] = arr_sorted[i] && (out.pos[i].reps == 1 || out.pos[i].hold == 0);
   }
 
-  // ---- the schedule: op ids  Q(s) = service s, F(v) = n + v, A(b) = n + np + b
+  // ---- the schedule: op ids  Q(s) = service s, F(v) = n + v, A(b) = n + np + b,
+  // Z(v) = n + np + nb + v: the start of a position of a zero-hold service
+  // (start = arrival, no queue: one op per position, so such a service can be
+  // called both inside a call step and after it)
   const uint32_t nq = (uint32_t)n, nb = (uint32_t)out.steps.size();
-  const uint32_t n_ops = nq + np + nb;
+  const uint32_t n_ops = nq + np + nb + np;
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> pred(n_ops);  // (op, weight)
-  auto Q = [&](uint32_t v) { return (uint32_t)pos_svc[v]; };
+  auto zero = [&](uint32_t v) { return out.pos[v].hold == 0; };
+  auto Q = [&](uint32_t v) { return zero(v) ? nq + np + nb + v : (uint32_t)pos_svc[v]; };
   auto F = [&](uint32_t v) { return nq + v; };
   auto Ab = [&](uint32_t b) { return nq + np + b; };
   for (uint32_t v = 0; v < np; ++v) {
@@ -237,12 +244,14 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     R += 1;
   }
   // ---- lay the rounds out
-  std::vector<std::vector<uint32_t>> arr(R), fast(R);
+  std::vector<std::vector<uint32_t>> arr(R), fast(R), zpos(R);
   std::vector<std::vector<int32_t>> srt(R);
   std::vector<std::vector<std::vector<uint32_t>>> fin(R, std::vector<std::vector<uint32_t>>(out.n_levels));
   for (uint32_t b = 0; b < nb; ++b) arr[rnd[Ab(b)]].push_back(b);
+  for (uint32_t v = 0; v < np; ++v)
+    if (zero(v)) zpos[rnd[Q(v)]].push_back(v);
   for (int32_t s = 0; s < n; ++s) {
-    if (svc_pos[s].empty()) continue;
+    if (svc_pos[s].empty() || shape[s].hold == 0) continue;
     bool need = svc_pos[s].size() > 1;
     for (uint32_t v : svc_pos[s]) need = need || !arr_sorted[v];
     if (need) {
@@ -259,6 +268,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (!(out.pos[v].flags & kDesFlagFused)) fin[rnd[F(v)]][depth[v]].push_back(v);
   out.arr_off.assign(R + 1, 0);
   out.fast_off.assign(R + 1, 0);
+  out.zero_off.assign(R + 1, 0);
   out.fast_split.assign(5 * R, 0);
   out.sorted_off.assign(R + 1, 0);
   out.fin_round_off.assign(R + 1, 0);
@@ -280,6 +290,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     out.fast_split[5 * r + 4] = at;
     out.fast_pos.insert(out.fast_pos.end(), fast[r].begin(), fast[r].end());
     out.fast_off[r + 1] = (uint32_t)out.fast_pos.size();
+    out.zero_pos.insert(out.zero_pos.end(), zpos[r].begin(), zpos[r].end());
+    out.zero_off[r + 1] = (uint32_t)out.zero_pos.size();
     for (int32_t s : srt[r]) {
       DesSortSvc ss;
       ss.row = (uint32_t)p.svc_row[s];

@@ -103,15 +103,20 @@ def test_des_class():
     _rejects(_handler(mesh_topology(800, 4)), "static walk")
     doc = tree_topology(3, 3)
     doc["services"][-1]["numReplicas"] = 65
+    isim.DesHandler(_handler(doc), 1_000_000)  # no sleeps: never queues, replicas do not matter
+    doc["services"][-1]["script"] = [{"sleep": "1ms"}]
     _rejects(_handler(doc), "more than 64 replicas")
     d = isim.DesHandler(_handler(realistic_topology(200, concurrent=True, sleep_ms=(1, 5))), 5_000_000)
     assert (d.info.n_positions, d.info.table_rows) == (200, 200)
     assert d.info.n_levels >= 2 and d.info.max_width >= 1
     assert d.workspace_bytes(1000) >= 200 * 1000 * 8 + 1000 * 12
     # DAG graphs (a service at several positions) and replicated callers take the sort path
-    canon = yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read())
+    canon = json.loads(yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read()))
     # b is called inside d's first call step (through c) and in its second:
-    # b's queue would wait for its own finish
+    # without sleeps b never queues (one start op per position) ...
+    isim.DesHandler(_handler(canon), 1_000_000)
+    # ... with a hold, b's queue would wait for its own finish
+    canon["services"][1]["script"] = [{"sleep": "1ms"}]
     _rejects(_handler(canon), "called both inside a call step and after it")
     dc = isim.DesHandler(_handler(canonical_concurrent()), 1_000_000)
     assert dc.info.n_positions == 6

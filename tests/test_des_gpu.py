@@ -261,3 +261,34 @@ def test_overflow_retries_wide(gpu):
     got[isim.native.ST_DES_RETRY] = 0
     assert np.array_equal(got, stats)
     assert np.array_equal(c.d.fold(tab.cpu().numpy().view(np.uint64)), rows)
+
+
+# ---- zero-hold services (no sleeps): start = arrival, one op per position
+
+def _fixture_doc(name):
+    import os
+    from isim.yamljson import yaml_to_json
+    from conftest import TOPOLOGIES
+    return json.loads(yaml_to_json(open(os.path.join(TOPOLOGIES, name), "rb").read()))
+
+
+@pytest.mark.parametrize("name", ["canonical.yaml", "canonical-2-replicas.yaml", "10-svc_1000-end.yaml",
+                                  "chain-3-services.yaml", "tree-111-services.yaml", "1-service.yaml"])
+def test_reference_topologies_as_written(gpu, name):
+    # the reference's example graphs have no sleeps: nothing queues, the
+    # cyclic canonical schedule and 100-replica services are in the class
+    doc = _fixture_doc(name)
+    doc.setdefault("defaults", {})["errorRate"] = 0.1
+    DesCase(doc, 200_000).compare(0, 4000)
+
+
+@pytest.mark.parametrize("mean", [150_000, 1_000_000])
+def test_canonical_zero_hold_cycle_with_queues(gpu, mean):
+    # b (no sleep) is called inside d's first step (through c) and in its
+    # second; a, c and d hold their workers
+    doc = _fixture_doc("canonical.yaml")
+    for s in doc["services"]:
+        if s["name"] != "b":
+            s["script"] = [{"sleep": "300us"}] + s.get("script", [])
+    doc["services"][0]["numReplicas"] = 2
+    DesCase(doc, mean).compare(0, 6000)
