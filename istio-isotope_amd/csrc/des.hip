@@ -213,6 +213,29 @@ __device__ __forceinline__ void store4n(T *p, uint64_t base, uint64_t n, const u
       if (base + i < n) p[base + i] = (T)x[i];
   }
 }
+// the same in the row type (no widening: 4 VGPRs per u32 row)
+template <typename T>
+__device__ __forceinline__ void load4t(const T *p, uint64_t base, uint64_t n, T (&x)[kPer]) {
+  if (base + kPer <= n) {
+    if constexpr (sizeof(T) == 4) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(p + base);
+      x[0] = v.x;
+      x[1] = v.y;
+      x[2] = v.z;
+      x[3] = v.w;
+    } else {
+      const ulonglong2 a = reinterpret_cast<const ulonglong2 *>(p + base)[0];
+      const ulonglong2 b = reinterpret_cast<const ulonglong2 *>(p + base)[1];
+      x[0] = a.x;
+      x[1] = a.y;
+      x[2] = b.x;
+      x[3] = b.y;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) x[i] = base + i < n ? p[base + i] : (T)0;
+  }
+}
 __device__ __forceinline__ void load4a(const uint64_t *p, uint64_t base, uint64_t n, uint64_t (&x)[kPer]) {
   load4n<uint64_t>(p, base, n, x);
 }
@@ -783,17 +806,35 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) m[i] += P.floor;
     if (!leaf) {
-      for (uint32_t c = 0; c < P.child_cnt; ++c) {
-        uint64_t f[kPer];
-        load4n<T>(row<T>(k.W, k.ld, k.child[P.child_off + c]), b0, te, f);
-        const bool in_max = c >= c_max_from;
+      // children's finishes: several rows in flight per step (each child row is a
+      // full memory latency; one at a time left the hubs latency-bound)
+      T cm[kPer] = {0, 0, 0, 0};
+      auto take = [&](const T (&f)[kPer], bool in_max) {
 #pragma unroll
         for (uint32_t i = 0; i < kPer; ++i) {
-          const uint64_t tc = f[i] & Row<T>::kMask;
-          if (in_max) m[i] = tc > m[i] ? tc : m[i];
+          const T tc = f[i] & (T)Row<T>::kMask;
+          if (in_max) cm[i] = tc > cm[i] ? tc : cm[i];
           sto |= (uint32_t)(f[i] >> Row<T>::kTop) << i;
         }
+      };
+      const uint32_t *ch = k.child + P.child_off;
+      const uint32_t cnt = P.child_cnt;
+      constexpr uint32_t CB = sizeof(T) == 4 ? 4 : 2;  // rows in flight (VGPR budget of 8 waves/SIMD)
+      uint32_t c = 0;
+      for (; c + CB <= cnt; c += CB) {
+        T f[CB][kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.W, k.ld, ch[c + j]), b0, te, f[j]);
+#pragma unroll
+        for (uint32_t j = 0; j < CB; ++j) take(f[j], c + j >= c_max_from);
       }
+      for (; c < cnt; ++c) {
+        T f[kPer];
+        load4t<T>(row<T>(k.W, k.ld, ch[c]), b0, te, f);
+        take(f, c >= c_max_from);
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) m[i] = (uint64_t)cm[i] > m[i] ? (uint64_t)cm[i] : m[i];
     }
     uint64_t o[kPer];
     const uint32_t stm = des_status4(k, v, b0);
