@@ -506,8 +506,8 @@ __device__ __forceinline__ void des_flush_waits(const DesK &k, uint32_t trow_idx
 // (S or, fused, F | status, relative to A_t), waits and durations.
 template <typename T, bool FUSED>
 __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uint64_t base, uint64_t N,
-                                             uint64_t x, const uint64_t (&a)[kPer], const uint64_t (&At)[kPer],
-                                             uint32_t mask, uint32_t stm, uint64_t (&out)[kPer], uint32_t *hist,
+                                             uint64_t x, const uint64_t (&a)[kPer], const T (&r)[kPer],
+                                             uint64_t off, uint32_t mask, uint32_t stm, uint64_t (&out)[kPer], uint32_t *hist,
                                              uint64_t &wsum, uint64_t &wmax, uint64_t &d0, uint64_t &d1,
                                              uint64_t &n5, bool &bad) {
   uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
@@ -519,7 +519,7 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
       wsum += w;
       wmax = w > wmax ? w : wmax;
       x = S + P.hold;
-      uint64_t val = S - At[i];
+      uint64_t val = w + (uint64_t)r[i] + off;  // S - A_t (off is 0 for the entry: r = 0)
       if constexpr (FUSED) {
         const uint64_t F = val + P.floor;
         const uint32_t st = (stm >> i) & 1u;
@@ -540,19 +540,19 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
   if constexpr (FUSED) hist_add4(hist, bin);
 }
 
-// this thread's 4 traces: relative arrivals + A_t -> absolute arrivals a, A_t
+// this thread's 4 traces: absolute arrivals a = A_t + relative arrival, and
+// the relative arrivals' row values r (S relative = wait + r + off)
 template <typename T>
 __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint64_t off, uint64_t base,
-                                              uint64_t N, uint64_t (&a)[kPer], uint64_t (&At)[kPer]) {
-  load4a(k.A, base, N, At);
+                                              uint64_t N, uint64_t (&a)[kPer], T (&r)[kPer]) {
+  load4a(k.A, base, N, a);
   if (par) {
-    uint64_t r[kPer];
-    load4n<T>(par, base, N, r);
+    load4t<T>(par, base, N, r);
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] = At[i] + r[i] + off;
+    for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)r[i] + off;
   } else {
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] = At[i];
+    for (uint32_t i = 0; i < kPer; ++i) r[i] = 0;
   }
 }
 
@@ -580,8 +580,9 @@ __global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
   bool bad = false;
   for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
     const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
-    uint64_t a[kPer], At[kPer], o[kPer] = {0, 0, 0, 0};
-    load_arrivals<T>(k, par, off, base, N, a, At);
+    uint64_t a[kPer], o[kPer] = {0, 0, 0, 0};
+    T ar[kPer];
+    load_arrivals<T>(k, par, off, base, N, a, ar);
     uint32_t rr[kPer];
     const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;  // fused leaves: own error statuses, bit i
 #pragma unroll
@@ -607,7 +608,7 @@ __global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
       const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
       const uint64_t cin = carry[r];
       const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-      queue_finish<T, FUSED>(k, P, base, N, x, a, At, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+      queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
       __syncthreads();  // every thread has read carry[r]
       if (threadIdx.x == kDownThreads - 1) {
         uint64_t xe = x;
@@ -675,8 +676,9 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   T *out = row<T>(k.W, k.ld, v);
   ChainState *cs = k.chain + (uint64_t)v * k.n_chunks;
   const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
-  uint64_t a[kPer], At[kPer];
-  load_arrivals<T>(k, par, off, base, N, a, At);
+  uint64_t a[kPer];
+  T ar[kPer];
+  load_arrivals<T>(k, par, off, base, N, a, ar);
   const uint32_t stm = FUSED && base < N ? des_status4(k, v, base) : 0u;
   MaxPlus f{0, 0};
   uint32_t mask = 0;
@@ -752,7 +754,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   uint64_t o[kPer] = {0, 0, 0, 0};
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
-  queue_finish<T, FUSED>(k, P, base, N, x, a, At, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+  queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
   store4n<T>(out, base, N, o);
   flag_overflow(k, bad);
   des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
