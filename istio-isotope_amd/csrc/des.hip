@@ -52,6 +52,9 @@ constexpr uint32_t kDesUpThreads = 256;
 #define ISIM_DES_DOWN_THREADS 512
 #endif
 constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-position queue pass
+#ifndef ISIM_DES_DOWN_WAVES
+#define ISIM_DES_DOWN_WAVES 6  // waves per SIMD the one-workgroup-per-position pass is compiled for
+#endif
 
 __constant__ int32_t c_ln[257] = {
 #include "des_ln_table.inc"
@@ -201,6 +204,21 @@ __device__ __forceinline__ void load4n(const T *p, uint64_t base, uint64_t n, ui
   } else {
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) x[i] = base + i < n ? (uint64_t)p[base + i] : 0;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4t(T *p, uint64_t base, uint64_t n, const T (&x)[kPer]) {
+  if (base + kPer <= n) {
+    if constexpr (sizeof(T) == 4) {
+      *reinterpret_cast<uint4 *>(p + base) = make_uint4(x[0], x[1], x[2], x[3]);
+    } else {
+      reinterpret_cast<ulonglong2 *>(p + base)[0] = make_ulonglong2(x[0], x[1]);
+      reinterpret_cast<ulonglong2 *>(p + base)[1] = make_ulonglong2(x[2], x[3]);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i)
+      if (base + i < n) p[base + i] = x[i];
   }
 }
 template <typename T>
@@ -507,7 +525,7 @@ __device__ __forceinline__ void des_flush_waits(const DesK &k, uint32_t trow_idx
 template <typename T, bool FUSED>
 __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uint64_t base, uint64_t N,
                                              uint64_t x, const uint64_t (&a)[kPer], const T (&r)[kPer],
-                                             uint64_t off, uint32_t mask, uint32_t stm, uint64_t (&out)[kPer], uint32_t *hist,
+                                             uint64_t off, uint32_t mask, uint32_t stm, T (&out)[kPer], uint32_t *hist,
                                              uint64_t &wsum, uint64_t &wmax, uint64_t &d0, uint64_t &d1,
                                              uint64_t &n5, bool &bad) {
   uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
@@ -534,7 +552,7 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
       } else {
         bad |= !Row<T>::fits(val);
       }
-      out[i] = val;
+      out[i] = (T)val;
     }
   }
   if constexpr (FUSED) hist_add4(hist, bin);
@@ -559,7 +577,7 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 // ---- queue pass, one workgroup per position (wide groups; replicated
 // services: per-replica scans, the routing draw per trace)
 template <typename T, bool MULTI, bool FUSED>
-__global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
+__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(DesK k) {
   __shared__ MaxPlus wtot[kDownThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
   __shared__ uint64_t red[3 * kDownThreads / 64];
@@ -580,7 +598,8 @@ __global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
   bool bad = false;
   for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
     const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
-    uint64_t a[kPer], o[kPer] = {0, 0, 0, 0};
+    uint64_t a[kPer];
+    T o[kPer] = {0, 0, 0, 0};
     T ar[kPer];
     load_arrivals<T>(k, par, off, base, N, a, ar);
     uint32_t rr[kPer];
@@ -619,7 +638,7 @@ __global__ void __launch_bounds__(kDownThreads, 8) des_down(DesK k) {
       }
       __syncthreads();
     }
-    store4n<T>(out, base, N, o);
+    store4t<T>(out, base, N, o);
   }
   flag_overflow(k, bad);
   des_flush_waits<kDownThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
@@ -751,11 +770,11 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
   const uint64_t cin = s_carry;
   const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-  uint64_t o[kPer] = {0, 0, 0, 0};
+  T o[kPer] = {0, 0, 0, 0};
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
   queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
-  store4n<T>(out, base, N, o);
+  store4t<T>(out, base, N, o);
   flag_overflow(k, bad);
   des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
   if constexpr (FUSED) {
