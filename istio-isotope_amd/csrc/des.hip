@@ -65,17 +65,20 @@ __device__ __forceinline__ uint32_t des_xor3(uint32_t a, uint32_t b, uint32_t c)
 }
 
 // Philox4x32-10 (Random123), counter (t_lo, t_hi, w2, w3), key (k0, k1)
+__device__ __forceinline__ void des_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+  const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+  const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+  const uint32_t n0 = des_xor3((uint32_t)(p1 >> 32), c[1], k0);
+  const uint32_t n2 = des_xor3((uint32_t)(p0 >> 32), c[3], k1);
+  c[0] = n0;
+  c[1] = (uint32_t)p1;
+  c[2] = n2;
+  c[3] = (uint32_t)p0;
+}
 __device__ __forceinline__ void des_philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = des_xor3((uint32_t)(p1 >> 32), c[1], k0);
-    const uint32_t n2 = des_xor3((uint32_t)(p0 >> 32), c[3], k1);
-    c[0] = n0;
-    c[1] = (uint32_t)p1;
-    c[2] = n2;
-    c[3] = (uint32_t)p0;
+    des_round(c, k0, k1);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
@@ -435,17 +438,39 @@ __global__ void __launch_bounds__(256) des_status(DesK k) {
   }
   uint32_t bits[4] = {0, 0, 0, 0};
   const uint32_t any = thr[0] | thr[1] | thr[2] | thr[3];
-  for (uint32_t b = 0; b < 32; ++b) {
-    const uint64_t t = w * 32 + b;
-    if (t >= k.N) break;
-    if (any) {
-      uint32_t c[4] = {(uint32_t)(k.trace_begin + t), (uint32_t)((k.trace_begin + t) >> 32), (uint32_t)g, 0u};
-      des_philox(c, k.k0, k.k1);
+  auto put = [&](const uint32_t (&c)[4], uint32_t b) {
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) bits[j] |= (uint32_t)(always[j] || (thr[j] && c[j] < thr[j])) << b;
-    } else {
+    for (uint32_t j = 0; j < 4; ++j) bits[j] |= (uint32_t)(always[j] || (thr[j] && c[j] < thr[j])) << b;
+  };
+  if (any && w * 32 + 32 <= k.N) {
+    // two independent Philox chains per step (ILP)
+    for (uint32_t b = 0; b < 16; ++b) {
+      const uint64_t t0 = k.trace_begin + w * 32 + b, t1 = t0 + 16;
+      uint32_t c0[4] = {(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)g, 0u};
+      uint32_t c1[4] = {(uint32_t)t1, (uint32_t)(t1 >> 32), (uint32_t)g, 0u};
+      uint32_t k0 = k.k0, k1 = k.k1;
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) bits[j] |= always[j] << b;
+      for (int r = 0; r < 10; ++r) {
+        des_round(c0, k0, k1);
+        des_round(c1, k0, k1);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+      }
+      put(c0, b);
+      put(c1, b + 16);
+    }
+  } else {
+    for (uint32_t b = 0; b < 32; ++b) {
+      const uint64_t t = w * 32 + b;
+      if (t >= k.N) break;
+      if (any) {
+        uint32_t c[4] = {(uint32_t)(k.trace_begin + t), (uint32_t)((k.trace_begin + t) >> 32), (uint32_t)g, 0u};
+        des_philox(c, k.k0, k.k1);
+        put(c, b);
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) bits[j] |= always[j] << b;
+      }
     }
   }
 #pragma unroll
