@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -551,6 +552,14 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   const isim::DesPlan &d = h->des;
   if (n_traces * (uint64_t)std::max<uint32_t>(1, d.max_sort_pos) > 0xFFFFFFFFull)
     return fail(ISIM_EINVAL, "n_traces x positions of one service above 2^32 per DES batch");
+  if (d.max_rep_bits) {
+    // sort keys hold replica | arrival: the batch's arrival span (an exponential
+    // gap is at most 24 ln 2 = 16.6 means) plus the static latency must fit
+    const long double span = (long double)n_traces * dp->mean_interarrival_ns * 17.0L +
+                             (long double)h->prog.max_latency;
+    if (span >= std::ldexp(1.0L, 64 - (int)d.max_rep_bits - 1))
+      return fail(ISIM_EINVAL, "DES batch too long for the sort keys of a replicated service (arrival span)");
+  }
   const uint64_t words = stats_words(h);
   const uint32_t rows = (uint32_t)h->prog.row_svc.size();
   if (!d_workspace || workspace_bytes < isim::des_workspace_bytes(d, n_traces, words, rows))

@@ -93,6 +93,7 @@ struct DesPlan {
   std::vector<uint32_t> fin_pos, fin_off;        // finish groups (one depth each), deepest first
   std::vector<uint32_t> fin_round_off;           // [rounds + 1] into the finish groups
   uint32_t max_sort_pos = 0;         // most positions of one sort-path service
+  uint32_t max_rep_bits = 0;         // sort keys: bits of the largest replica index of a sort-path service
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 

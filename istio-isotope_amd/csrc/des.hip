@@ -48,6 +48,11 @@ constexpr uint32_t kDownChunk = kPer * kDesThreads;    // traces per down-pass c
 #define ISIM_DES_CHAIN_BELOW 256  // positions per launch below which the chained scan is used
 #endif
 constexpr uint32_t kDesUpThreads = 256;
+
+// sort keys of a service with `reps` replicas: replica << shift | arrival,
+// shift = 64 - bits(reps - 1) (arrivals below 2^shift ns: >= 2^48 ns for up
+// to 65536 replicas; the host checks the batch's arrival span)
+__device__ __forceinline__ uint32_t rep_bits(uint32_t reps) { return reps > 1 ? 32u - __builtin_clz(reps - 1u) : 0u; }
 #ifndef ISIM_DES_DOWN_THREADS
 #define ISIM_DES_DOWN_THREADS 512
 #endif
@@ -989,8 +994,9 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
 }
 
 // ---- sort path: arrivals of all positions of one service,
-// item i = t * P + j (j = the position's rank in hop order), keyed by the
-// absolute arrival, so a stable sort leaves ties in (t, hop) order
+// item i = t * P + j (j = the position's rank in hop order), keyed by
+// (replica | absolute arrival), so a stable sort groups each replica's
+// queue contiguously with ties in (t, hop) order
 template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
   const uint32_t P = k.svc.pos_cnt;
@@ -999,72 +1005,123 @@ __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
        i += (uint64_t)gridDim.x * kDesUpThreads) {
     const uint64_t t = i / P;
     const uint32_t v = k.sort_pos[k.svc.pos_off + (uint32_t)(i - t * P)];
-    k.keys[i] = k.A[t] + des_arrival<T>(k, v, k.pos[v], t);
+    const uint64_t a = k.A[t] + des_arrival<T>(k, v, k.pos[v], t);
+    const uint32_t rb = rep_bits(k.svc.reps);
+    uint64_t key = a;
+    if (rb) {
+      const uint64_t r = des_draw(k.trace_begin + t, v, 0x80000002u, 0, k.k0, k.k1) % k.svc.reps;
+      key = r << (64 - rb) | a;
+      if (a >> (64 - rb)) atomicOr(k.ovf, 1u);  // never within the host's arrival-span check
+    }
+    k.keys[i] = key;
     k.vals[i] = (uint32_t)i;
   }
 }
 
-// FIFO scan of one sort-path service over its sorted arrivals (one workgroup)
+// FIFO scan of one sort-path service over its sorted arrivals (one
+// workgroup): the replicas' queues are contiguous segments, scanned as one
+// SEGMENTED max-plus scan (a segment starts with an idle worker, x = 0)
+struct SegMP {
+  uint64_t B, C;
+  uint32_t f;  // the span contains a segment start: its input is replaced by 0
+};
+__device__ __forceinline__ SegMP smp_then(SegMP first, SegMP second) {
+  if (second.f) return second;
+  const MaxPlus m = mp_then(MaxPlus{first.B, first.C}, MaxPlus{second.B, second.C});
+  return {m.B, m.C, first.f};
+}
+__device__ __forceinline__ uint64_t smp_apply(SegMP m, uint64_t x) {
+  const uint64_t xi = m.f ? 0 : x;
+  return xi + m.B > m.C ? xi + m.B : m.C;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
-  __shared__ MaxPlus wtot[kDesThreads / 64];
-  __shared__ uint64_t carry[kDesMaxReplicas];
+  __shared__ SegMP wtot[kDesThreads / 64];
   __shared__ uint64_t red[2 * kDesThreads / 64];
-  __shared__ MaxPlus xs[kDesThreads];
+  __shared__ SegMP xs[kDesThreads];
+  __shared__ uint64_t s_carry;
   const DesSortSvc sv = k.svc;
-  const uint32_t P = sv.pos_cnt, reps = sv.reps;
+  const uint32_t P = sv.pos_cnt;
   const uint64_t M = k.N * P;
-  if (threadIdx.x < reps) carry[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_carry = 0;
   __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t rb = rep_bits(sv.reps), shift = 64 - rb;
+  const uint64_t amask = rb ? (1ull << shift) - 1 : ~0ull;
   uint64_t wsum = 0, wmax = 0;
   bool bad = false;
   for (uint64_t c0 = 0; c0 < M; c0 += kDownChunk) {
     const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
     uint64_t a[kPer], tt[kPer];
-    uint32_t vv[kPer], rr[kPer];
+    uint32_t vv[kPer], st[kPer];
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
       const uint64_t q = base + i;
       a[i] = 0;
       tt[i] = 0;
       vv[i] = 0;
-      rr[i] = 0;
+      st[i] = 0;
       if (q < M) {
-        a[i] = k.skeys[q];
+        const uint64_t key = k.skeys[q];
+        a[i] = key & amask;
+        st[i] = q == 0 || (rb && (k.skeys[q - 1] >> shift) != (key >> shift));  // a replica's first item
         const uint32_t idx = k.svals[q];
         tt[i] = idx / P;
         vv[i] = k.sort_pos[sv.pos_off + (idx - (uint32_t)tt[i] * P)];
-        if (reps > 1) rr[i] = des_draw(k.trace_begin + tt[i], vv[i], 0x80000002u, 0, k.k0, k.k1) % reps;
       }
     }
-    for (uint32_t r = 0; r < reps; ++r) {
-      MaxPlus f{0, 0};
+    SegMP f{0, 0, 0};
 #pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i)
-        if (base + i < M && rr[i] == r) f = mp_then(f, MaxPlus{sv.hold, a[i] + sv.hold});
-      const MaxPlus inc = mp_block_scan(f, wtot);
-      xs[threadIdx.x] = inc;
-      __syncthreads();
-      const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
-      const uint64_t cin = carry[r];
-      uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+    for (uint32_t i = 0; i < kPer; ++i)
+      if (base + i < M) f = smp_then(f, SegMP{sv.hold, a[i] + sv.hold, st[i]});
+    // inclusive block scan of the segmented maps
+    SegMP v = f;
 #pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) {
-        if (base + i < M && rr[i] == r) {
-          const uint64_t S = x > a[i] ? x : a[i];
-          const uint64_t rel = S - k.A[tt[i]];
-          bad |= !Row<T>::fits(rel);
-          row<T>(k.W, k.ld, vv[i])[tt[i]] = (T)rel;
-          const uint64_t w = S - a[i];
-          wsum += w;
-          wmax = w > wmax ? w : wmax;
-          x = S + sv.hold;
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == kDesThreads - 1) carry[r] = x;
-      __syncthreads();
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      SegMP o;
+      o.B = __shfl_up(v.B, d, 64);
+      o.C = __shfl_up(v.C, d, 64);
+      o.f = __shfl_up(v.f, d, 64);
+      if (lane >= d) v = smp_then(o, v);
     }
+    if (lane == 63) wtot[wave] = v;
+    __syncthreads();
+    if (wave == 0) {
+      SegMP w = lane < kDesThreads / 64 ? wtot[lane] : SegMP{0, 0, 0};
+#pragma unroll
+      for (uint32_t d = 1; d < kDesThreads / 64; d <<= 1) {
+        SegMP o;
+        o.B = __shfl_up(w.B, d, 64);
+        o.C = __shfl_up(w.C, d, 64);
+        o.f = __shfl_up(w.f, d, 64);
+        if (lane >= d) w = smp_then(o, w);
+      }
+      if (lane < kDesThreads / 64) wtot[lane] = w;
+    }
+    __syncthreads();
+    if (wave > 0) v = smp_then(wtot[wave - 1], v);
+    xs[threadIdx.x] = v;
+    __syncthreads();
+    const SegMP pre = threadIdx.x ? xs[threadIdx.x - 1] : SegMP{0, 0, 0};
+    uint64_t x = smp_apply(pre, s_carry);
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      if (base + i < M) {
+        if (st[i]) x = 0;  // the replica's worker is idle before its first invocation
+        const uint64_t S = x > a[i] ? x : a[i];
+        const uint64_t rel = S - k.A[tt[i]];
+        bad |= !Row<T>::fits(rel);
+        row<T>(k.W, k.ld, vv[i])[tt[i]] = (T)rel;
+        const uint64_t w = S - a[i];
+        wsum += w;
+        wmax = w > wmax ? w : wmax;
+        x = S + sv.hold;
+      }
+    }
+    __syncthreads();  // every thread has read s_carry
+    if (threadIdx.x == kDesThreads - 1) s_carry = smp_apply(xs[kDesThreads - 1], s_carry);
+    __syncthreads();
   }
   flag_overflow(k, bad);
   des_flush_waits<kDesThreads>(k, sv.row, wsum, wmax, M, M * sv.hold, red);

@@ -93,10 +93,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (!shaped[svc]) {
       shape[svc] = shape_of(g.services[svc]);
       shaped[svc] = 1;
-      // a zero-hold service never makes an invocation wait (start = arrival):
-      // its replicas do not matter
-      if (shape[svc].hold > 0 && std::max<int32_t>(1, g.services[svc].num_replicas) > (int32_t)kDesMaxReplicas) {
-        err = "service \"" + g.services[svc].name + "\" has more than 64 replicas (DES limit)";
+      if (std::max<int32_t>(1, g.services[svc].num_replicas) > 65536) {
+        err = "service \"" + g.services[svc].name + "\" has more than 65536 replicas (DES limit)";
         return ISIM_EINVAL;
       }
     }
@@ -252,7 +250,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     if (zero(v)) zpos[rnd[Q(v)]].push_back(v);
   for (int32_t s = 0; s < n; ++s) {
     if (svc_pos[s].empty() || shape[s].hold == 0) continue;
-    bool need = svc_pos[s].size() > 1;
+    // the one-workgroup-per-position pass keeps per-replica carries in LDS
+    // (<= kDesMaxReplicas); more replicas: the sort path's segmented scan
+    bool need = svc_pos[s].size() > 1 || std::max<int32_t>(1, g.services[s].num_replicas) > (int32_t)kDesMaxReplicas;
     for (uint32_t v : svc_pos[s]) need = need || !arr_sorted[v];
     if (need) {
       srt[rnd[s]].push_back(s);
@@ -301,6 +301,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       ss.hold = shape[s].hold;
       out.sort_pos.insert(out.sort_pos.end(), svc_pos[s].begin(), svc_pos[s].end());
       out.max_sort_pos = std::max(out.max_sort_pos, ss.pos_cnt);
+      uint32_t rb = 0;
+      while (ss.reps > 1 && ((ss.reps - 1) >> rb) != 0) ++rb;
+      out.max_rep_bits = std::max(out.max_rep_bits, rb);
       out.sorted.push_back(ss);
     }
     out.sorted_off[r + 1] = (uint32_t)out.sorted.size();

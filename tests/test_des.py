@@ -105,7 +105,9 @@ def test_des_class():
     doc["services"][-1]["numReplicas"] = 65
     isim.DesHandler(_handler(doc), 1_000_000)  # no sleeps: never queues, replicas do not matter
     doc["services"][-1]["script"] = [{"sleep": "1ms"}]
-    _rejects(_handler(doc), "more than 64 replicas")
+    isim.DesHandler(_handler(doc), 1_000_000)  # > 64 replicas: the sort path's segmented scan
+    doc["services"][-1]["numReplicas"] = 70000
+    _rejects(_handler(doc), "more than 65536 replicas")
     d = isim.DesHandler(_handler(realistic_topology(200, concurrent=True, sleep_ms=(1, 5))), 5_000_000)
     assert (d.info.n_positions, d.info.table_rows) == (200, 200)
     assert d.info.n_levels >= 2 and d.info.max_width >= 1

@@ -292,3 +292,19 @@ def test_canonical_zero_hold_cycle_with_queues(gpu, mean):
             s["script"] = [{"sleep": "300us"}] + s.get("script", [])
     doc["services"][0]["numReplicas"] = 2
     DesCase(doc, mean).compare(0, 6000)
+
+
+# ---- replicated services on the sort path: one segmented scan over the
+# replicas' queues (any replica count)
+
+@pytest.mark.parametrize("reps", [65, 300])
+def test_many_replicas_with_holds(gpu, reps):
+    doc = _sleepy_tree(3, 3)
+    doc["services"][2]["numReplicas"] = reps  # a middle service
+    doc["services"][-1]["numReplicas"] = reps  # a leaf
+    DesCase(doc, 30_000).compare(0, 9000)
+
+
+def test_replicated_dag_segmented(gpu):
+    # several positions per service and replicas: sort path, segmented by replica
+    DesCase(_dag(levels=4, width=4, fan=2, reps=7), 120_000).compare(3, 8000)
