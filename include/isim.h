@@ -236,8 +236,8 @@ ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *st
  * call counters are those of the static walk; latencies and the per-service
  * durations include queueing.  Exact (bit-identical to the sequential
  * event-driven oracle) for the DES graph class of DESIGN.md §10.1: static
- * walks of at most 2^24 invocations and 64 replicas per service whose
- * call-step schedule is acyclic (isim_des_info_get returns ISIM_EINVAL with
+ * walks of at most 2^24 invocations and 65536 replicas per service whose
+ * call-step schedule is acyclic for services with sleeps (isim_des_info_get returns ISIM_EINVAL with
  * the reason otherwise).  Times are kept per trace relative to its arrival:
  * in 32-bit rows by default; a batch with a latency of 2^31 ns (2.1 s) or
  * more is then not accumulated (ISIM_ST_DES_RETRY counts it) and must be
