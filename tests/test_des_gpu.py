@@ -308,3 +308,54 @@ def test_many_replicas_with_holds(gpu, reps):
 def test_replicated_dag_segmented(gpu):
     # several positions per service and replicas: sort path, segmented by replica
     DesCase(_dag(levels=4, width=4, fan=2, reps=7), 120_000).compare(3, 8000)
+
+
+# ---- random graphs: every DES feature at once (call steps after call
+# steps, concurrent sleeps, replicas up to 70, zero-hold services, shared
+# callees), against the event-driven oracle
+
+def _random_graph(seed):
+    import random
+    rnd = random.Random(seed)
+    layers = [rnd.randint(1, 3) for _ in range(rnd.randint(2, 4))]
+    layers[0] = 1
+    names = [[f"s{l}_{j}" for j in range(w)] for l, w in enumerate(layers)]
+    svcs = []
+    for l, row in enumerate(names):
+        for name in row:
+            script = []
+            if rnd.random() < 0.7:
+                script.append({"sleep": f"{rnd.randint(0, 400)}us"})
+            if l + 1 < len(names):
+                callees = rnd.sample(names[l + 1], rnd.randint(1, len(names[l + 1])))
+                while callees:
+                    take = callees[:rnd.randint(1, len(callees))]
+                    callees = callees[len(take):]
+                    step = [{"call": c} for c in take]
+                    if rnd.random() < 0.4:
+                        step.append({"sleep": f"{rnd.randint(1, 200)}us"})
+                    script.append(step if len(step) > 1 or rnd.random() < 0.5 else step[0])
+                    if rnd.random() < 0.4:
+                        script.append({"sleep": f"{rnd.randint(1, 150)}us"})
+            if rnd.random() < 0.25:  # a zero-hold service
+                script = [c for c in script if not (isinstance(c, dict) and "sleep" in c)]
+                script = [[x for x in c if "sleep" not in x] if isinstance(c, list) else c for c in script]
+                script = [c for c in script if c != []]
+            reps = rnd.choice([1, 1, 1, 2, 3, 5, 70])
+            svcs.append({"name": name, "script": script, "numReplicas": reps,
+                         "errorRate": rnd.choice([0, 0.01, 0.05, 0.3])})
+    svcs[0]["isEntrypoint"] = True
+    return {"services": svcs}
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_graphs(gpu, seed):
+    doc = _random_graph(seed)
+    mode = isim.MODE_B if seed % 3 == 0 else isim.MODE_A
+    mean = [60_000, 300_000, 2_000_000][seed % 3]
+    try:
+        c = DesCase(doc, mean, error_mode=mode)
+    except isim.IsimError as e:  # outside the class: a dynamic walk or a cyclic schedule with holds
+        assert e.code == isim.native.EINVAL
+        pytest.skip(str(e)[:80])
+    c.compare(seed, 3000)
