@@ -101,8 +101,9 @@ typedef struct {
 #define ISIM_ST_N_500 4
 #define ISIM_ST_NOT_MIN_LATENCY 5 /* ~min latency (so min and max both merge with MAX) */
 #define ISIM_ST_MAX_LATENCY 6
-#define ISIM_ST_DES_RETRY 7       /* DES batches NOT accumulated: a latency reached 2^31 ns in 32-bit rows;
-                                     rerun them with ISIM_DES_FLAG_WIDE (isim_serve_des does) */
+#define ISIM_ST_DES_RETRY 7       /* DES batches NOT accumulated: a latency reached 2^31 ns in 32-bit rows
+                                     (rerun them with ISIM_DES_FLAG_WIDE; isim_serve_des does), or a cyclic
+                                     schedule found no fixed point within 256 passes */
 #define ISIM_ST_PROM 8            /* [2][33] latency histogram, Prometheus duration buckets
                                      (prometheus/handler.go:26-31), index [status500][bucket] */
 #define ISIM_N_PROM 33
@@ -236,12 +237,15 @@ ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *st
  * call counters are those of the static walk; latencies and the per-service
  * durations include queueing.  Exact (bit-identical to the sequential
  * event-driven oracle) for the DES graph class of DESIGN.md §10.1: static
- * walks of at most 2^24 invocations and 65536 replicas per service whose
- * call-step schedule is acyclic for services with sleeps (isim_des_info_get returns ISIM_EINVAL with
- * the reason otherwise).  Times are kept per trace relative to its arrival:
- * in 32-bit rows by default; a batch with a latency of 2^31 ns (2.1 s) or
- * more is then not accumulated (ISIM_ST_DES_RETRY counts it) and must be
- * rerun with ISIM_DES_FLAG_WIDE (64-bit rows). */
+ * walks of at most 2^24 invocations and 65536 replicas per service
+ * (isim_des_info_get returns ISIM_EINVAL with the reason otherwise).  Times
+ * are kept per trace relative to its arrival: in 32-bit rows by default;
+ * a batch with a latency of 2^31 ns (2.1 s) or more is then not accumulated
+ * (ISIM_ST_DES_RETRY counts it) and must be rerun with ISIM_DES_FLAG_WIDE
+ * (64-bit rows).  A graph whose call-step
+ * schedule is cyclic (a service with sleeps invoked both inside a caller's
+ * call step and after it) runs as passes to a fixed point; its batches
+ * synchronize hip_stream once per pass. */
 #define ISIM_DES_FLAG_WIDE 1u    /* 64-bit rows: any latency */
 typedef struct {
   uint64_t mean_interarrival_ns; /* 1 .. 2^34: mean gap of the exponential arrivals */

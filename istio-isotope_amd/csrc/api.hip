@@ -629,7 +629,7 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
         break;
       }
       rc = isim_serve_des_device(h, &p, trace_begin, n_traces, d_rec, d_stats, d_tab, d_ws, ws_bytes + 8, s);
-      if (rc != ISIM_OK || (p.flags & ISIM_DES_FLAG_WIDE)) break;
+      if (rc != ISIM_OK) break;
       uint64_t retry = 0;
       if (hipMemcpyAsync(&retry, d_stats + ISIM_ST_DES_RETRY, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
           hipStreamSynchronize(s) != hipSuccess) {
@@ -637,6 +637,11 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
         break;
       }
       if (!retry) break;
+      if (p.flags & ISIM_DES_FLAG_WIDE) {
+        rc = fail(ISIM_EINVAL, "DES batch not accumulated with 64-bit rows: the cyclic schedule found no fixed point "
+                               "within 256 passes (or arrivals beyond the sort keys)");
+        break;
+      }
       p.flags |= ISIM_DES_FLAG_WIDE;
     }
     if (rc != ISIM_OK) break;

@@ -80,6 +80,7 @@ struct DesPlan {
   std::vector<uint32_t> slot_mult;   // per slot: calls through it per trace
   uint32_t n_levels = 0, max_width = 0;  // invocation-tree depth, widest depth
   bool general = false;              // some script has several call steps
+  bool cyclic = false;               // the schedule runs as passes to a fixed point (back edges cut)
   // the schedule: rounds of (step begins, queues, finishes)
   std::vector<uint32_t> arr_ops, arr_off;        // BK rows computed in round r
   std::vector<uint32_t> fast_pos, fast_off;      // single-position trace-ordered services
@@ -104,7 +105,7 @@ struct DesLaunch {
   const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops, *d_zero_pos;
   const uint32_t *d_mult;            // per slot: calls per trace (executed-call counters)
   // workspace parts (des_carve)
-  void *W, *BK;                      // rows [n_pos][ld], [steps][ld] of u32 (narrow) or u64
+  void *W, *WF, *BK;                 // rows [n_pos][ld] (starts, finishes), [steps][ld] of u32 or u64
   uint64_t *A, *blk;                 // [N] arrival times, chunk sums
   uint32_t *E;                       // [N] per-trace 500 count
   void *chain;                       // chained-scan states of the down pass (des_chain_bytes)

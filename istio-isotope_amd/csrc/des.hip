@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -133,14 +135,18 @@ struct DesK {
   const uint32_t *level_pos;  // the positions of the launch (fast queue or finish group)
   const uint32_t *arr_ops;    // BK rows of the launch (step begins)
   void *BK;                   // [steps][ld] row type T
-  void *W;                    // [n_pos][ld] row type T
+  void *W;                    // [n_pos][ld] row type T: starts S
+  void *WF;                   // [n_pos][ld] row type T: finishes F | status (separate rows, so a
+                              // fixed-point pass reads last pass's F while S is being rewritten)
   uint64_t *A;                // [N] absolute arrival times
   uint32_t *E;                // [N] per-trace 500 count
   uint64_t *blk;
   uint64_t *stats;            // narrow rows: the staging copy (des_commit)
   uint64_t *table;            // [rows][ISIM_DES_ROW_WORDS] (staged likewise)
   isim_trace_rec *records;
-  uint32_t *ovf;              // narrow rows: a value reached 2^31
+  uint32_t *ovf;              // bit 0: a 32-bit row value reached 2^31; bit 1: no fixed point
+  uint32_t *changed;          // fixed-point passes: set when a stored row value changes (null: no tracking)
+  uint32_t quiet;             // fixed-point passes before the last: no statistics
   const uint32_t *stbits;     // own error status of (position, trace): bit t%32 of word [v][t/32]
   uint32_t st_wpr;            // words per status row
   uint64_t N, trace_begin, mean_ns;
@@ -262,6 +268,24 @@ __device__ __forceinline__ void load4t(const T *p, uint64_t base, uint64_t n, T 
     for (uint32_t i = 0; i < kPer; ++i) x[i] = base + i < n ? p[base + i] : (T)0;
   }
 }
+__device__ __forceinline__ void load4a(const uint64_t *p, uint64_t base, uint64_t n, uint64_t (&x)[kPer]);
+
+// stores of row values; in fixed-point passes a changed value is flagged
+template <typename T>
+__device__ __forceinline__ void track4(const DesK &k, const T *p, uint64_t base, uint64_t n, const T (&x)[kPer]) {
+  if (!k.changed) return;
+  T o[kPer];
+  load4t<T>(p, base, n, o);
+  bool d = false;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) d |= base + i < n && o[i] != x[i];
+  if (d) atomicOr(k.changed, 1u);
+}
+template <typename T>
+__device__ __forceinline__ void track1(const DesK &k, const T *p, T x) {
+  if (k.changed && *p != x) atomicOr(k.changed, 1u);
+}
+
 __device__ __forceinline__ void load4a(const uint64_t *p, uint64_t base, uint64_t n, uint64_t (&x)[kPer]) {
   load4n<uint64_t>(p, base, n, x);
 }
@@ -572,7 +596,7 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
         const uint64_t F = val + P.floor;
         const uint32_t st = (stm >> i) & 1u;
         const uint64_t dur = w + P.floor;  // F - a
-        if (st) atomicAdd(k.E + base + i, 1u);
+        if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
         n5 += st;
         d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
         d0 += st ? 0 : dur;
@@ -623,7 +647,7 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(De
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
-  T *out = row<T>(k.W, k.ld, v);
+  T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
   for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
@@ -668,9 +692,11 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(De
       }
       __syncthreads();
     }
+    if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
     store4t<T>(out, base, N, o);
   }
   flag_overflow(k, bad);
+  if (k.quiet) return;
   des_flush_waits<kDownThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
@@ -722,7 +748,7 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
-  T *out = row<T>(k.W, k.ld, v);
+  T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
   ChainState *cs = k.chain + (uint64_t)v * k.n_chunks;
   const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
   uint64_t a[kPer];
@@ -804,8 +830,10 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
   queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+  if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
   store4t<T>(out, base, N, o);
   flag_overflow(k, bad);
+  if (k.quiet) return;
   des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
   if constexpr (FUSED) {
     __syncthreads();
@@ -827,7 +855,8 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   // trace range: split boundaries on multiples of 16 (aligned vector accesses)
   const uint64_t tb = blockIdx.x ? (N * blockIdx.x / k.splits) & ~15ull : 0;
   const uint64_t te = blockIdx.x + 1 == k.splits ? N : (N * (blockIdx.x + 1) / k.splits) & ~15ull;
-  T *mine = row<T>(k.W, k.ld, v);
+  const T *mine = row<T>(k.W, k.ld, v);
+  T *fin = row<T>(k.WF, k.ld, v);
   const DesPosExt X = k.ext[v];
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
@@ -875,13 +904,13 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
       for (; c + CB <= cnt; c += CB) {
         T f[CB][kPer];
 #pragma unroll
-        for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.W, k.ld, ch[c + j]), b0, te, f[j]);
+        for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, te, f[j]);
 #pragma unroll
         for (uint32_t j = 0; j < CB; ++j) take(f[j], c + j >= c_max_from);
       }
       for (; c < cnt; ++c) {
         T f[kPer];
-        load4t<T>(row<T>(k.W, k.ld, ch[c]), b0, te, f);
+        load4t<T>(row<T>(k.WF, k.ld, ch[c]), b0, te, f);
         take(f, c >= c_max_from);
       }
 #pragma unroll
@@ -901,7 +930,7 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
         const uint64_t dur = F - a[i];
         bad |= !Row<T>::fits(F);
         o[i] = F | ((uint64_t)st << Row<T>::kTop);
-        if (st) atomicAdd(k.E + t, 1u);
+        if (st && !k.quiet) atomicAdd(k.E + t, 1u);
         n500 += st;
         dsum1 += st ? dur : 0;
         dsum0 += st ? 0 : dur;
@@ -909,9 +938,16 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
       }
     }
     hist_add4(hist, bin);
-    store4n<T>(mine, b0, te, o);
+    if (k.changed) {
+      T ot[kPer];
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) ot[i] = (T)o[i];
+      track4<T>(k, fin, b0, te, ot);
+    }
+    store4n<T>(fin, b0, te, o);
   }
   flag_overflow(k, bad);
+  if (k.quiet) return;
   des_flush_durations<kDesUpThreads>(k, P, hist, dsum0, dsum1, n500, red);
 }
 
@@ -925,8 +961,8 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   __syncthreads();
   const uint64_t N = k.N;
   // an overflowed narrow batch is dropped (des_commit): records untouched
-  const bool keep = sizeof(T) == 8 || *k.ovf == 0;
-  const T *F0 = row<T>(k.W, k.ld, 0);  // position 0: the entry
+  const bool keep = *k.ovf == 0;
+  const T *F0 = row<T>(k.WF, k.ld, 0);  // position 0: the entry
   uint64_t sl = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * kDesUpThreads + threadIdx.x; t < N;
        t += (uint64_t)gridDim.x * kDesUpThreads) {
@@ -1124,6 +1160,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
     __syncthreads();
   }
   flag_overflow(k, bad);
+  if (k.quiet) return;
   des_flush_waits<kDesThreads>(k, sv.row, wsum, wmax, M, M * sv.hold, red);
 }
 
@@ -1143,12 +1180,13 @@ __global__ void __launch_bounds__(kDesUpThreads) des_arrive(DesK k) {
     } else {
       v = (uint64_t)row<T>(k.BK, k.ld, st.prev)[t] + st.smax;
       for (uint32_t j = 0; j < st.child_cnt; ++j) {
-        const uint64_t f = row<T>(k.W, k.ld, k.child[st.child_off + j])[t] & Row<T>::kMask;
+        const uint64_t f = row<T>(k.WF, k.ld, k.child[st.child_off + j])[t] & Row<T>::kMask;
         v = f > v ? f : v;
       }
     }
     v += st.add;
     bad |= !Row<T>::fits(v);
+    track1<T>(k, out + t, (T)v);
     out[t] = (T)v;
   }
   flag_overflow(k, bad);
@@ -1172,7 +1210,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_zero(DesK k) {
     out[t] = (T)a;
   }
   flag_overflow(k, bad);
-  if (threadIdx.x == 0 && te > tb)
+  if (threadIdx.x == 0 && te > tb && !k.quiet)
     atomicAdd((unsigned long long *)(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS + ISIM_DES_COUNT),
               (unsigned long long)(te - tb));
 }
@@ -1230,7 +1268,7 @@ uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n, uint64_t stats_wor
   const uint64_t ld = row_ld(n);
   const uint64_t m = (uint64_t)plan.max_sort_pos * n;
   const uint64_t sort = m ? 2 * al256(m * 8) + 2 * al256(m * 4) + al256(sort_temp_bytes(m)) : 0;
-  return al256((uint64_t)plan.pos.size() * ld * 8) + al256((uint64_t)plan.steps.size() * ld * 8) + al256(n * 8) +
+  return 2 * al256((uint64_t)plan.pos.size() * ld * 8) + al256((uint64_t)plan.steps.size() * ld * 8) + al256(n * 8) +
          al256(n * 4) + al256((nblk + 1) * 8) + al256(des_chain_bytes(plan, n)) + 256 +
          al256((stats_words + table_rows * ISIM_DES_ROW_WORDS) * 8) +
          al256((uint64_t)plan.pos.size() * status_wpr(n) * 4) + sort;
@@ -1246,6 +1284,7 @@ void des_carve(DesLaunch &L, void *workspace) {
     return p;
   };
   L.W = take((uint64_t)plan.pos.size() * ld * 8);
+  L.WF = take((uint64_t)plan.pos.size() * ld * 8);
   L.BK = take((uint64_t)plan.steps.size() * ld * 8);
   L.A = (uint64_t *)take(n * 8);
   L.E = (uint32_t *)take(n * 4);
@@ -1337,14 +1376,14 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       hipLaunchKernelGGL(des_up<T>, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
     }
   }
-  uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
-  fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;
-  hipLaunchKernelGGL(des_finalize<T>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
   return 0;
 }
 
-// Host launcher: the whole DES of one batch on `stream` (no allocation, no
-// host synchronisation).
+// Host launcher: the whole DES of one batch on `stream` (no allocation; no
+// host synchronisation unless the schedule is cyclic: its fixed-point passes
+// read one flag per pass).
+constexpr uint32_t kMaxPasses = 256;
+
 int des_launch(const DesLaunch &L, void *stream_) {
   using namespace dev;
   hipStream_t stream = (hipStream_t)stream_;
@@ -1357,6 +1396,7 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.child = L.d_child;
   k.arr_ops = L.d_arr_ops;
   k.W = L.W;
+  k.WF = L.WF;
   k.BK = L.BK;
   k.A = L.A;
   k.E = L.E;
@@ -1364,9 +1404,10 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.ovf = L.ovf;
   k.stbits = L.stbits;
   k.st_wpr = (uint32_t)status_wpr(L.n_traces);
-  // narrow rows: statistics go to the staging copy, merged by des_commit
-  k.stats = narrow ? L.stage : L.d_stats;
-  k.table = narrow ? L.stage + L.stats_words : L.d_table;
+  // statistics go to the staging copy, merged by des_commit unless the batch
+  // is dropped (a 32-bit row overflowed, or no fixed point)
+  k.stats = L.stage;
+  k.table = L.stage + L.stats_words;
   k.records = L.d_records;
   k.N = L.n_traces;
   k.ld = row_ld(L.n_traces);
@@ -1382,12 +1423,10 @@ int des_launch(const DesLaunch &L, void *stream_) {
   const uint64_t tk_bytes = al256(chain_tickets(*L.plan) * 4);
   uint32_t *tickets = (uint32_t *)L.chain;
   k.chain = (ChainState *)((char *)L.chain + tk_bytes);
+  const uint64_t chain_bytes = des_chain_bytes(*L.plan, L.n_traces);
   if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
-  if (hipMemsetAsync(L.chain, 0, des_chain_bytes(*L.plan, L.n_traces), stream) != hipSuccess) return 1;
-  if (narrow) {
-    if (hipMemsetAsync(L.ovf, 0, 4, stream) != hipSuccess) return 1;
-    if (hipMemsetAsync(L.stage, 0, (L.stats_words + table_words) * 8, stream) != hipSuccess) return 1;
-  }
+  if (hipMemsetAsync(L.ovf, 0, 8, stream) != hipSuccess) return 1;  // overflow flag + changed flag
+  if (hipMemsetAsync(L.stage, 0, (L.stats_words + table_words) * 8, stream) != hipSuccess) return 1;
   hipLaunchKernelGGL(des_arrivals, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_scan_blocks, dim3(1), dim3(kDesThreads), 0, stream, k);
   hipLaunchKernelGGL(des_add_blocks, dim3(k.n_blk), dim3(kDesThreads), 0, stream, k);
@@ -1395,8 +1434,45 @@ int des_launch(const DesLaunch &L, void *stream_) {
     const uint64_t threads = (uint64_t)((L.n_pos + 3) / 4) * k.st_wpr;
     hipLaunchKernelGGL(des_status, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, k);
   }
-  const int rc = narrow ? des_rounds<uint32_t>(L, k, tickets, stream) : des_rounds<uint64_t>(L, k, tickets, stream);
-  if (rc) return rc;
+  auto pass = [&](const DesK &kk) -> int {
+    if (hipMemsetAsync(L.chain, 0, chain_bytes, stream) != hipSuccess) return 1;
+    return narrow ? des_rounds<uint32_t>(L, kk, tickets, stream) : des_rounds<uint64_t>(L, kk, tickets, stream);
+  };
+  if (L.plan->cyclic) {
+    // fixed point: back-edge rows start at 0 (a lower bound of every
+    // relative time); quiet passes until no stored value changes, then the
+    // pass that records the statistics
+    const uint64_t rb = narrow ? 4 : 8;
+    if (hipMemsetAsync(L.W, 0, (uint64_t)L.n_pos * k.ld * rb, stream) != hipSuccess ||
+        hipMemsetAsync(L.WF, 0, (uint64_t)L.n_pos * k.ld * rb, stream) != hipSuccess ||
+        hipMemsetAsync(L.BK, 0, (uint64_t)L.plan->steps.size() * k.ld * rb, stream) != hipSuccess)
+      return 1;
+    DesK kq = k;
+    kq.quiet = 1;
+    kq.changed = L.ovf + 1;
+    uint32_t p = 0;
+    for (; p < kMaxPasses; ++p) {
+      if (hipMemsetAsync(kq.changed, 0, 4, stream) != hipSuccess) return 1;
+      if (pass(kq)) return 1;
+      uint32_t changed = 1;
+      if (hipMemcpyAsync(&changed, kq.changed, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess)
+        return 1;
+      if (!changed) break;
+    }
+    if (std::getenv("ISIM_DES_DEBUG")) std::fprintf(stderr, "isim des: cyclic schedule, %u passes\n", p + 1);
+    if (p == kMaxPasses) {
+      static const uint32_t no_fixed_point = 2;
+      if (hipMemcpyAsync(L.ovf, &no_fixed_point, 4, hipMemcpyHostToDevice, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess)
+        return 1;
+    }
+  }
+  if (pass(k)) return 1;
+  uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
+  fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;
+  if (narrow) hipLaunchKernelGGL(des_finalize<uint32_t>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
+  else hipLaunchKernelGGL(des_finalize<uint64_t>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
   if (L.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
     uint32_t n_slots = L.n_slots;
     uint64_t n = L.n_traces;
@@ -1407,12 +1483,10 @@ int des_launch(const DesLaunch &L, void *stream_) {
         hipSuccess)
       return 1;
   }
-  if (narrow) {
-    uint64_t g = (L.stats_words + table_words + 255) / 256;
-    g = g < 1024 ? g : 1024;
-    hipLaunchKernelGGL(des_commit, dim3((uint32_t)(g ? g : 1)), dim3(256), 0, stream, L.stage, L.d_stats,
-                       L.d_table, L.stats_words, table_words, (const uint32_t *)L.ovf);
-  }
+  uint64_t g = (L.stats_words + table_words + 255) / 256;
+  g = g < 1024 ? g : 1024;
+  hipLaunchKernelGGL(des_commit, dim3((uint32_t)(g ? g : 1)), dim3(256), 0, stream, L.stage, L.d_stats, L.d_table,
+                     L.stats_words, table_words, (const uint32_t *)L.ovf);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

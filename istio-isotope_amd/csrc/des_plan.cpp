@@ -10,10 +10,12 @@
 //   3. finishes      F of positions whose start and callees are settled,
 //                    deepest first.
 // Every operation goes in the earliest round its inputs allow (longest path
-// over the dependency graph); a dependency cycle — a service with a nonzero
-// hold invoked both inside a call step and after it within one caller's
-// script — has no schedule and is rejected.  Zero-hold services (no sleeps)
-// never queue: each of their positions starts at its arrival, one op each.  Graphs whose scripts have at most one call step
+// over the dependency graph).  A dependency cycle — a service with a hold
+// invoked both inside a call step and after it within one caller's script —
+// is cut at the back edges of a depth-first search and the schedule runs as
+// repeated passes to its fixed point (des.hip).  Zero-hold services (no
+// sleeps) never queue: each of their positions starts at its arrival, one op
+// each.  Graphs whose scripts have at most one call step
 // get the shortest schedule: queues by service level, all finishes last.
 #include "des.h"
 
@@ -209,18 +211,86 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       for (uint32_t j = 0; j < st.child_cnt; ++j) pred[Ab(b)].push_back({F(out.child[st.child_off + j]), 1});
     }
   }
-  // longest path by relaxation; more passes than ops means a cycle
-  std::vector<uint32_t> rnd(n_ops, 0);
   std::vector<char> used(n_ops, 0);
   for (uint32_t v = 0; v < np; ++v) used[Q(v)] = used[F(v)] = 1;
   for (uint32_t b = 0; b < nb; ++b) used[Ab(b)] = 1;
+  // cycles (a service with a hold invoked both inside a caller's call step
+  // and after it): every cycle of the operation graph runs through an edge
+  // F(v) -> A(b) (a step begin waiting for the previous step's callees) —
+  // positions form a tree and the service graph is acyclic, so without
+  // those edges paths only go down (queues, step begins) or up among
+  // finishes.  Those edges inside a strongly connected component are cut;
+  // the schedule then runs as repeated passes to its fixed point
+  // (des_launch), the cut step begins reading the previous pass's finish
+  // rows (F rows hold their final value at the end of a pass).
+  {
+    // Tarjan's strongly connected components, iterative
+    std::vector<std::vector<uint32_t>> succ(n_ops);
+    for (uint32_t o = 0; o < n_ops; ++o)
+      for (auto &e : pred[o]) succ[e.first].push_back(o);
+    std::vector<int32_t> idx(n_ops, -1), low(n_ops, 0), comp(n_ops, -1);
+    std::vector<char> on(n_ops, 0);
+    std::vector<uint32_t> stk, comp_size;
+    std::vector<std::pair<uint32_t, uint32_t>> call;  // (op, next successor)
+    int32_t counter = 0;
+    for (uint32_t r0 = 0; r0 < n_ops; ++r0) {
+      if (!used[r0] || idx[r0] >= 0) continue;
+      call.push_back({r0, 0});
+      idx[r0] = low[r0] = counter++;
+      stk.push_back(r0);
+      on[r0] = 1;
+      while (!call.empty()) {
+        const uint32_t u = call.back().first;
+        if (call.back().second < succ[u].size()) {
+          const uint32_t w = succ[u][call.back().second++];
+          if (idx[w] < 0) {
+            idx[w] = low[w] = counter++;
+            stk.push_back(w);
+            on[w] = 1;
+            call.push_back({w, 0});
+          } else if (on[w]) {
+            low[u] = std::min(low[u], idx[w]);
+          }
+        } else {
+          call.pop_back();
+          if (!call.empty()) low[call.back().first] = std::min(low[call.back().first], low[u]);
+          if (low[u] == idx[u]) {
+            const int32_t c = (int32_t)comp_size.size();
+            uint32_t n_in = 0, w;
+            do {
+              w = stk.back();
+              stk.pop_back();
+              on[w] = 0;
+              comp[w] = c;
+              ++n_in;
+            } while (w != u);
+            comp_size.push_back(n_in);
+          }
+        }
+      }
+    }
+    auto is_f = [&](uint32_t o) { return o >= nq && o < nq + np; };
+    auto is_a = [&](uint32_t o) { return o >= nq + np && o < nq + np + nb; };
+    for (uint32_t o = 0; o < n_ops; ++o) {
+      if (!used[o] || !is_a(o) || comp_size[comp[o]] < 2) continue;
+      auto &pl = pred[o];
+      const size_t before = pl.size();
+      pl.erase(std::remove_if(pl.begin(), pl.end(),
+                              [&](const std::pair<uint32_t, uint32_t> &e) {
+                                return is_f(e.first) && comp[e.first] == comp[o];
+                              }),
+               pl.end());
+      if (pl.size() != before) out.cyclic = true;
+    }
+  }
+  // longest path by relaxation (acyclic now)
+  std::vector<uint32_t> rnd(n_ops, 0);
   bool changed = true;
   uint32_t pass = 0;
   while (changed) {
     changed = false;
     if (++pass > n_ops + 2) {
-      err = "a service is called both inside a call step and after it (through one caller's later steps); "
-            "its queue would depend on its own finish: no DES schedule";
+      err = "DES schedule: dependency cycle left after removing back edges (internal error)";
       return ISIM_EINVAL;
     }
     for (uint32_t o = 0; o < n_ops; ++o) {

@@ -355,7 +355,31 @@ def test_random_graphs(gpu, seed):
     mean = [60_000, 300_000, 2_000_000][seed % 3]
     try:
         c = DesCase(doc, mean, error_mode=mode)
-    except isim.IsimError as e:  # outside the class: a dynamic walk or a cyclic schedule with holds
-        assert e.code == isim.native.EINVAL
+    except isim.IsimError as e:  # outside the class: a dynamic walk (mode-B aborts)
+        assert e.code == isim.native.EINVAL and "static walk" in str(e)
         pytest.skip(str(e)[:80])
     c.compare(seed, 3000)
+
+
+# ---- cyclic schedules: passes to the fixed point
+
+@pytest.mark.parametrize("mean", [120_000, 400_000, 3_000_000])
+def test_canonical_with_holds(gpu, mean):
+    # b (with a sleep) is called inside d's first step (through c) and in
+    # its second: b's queue depends on its own finishes
+    doc = _fixture_doc("canonical.yaml")
+    for s in doc["services"]:
+        s["script"] = [{"sleep": "250us"}] + s.get("script", [])
+    DesCase(doc, mean).compare(0, 5000)
+
+
+def test_cyclic_mode_b_and_wide(gpu):
+    doc = _fixture_doc("canonical.yaml")
+    for s in doc["services"]:
+        s["script"] = [{"sleep": "150us"}] + s.get("script", [])
+        s["errorRate"] = 0.05
+    c = DesCase(doc, 300_000, error_mode=isim.MODE_A)
+    c.compare(7, 3000)
+    r1, s1, t1 = c.d.serve(7, 3000)
+    r2, s2, t2 = c.d.serve(7, 3000, wide=True)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(t1, t2)

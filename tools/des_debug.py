@@ -1,21 +1,22 @@
-"""Debug helper: one DES device batch, narrow rows, print the stats header."""
+"""Debug helper: DES of one random test graph (tests/test_des_gpu.py) vs the oracle."""
+import os
 import sys
 import numpy as np
-import torch
 sys.path[:0] = ["tests", "istio-isotope_amd", "."]
+os.environ["ISIM_DES_DEBUG"] = "1"
 import isim
-from test_des_gpu import DesCase, _sleepy_tree
+from test_des_gpu import DesCase, _random_graph
 
-c = DesCase(_sleepy_tree(3, 3), 900_000)
-n = 5000
-dev = torch.device("cuda", 0)
-st = torch.zeros(c.h.stats_words, dtype=torch.int64, device=dev)
-tab = torch.zeros(max(1, c.d.table_words), dtype=torch.int64, device=dev)
-wsb = c.d.workspace_bytes(n)
-ws = torch.zeros(wsb // 8 + 1, dtype=torch.int64, device=dev)
-s = torch.cuda.current_stream().cuda_stream
-c.d.serve_device(0, n, 0, st.data_ptr(), tab.data_ptr(), ws.data_ptr(), wsb, s)
-torch.cuda.synchronize()
-print("header", st[:8].tolist())
-_, s0, t0 = c.d.serve(0, n, records=False)
-print("sync header", s0[:8].tolist())
+seed = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+doc = _random_graph(seed)
+import json
+print(json.dumps(doc))
+mode = isim.MODE_B if seed % 3 == 0 else isim.MODE_A
+mean = [60_000, 300_000, 2_000_000][seed % 3]
+c = DesCase(doc, mean, error_mode=mode)
+for n in (1, 2, 10, 100, 3000):
+    try:
+        r, s, t = c.d.serve(seed, n, wide=True)
+        print(n, "ok", s[:8])
+    except Exception as e:
+        print(n, "fail", e)
