@@ -290,6 +290,8 @@ def main():
         if args.batch == 1 << 22:
             args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
         return main_des(args, h, json_text, desc, params, rank, world, dev)
+    if args.config == "c2" and args.batch == 1 << 22:
+        args.batch = 1 << 27  # BASELINE config 2: ~100M traces; a draw-free walk is a record fill (2 GiB)
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
     B = args.batch
@@ -376,8 +378,9 @@ def main():
                        launch=launch),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
-        "compute_roofline": compute_roofline(stream, info, B, kern_ms),
+                     "kernel": "isim_fill_const (draw-free walk: one trace walked, records filled)"
+                     if launch["fill"] else "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+        "compute_roofline": None if launch["fill"] else compute_roofline(stream, info, B, kern_ms),
         "occupancy": occupancy,
         "hop_visits_per_s": value * hops_per_trace,
         "n_500_frac": folded["n_500"] / total,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 4
+#define ISIM_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -85,6 +85,7 @@ typedef struct {
 /* isim_params.flags */
 #define ISIM_FLAG_NO_STREAM 1u  /* run static walks on the interpreter kernel instead of the draw stream */
 #define ISIM_FLAG_NO_SVC_DUR 2u /* dynamic walks: do not record per-service invocation durations */
+#define ISIM_FLAG_WALK_ALL 4u   /* draw-free static walks: walk every trace (default: walk one, fill the rest) */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -158,6 +159,8 @@ typedef struct {
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
   int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
                                 5 draw stream with the mode-B bit stack (call depth <= 32) */
+  int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
+                                (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
 } isim_launch_info;
 
 ISIM_API const char *isim_last_error(void);

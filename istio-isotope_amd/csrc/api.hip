@@ -41,6 +41,10 @@ struct DevState {
   uint32_t *d_mult = nullptr;  // draw stream: per-slot call multiplicity
   uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
   unsigned long long *d_work = nullptr;  // kWorkSlots sets of batch queues, zero between launches
+  // draw-free static walks (no error draw anywhere): every trace walks alike
+  bool draw_free = false;
+  uint64_t *d_const_stats = nullptr;     // the stats of one trace (computed on first use)
+  isim_trace_rec const_rec{};
   uint32_t work_next = 0;                // next queue (launches in flight use distinct queues)
   void *kernel = nullptr;
   uint32_t threads = 0;
@@ -79,6 +83,7 @@ struct isim_handler {
         (void)hipFree(kv.second.d_mult);
         (void)hipFree(kv.second.d_dur);
         (void)hipFree(kv.second.d_work);
+        (void)hipFree(kv.second.d_const_stats);
         (void)hipFree(kv.second.d_des_pos);
         (void)hipFree(kv.second.d_des_child);
         (void)hipFree(kv.second.d_des_level);
@@ -154,6 +159,10 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   // mode B on the draw stream: the per-lane bit stack holds 32 stack positions
   if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B && p.max_depth <= 32) st.kind = 5;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
+  if (st.kind >= 4) {
+    st.draw_free = true;
+    for (const isim::Node &nd : p.stream) st.draw_free = st.draw_free && nd.thr == 0;
+  }
   HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)st.lds_bytes));
   int per_cu = 0;
@@ -340,6 +349,7 @@ int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out)
   out->blocks_per_cu = (int32_t)st->per_cu;
   out->max_blocks = (int32_t)st->max_blocks;
   out->kernel_kind = (int32_t)st->kind;
+  out->fill = st->draw_free && !(h->params.flags & ISIM_FLAG_WALK_ALL) ? 1 : 0;
   return ISIM_OK;
 }
 
@@ -351,15 +361,8 @@ int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32_t *slot_
   return ISIM_OK;
 }
 
-int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, isim_trace_rec *d_records,
-                      uint64_t *d_stats, void *hip_stream) {
-  if (!h || !d_stats) return fail(ISIM_EINVAL, "null argument");
-  if (n_traces == 0) return ISIM_OK;
-  int device = 0;
-  HIPCHK(hipGetDevice(&device));
-  DevState *st = nullptr;
-  int rc = prepare_device(h, device, st);
-  if (rc != ISIM_OK) return rc;
+static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
+                       isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
   isim::KParams kp{};
   kp.trace_begin = trace_begin;
   kp.n_traces = n_traces;
@@ -391,6 +394,61 @@ int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, 
                            (hipStream_t)hip_stream));
   }
   return ISIM_OK;
+}
+
+// A draw-free static walk gives every trace the same record and statistics:
+// walk ONE trace with the stream kernel (once per device), then a batch is
+// a record fill plus n x that trace's statistics (bit-identical by
+// construction).
+static int prepare_constant(isim_handler *h, DevState *st) {
+  std::lock_guard<std::mutex> lk(h->mu);
+  if (st->d_const_stats) return ISIM_OK;
+  const uint64_t words = stats_words(h);
+  uint64_t *d_s1 = nullptr;
+  isim_trace_rec *d_r1 = nullptr;
+  hipStream_t s = nullptr;
+  int rc = ISIM_OK;
+  if (hipStreamCreate(&s) != hipSuccess || hipMalloc(&d_s1, words * 8) != hipSuccess ||
+      hipMalloc(&d_r1, sizeof(isim_trace_rec)) != hipSuccess || hipMemsetAsync(d_s1, 0, words * 8, s) != hipSuccess)
+    rc = fail(ISIM_EHIP, "constant-walk setup failed");
+  if (rc == ISIM_OK) rc = launch_walk(h, st, 0, 1, d_r1, d_s1, s);
+  if (rc == ISIM_OK && (hipMemcpyAsync(&st->const_rec, d_r1, sizeof(isim_trace_rec), hipMemcpyDeviceToHost, s) !=
+                            hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess))
+    rc = fail(ISIM_EHIP, "constant-walk setup failed");
+  (void)hipFree(d_r1);
+  if (s) (void)hipStreamDestroy(s);
+  if (rc != ISIM_OK) {
+    (void)hipFree(d_s1);
+    return rc;
+  }
+  st->d_const_stats = d_s1;
+  return ISIM_OK;
+}
+
+int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces, isim_trace_rec *d_records,
+                      uint64_t *d_stats, void *hip_stream) {
+  if (!h || !d_stats) return fail(ISIM_EINVAL, "null argument");
+  if (n_traces == 0) return ISIM_OK;
+  int device = 0;
+  HIPCHK(hipGetDevice(&device));
+  DevState *st = nullptr;
+  int rc = prepare_device(h, device, st);
+  if (rc != ISIM_OK) return rc;
+  if (st->draw_free && !(h->params.flags & ISIM_FLAG_WALK_ALL)) {
+    rc = prepare_constant(h, st);
+    if (rc != ISIM_OK) return rc;
+    const uint32_t words = (uint32_t)stats_words(h);
+    uint64_t blocks = (n_traces + 1023) / 1024;
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, 8192));
+    const isim_trace_rec r = st->const_rec;
+    const uint64_t *s1 = st->d_const_stats;
+    void *args[] = {&d_records, &n_traces, (void *)&r, &s1, &d_stats, (void *)&words};
+    HIPCHK(hipLaunchKernel(isim::fill_const_kernel(), dim3((uint32_t)blocks), dim3(256), args, 0,
+                           (hipStream_t)hip_stream));
+    return ISIM_OK;
+  }
+  return launch_walk(h, st, trace_begin, n_traces, d_records, d_stats, hip_stream);
 }
 
 int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint64_t n_traces, isim_trace_rec *h_records,

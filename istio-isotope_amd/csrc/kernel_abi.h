@@ -83,6 +83,7 @@ constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 // kind: 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream.
 void *walk_kernel(int kind, bool modeb, bool lds_counters);
 void *stream_calls_kernel();
+void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)
 uint32_t stream_traces_per_wave();
 
 }  // namespace isim

@@ -1003,6 +1003,32 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
 // Executed-call counters of a static walk: every trace makes mult[slot] calls
 // through each reachable call site, so a launch over n_traces adds
 // mult[slot] * n_traces (exact; added once per launch).
+// draw-free static walks: n copies of one trace's record, n x its statistics
+__global__ void __launch_bounds__(256) isim_fill_const(isim_trace_rec *__restrict__ rec, uint64_t n,
+                                                       isim_trace_rec r, const uint64_t *__restrict__ s1,
+                                                       uint64_t *__restrict__ gstats, uint32_t words) {
+  const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
+  if (rec) {
+    // streaming stores, 4 in flight per lane
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {(uint32_t)r.latency_ns, (uint32_t)(r.latency_ns >> 32), r.hops, r.status_err};
+    u32x4 *out = reinterpret_cast<u32x4 *>(rec);
+    uint64_t i = tid;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) __builtin_nontemporal_store(v, out + i + u * stride);
+    }
+    for (; i < n; i += stride) __builtin_nontemporal_store(v, out + i);
+  }
+  unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
+  for (uint64_t w = tid; w < words; w += stride) {
+    const uint64_t x = s1[w];
+    if (!x) continue;
+    if (w == ISIM_ST_NOT_MIN_LATENCY || w == ISIM_ST_MAX_LATENCY) atomicMax(st + w, (unsigned long long)x);
+    else atomicAdd(st + w, (unsigned long long)(x * n));
+  }
+}
+
 __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_slots, uint64_t n_traces,
                                   uint64_t *__restrict__ gstats) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1128,6 +1154,7 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters) {
 }
 
 void *stream_calls_kernel() { return (void *)&dev::isim_stream_calls; }
+void *fill_const_kernel() { return (void *)&dev::isim_fill_const; }
 uint32_t stream_traces_per_wave() { return 64u * (uint32_t)dev::kStreamTPL; }
 
 }  // namespace isim

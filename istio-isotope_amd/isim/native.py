@@ -22,9 +22,10 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 4  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 5  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
+FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
@@ -69,7 +70,8 @@ class HandlerInfo(C.Structure):
 
 class LaunchInfo(C.Structure):
     _fields_ = [("wg_threads", C.c_int32), ("lds_bytes", C.c_int32), ("lds_counters", C.c_int32),
-                ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32)]
+                ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32),
+                ("fill", C.c_int32)]
 
 
 class DesParams(C.Structure):

@@ -192,3 +192,22 @@ def test_batch_queue_rearms(gpu, kernel):
     assert fk["n_traces"] == k * n and f1["n_traces"] == n
     assert fk["sum_latency"] == k * f1["sum_latency"] and fk["n_500"] == k * f1["n_500"]
     assert np.array_equal(fk["site_calls"], k * f1["site_calls"])
+
+
+# ---- draw-free static walks: one walk, then a record fill + n x statistics
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+@pytest.mark.parametrize("n", [1, 1000, 1 << 20])
+def test_draw_free_fill(gpu, mode, n):
+    doc = config2_topology()
+    for i, s in enumerate(doc["services"]):
+        s["errorRate"] = 1 if i % 7 == 3 else 0  # deterministic 500s: statuses and error counts
+    j = json.dumps(doc)
+    fill = Case(j, None, isim.SimParams(error_mode=mode))
+    walk = isim.Handler(isim.ServiceGraph.from_json(j), None,
+                        isim.SimParams(error_mode=mode, flags=isim.native.FLAG_WALK_ALL))
+    r1, s1 = fill.gpu(3, n)
+    r2, s2 = walk.serve(3, n)
+    assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
+    if n <= 1000:
+        fill.compare(3, n)
