@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
+                    "fill the records (the library default) instead of walking every trace")
     ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
                     "64-bit only when a batch's latencies reach 2^31 ns)")
     ap.add_argument("--mean-interarrival-ns", type=int, default=6_000_000,
@@ -283,15 +285,16 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     json_text, desc = build_graph(args.config)
+    # every trace is walked unless --fill: a draw-free static walk (config 2)
+    # is otherwise walked once and filled, which is not a walk rate
     params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A,
-                            flags=isim.native.FLAG_NO_SVC_DUR if args.no_svc_dur else 0)
+                            flags=(isim.native.FLAG_NO_SVC_DUR if args.no_svc_dur else 0) |
+                            (0 if args.fill else isim.native.FLAG_WALK_ALL))
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
     if args.config == "c5":
         if args.batch == 1 << 22:
             args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
         return main_des(args, h, json_text, desc, params, rank, world, dev)
-    if args.config == "c2" and args.batch == 1 << 22:
-        args.batch = 1 << 27  # BASELINE config 2: ~100M traces; a draw-free walk is a record fill (2 GiB)
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
     B = args.batch
