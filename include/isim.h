@@ -262,7 +262,7 @@ typedef struct {
   int32_t max_width;             /* widest level */
   int32_t table_rows;            /* rows of the DES table (reachable services) */
   int32_t n_fused;               /* leaf positions finished in their queue pass (no up pass) */
-  int32_t reserved;
+  int32_t cyclic;                /* 1: the call-step schedule is cyclic (fixed-point passes) */
 } isim_des_info;
 
 ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);

@@ -582,6 +582,7 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   out->max_width = (int32_t)h->des.max_width;
   out->table_rows = (int32_t)h->prog.row_svc.size();
   for (const auto &q : h->des.pos) out->n_fused += (q.flags & isim::kDesFlagFused) ? 1 : 0;
+  out->cyclic = h->des.cyclic ? 1 : 0;
   return ISIM_OK;
 }
 

@@ -80,7 +80,7 @@ class DesParams(C.Structure):
 
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
-                ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("reserved", C.c_int32)]
+                ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32)]
 
 
 # every function declared in include/isim.h: name -> (restype, argtypes)

@@ -110,6 +110,7 @@ def test_des_class():
     _rejects(_handler(doc), "more than 65536 replicas")
     d = isim.DesHandler(_handler(realistic_topology(200, concurrent=True, sleep_ms=(1, 5))), 5_000_000)
     assert (d.info.n_positions, d.info.table_rows) == (200, 200)
+    assert d.info.cyclic == 0 and 0 < d.info.n_fused < 200  # the tree's leaves finish in their queue pass
     assert d.info.n_levels >= 2 and d.info.max_width >= 1
     assert d.workspace_bytes(1000) >= 200 * 1000 * 8 + 1000 * 12
     # DAG graphs (a service at several positions) and replicated callers take the sort path
@@ -119,8 +120,9 @@ def test_des_class():
     isim.DesHandler(_handler(canon), 1_000_000)
     # ... with a hold, b's queue waits for its own finish: a cyclic schedule,
     # run as passes to its fixed point
+    assert isim.DesHandler(_handler(canon), 1_000_000).info.cyclic == 0  # zero holds: per-position starts
     canon["services"][1]["script"] = [{"sleep": "1ms"}]
-    isim.DesHandler(_handler(canon), 1_000_000)
+    assert isim.DesHandler(_handler(canon), 1_000_000).info.cyclic == 1
     dc = isim.DesHandler(_handler(canonical_concurrent()), 1_000_000)
     assert dc.info.n_positions == 6
     assert dc.workspace_bytes(1000) > 6 * 1000 * 8 + 2 * 1000 * 24  # a and b: 2 positions each
