@@ -112,6 +112,10 @@ uint64_t stats_words(const isim_handler *h) {
   return ISIM_ST_SVC_DUR(h->prog.n_slots) + (uint64_t)ISIM_SVC_DUR_WORDS * svc_dur_rows(h);
 }
 
+#ifndef ISIM_DYN_MIN_GAIN
+#define ISIM_DYN_MIN_GAIN 0  // resident waves a smaller workgroup / global counters must add to be chosen
+#endif
+
 // LDS layout of the walk kernel for a given workgroup size (walk.hip).
 uint32_t lds_need(const isim::Program &p, uint32_t waves, bool counters) {
   uint32_t b = isim::kLdsAccBytes + isim::kHistWords * 4u;
@@ -159,6 +163,35 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   // mode B on the draw stream: the per-lane bit stack holds 32 stack positions
   if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B && p.max_depth <= 32) st.kind = 5;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
+  if (!p.static_walk) {
+    // dynamic walks keep per-lane frame stacks in LDS (waves x frames x 64
+    // lanes): the workgroup size with the most resident waves per CU, not the
+    // largest that fits
+    uint32_t best_w = waves, best_res = 0;
+    bool best_c = counters;
+    for (int c = counters ? 1 : 0; c >= 0; --c) {
+      void *kern = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, c != 0);
+      for (uint32_t w = 16; w >= 1; w >>= 1) {
+        const uint32_t need = lds_need(p, w, c != 0);
+        if (need > lds_max) continue;
+        HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+        int pc = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void *)kern, (int)(w * 64u), need));
+        const uint32_t res = (uint32_t)pc * w;
+        if (res > best_res + ISIM_DYN_MIN_GAIN) {  // the LDS counter table wins ties
+          best_res = res;
+          best_w = w;
+          best_c = c != 0;
+        }
+      }
+    }
+    waves = best_w;
+    counters = best_c;
+    st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
+    st.threads = waves * 64u;
+    st.lds_bytes = lds_need(p, waves, counters);
+    st.lds_counters = counters ? 1u : 0u;
+  }
   if (st.kind >= 4) {
     st.draw_free = true;
     for (const isim::Node &nd : p.stream) st.draw_free = st.draw_free && nd.thr == 0;
