@@ -59,6 +59,9 @@ __device__ __forceinline__ uint32_t rep_bits(uint32_t reps) { return reps > 1 ? 
 #define ISIM_DES_DOWN_THREADS 512
 #endif
 constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-position queue pass
+#ifndef ISIM_DES_MIX
+#define ISIM_DES_MIX 1  // fused and other single-replica positions of a round in one queue launch
+#endif
 #ifndef ISIM_DES_DOWN_WAVES
 #define ISIM_DES_DOWN_WAVES 6  // waves per SIMD the one-workgroup-per-position pass is compiled for
 #endif
@@ -631,13 +634,12 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 // ---- queue pass, one workgroup per position (wide groups; replicated
 // services: per-replica scans, the routing draw per trace)
 template <typename T, bool MULTI, bool FUSED>
-__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(DesK k) {
+__device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
   __shared__ MaxPlus wtot[kDownThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
   __shared__ uint64_t red[3 * kDownThreads / 64];
   __shared__ MaxPlus xs[kDownThreads];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
   const DesPos P = k.pos[v];
   const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
@@ -704,6 +706,20 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(De
   }
 }
 
+template <typename T, bool MULTI, bool FUSED>
+__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(DesK k) {
+  down_body<T, MULTI, FUSED>(k, k.level_pos[k.level_begin + blockIdx.x]);
+}
+
+// single-replica positions of a round, fused leaves and others in ONE launch
+// (better packing of the last wave of workgroups than two launches)
+template <typename T>
+__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_mix(DesK k) {
+  const uint32_t v = k.level_pos[k.level_begin + blockIdx.x];
+  if (k.pos[v].flags & kDesFlagFused) down_body<T, false, true>(k, v);
+  else down_body<T, false, false>(k, v);
+}
+
 // ---- queue pass, single-replica services of narrow groups: one workgroup
 // per (position, chunk of kDownChunk traces), chunks of a position chained by
 // a decoupled look-back over their max-plus maps.  Workgroups take tickets in
@@ -729,21 +745,25 @@ __device__ __forceinline__ void st_flag(uint32_t *p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the ticket of a chained-scan workgroup: (position, chunk) in launch order
+__device__ __forceinline__ uint32_t chain_ticket(const DesK &k) {
+  __shared__ uint32_t s_ticket;
+  if (threadIdx.x == 0) s_ticket = atomicAdd(k.chain_ticket, 1u);
+  __syncthreads();
+  return s_ticket;
+}
+
 template <typename T, bool FUSED>
-__global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
+__device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t chunk) {
   __shared__ MaxPlus wtot[kDesThreads / 64];
   __shared__ MaxPlus xs[kDesThreads];
   __shared__ uint64_t red[3 * kDesThreads / 64];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint32_t s_ticket;
   __shared__ uint64_t s_carry;
-  if (threadIdx.x == 0) s_ticket = atomicAdd(k.chain_ticket, 1u);
-  if constexpr (FUSED)
+  if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
-  __syncthreads();
-  const uint32_t ticket = s_ticket;
-  const uint32_t chunk = ticket % k.n_chunks;
-  const uint32_t v = k.level_pos[k.level_begin + ticket / k.n_chunks];
+    __syncthreads();
+  }
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
@@ -839,6 +859,20 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
     __syncthreads();
     des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red);
   }
+}
+
+template <typename T, bool FUSED>
+__global__ void __launch_bounds__(kDesThreads, 8) des_down_chain(DesK k) {
+  const uint32_t ticket = chain_ticket(k);
+  chain_body<T, FUSED>(k, k.level_pos[k.level_begin + ticket / k.n_chunks], ticket % k.n_chunks);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kDesThreads, 8) des_down_chain_mix(DesK k) {
+  const uint32_t ticket = chain_ticket(k);
+  const uint32_t v = k.level_pos[k.level_begin + ticket / k.n_chunks];
+  if (k.pos[v].flags & kDesFlagFused) chain_body<T, true>(k, v, ticket % k.n_chunks);
+  else chain_body<T, false>(k, v, ticket % k.n_chunks);
 }
 
 // ---- up pass: finish times, statuses, per-service durations.
@@ -1340,7 +1374,20 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
     //    chained scan (many workgroups per position); wide groups and
     //    replicated services one workgroup per position.
     k.level_pos = L.d_fast_pos;
-    for (uint32_t j = 0; j < 4; ++j) {
+    if (ISIM_DES_MIX) {
+      // single-replica positions (fused leaves or not): one launch
+      const uint32_t b = pl.fast_split[5 * r], e = pl.fast_split[5 * r + 2];
+      if (e > b) {
+        k.level_begin = b;
+        if (e - b < ISIM_DES_CHAIN_BELOW) {
+          k.chain_ticket = tickets + 4 * r;
+          hipLaunchKernelGGL(des_down_chain_mix<T>, dim3((e - b) * k.n_chunks), dim3(kDesThreads), 0, stream, k);
+        } else {
+          hipLaunchKernelGGL(des_down_mix<T>, dim3(e - b), dim3(kDownThreads), 0, stream, k);
+        }
+      }
+    }
+    for (uint32_t j = ISIM_DES_MIX ? 2 : 0; j < 4; ++j) {
       const uint32_t b = pl.fast_split[5 * r + j], e = pl.fast_split[5 * r + j + 1];
       if (e == b) continue;
       k.level_begin = b;
