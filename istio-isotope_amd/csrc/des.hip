@@ -62,6 +62,9 @@ constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-p
 #ifndef ISIM_DES_MIX
 #define ISIM_DES_MIX 1  // fused and other single-replica positions of a round in one queue launch
 #endif
+#ifndef ISIM_DES_SPLIT_TARGET
+#define ISIM_DES_SPLIT_TARGET 8192  // (position x trace-range) blocks per up / step-begin launch
+#endif
 #ifndef ISIM_DES_DOWN_WAVES
 #define ISIM_DES_DOWN_WAVES 6  // waves per SIMD the one-workgroup-per-position pass is compiled for
 #endif
@@ -1346,7 +1349,7 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
   k.sort_pos = L.d_sort_pos;
   // (position or row) x trace-range blocks: enough to fill the chip, >= 256 traces each
   auto splits_for = [&](uint32_t width) {
-    uint64_t sp = (4096 + width - 1) / width;
+    uint64_t sp = (ISIM_DES_SPLIT_TARGET + width - 1) / width;
     const uint64_t cap = (L.n_traces + 255) / 256;
     sp = sp < cap ? sp : cap;
     return (uint32_t)(sp ? sp : 1);
