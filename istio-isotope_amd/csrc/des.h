@@ -85,7 +85,7 @@ struct DesPlan {
   std::vector<uint32_t> arr_ops, arr_off;        // BK rows computed in round r
   std::vector<uint32_t> fast_pos, fast_off;      // single-position trace-ordered services
   // [rounds][5]: a round's fast positions by kernel variant (des_down<MULTI, FUSED>):
-  // [v][0..1) single replica, [1..2) fused single, [2..3) replicas, [3..4) fused replicas
+  // [v][0..1) fused single replica, [1..2) single, [2..3) fused replicated, [3..4) replicated
   std::vector<uint32_t> fast_split;
   std::vector<uint32_t> zero_pos, zero_off;      // positions of zero-hold services: start = arrival
   std::vector<DesSortSvc> sorted;                // sort-path services

@@ -1354,9 +1354,10 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
     sp = sp < cap ? sp : cap;
     return (uint32_t)(sp ? sp : 1);
   };
-  static void (*const down[4])(DesK) = {des_down<T, false, false>, des_down<T, false, true>,
-                                       des_down<T, true, false>, des_down<T, true, true>};
-  static void (*const chain[2])(DesK) = {des_down_chain<T, false>, des_down_chain<T, true>};
+  // the plan's variant order (des_plan.cpp): [single fused | single | replicated fused | replicated]
+  static void (*const down[4])(DesK) = {des_down<T, false, true>, des_down<T, false, false>,
+                                       des_down<T, true, true>, des_down<T, true, false>};
+  static void (*const chain[2])(DesK) = {des_down_chain<T, true>, des_down_chain<T, false>};
   for (uint32_t r = 0; r < pl.rounds(); ++r) {
     // 1. step begins (calls after calls)
     const uint32_t na = pl.arr_off[r + 1] - pl.arr_off[r];

@@ -347,8 +347,10 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     out.arr_ops.insert(out.arr_ops.end(), arr[r].begin(), arr[r].end());
     out.arr_off[r + 1] = (uint32_t)out.arr_ops.size();
     // grouped by kernel variant: single replica (no routing draw) or not, fused leaf or not
+    // fused leaves first: in a launch mixing both, the costlier workgroups
+    // start first and the last wave of workgroups is the cheaper kind
     auto variant = [&](uint32_t v) {
-      return (out.pos[v].reps > 1 ? 2u : 0u) + ((out.pos[v].flags & kDesFlagFused) ? 1u : 0u);
+      return (out.pos[v].reps > 1 ? 2u : 0u) + ((out.pos[v].flags & kDesFlagFused) ? 0u : 1u);
     };
     std::stable_sort(fast[r].begin(), fast[r].end(),
                      [&](uint32_t a, uint32_t b) { return variant(a) < variant(b); });
