@@ -381,6 +381,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     out.sorted_off[r + 1] = (uint32_t)out.sorted.size();
     for (uint32_t d = out.n_levels; d-- > 0;) {
       if (fin[r][d].empty()) continue;
+      // most children first: the costliest blocks start first
+      std::stable_sort(fin[r][d].begin(), fin[r][d].end(),
+                       [&](uint32_t a, uint32_t b) { return out.pos[a].child_cnt > out.pos[b].child_cnt; });
       out.fin_pos.insert(out.fin_pos.end(), fin[r][d].begin(), fin[r][d].end());
       out.fin_off.push_back((uint32_t)out.fin_pos.size());
     }
