@@ -86,6 +86,8 @@ typedef struct {
 #define ISIM_FLAG_NO_STREAM 1u  /* run static walks on the interpreter kernel instead of the draw stream */
 #define ISIM_FLAG_NO_SVC_DUR 2u /* dynamic walks: do not record per-service invocation durations */
 #define ISIM_FLAG_WALK_ALL 4u   /* draw-free static walks: walk every trace (default: walk one, fill the rest) */
+#define ISIM_FLAG_BIT_STACK 8u  /* mode B on the draw stream: the bit-stack kernel (kind 5, call depth <= 32;
+                                   kind 4 deeper) instead of the close-list kernel (kind 6) */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -158,7 +160,8 @@ typedef struct {
   int32_t blocks_per_cu;     /* resident workgroups per CU (occupancy query) */
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
   int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
-                                5 draw stream with the mode-B bit stack (call depth <= 32) */
+                                5 draw stream with the mode-B bit stack (call depth <= 32),
+                                6 draw stream with the mode-B close list (the default in mode B) */
   int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
 } isim_launch_info;

@@ -39,6 +39,9 @@ int fail(int code, const std::string &msg) {
 struct DevState {
   void *d_prog = nullptr;  // Ins[] (interpreters) or Node[] (draw stream)
   uint32_t *d_mult = nullptr;  // draw stream: per-slot call multiplicity
+  isim::StreamClose *d_closes = nullptr;  // mode-B draw stream (kind 6): close list
+  uint32_t *d_close_slot = nullptr;       // per close: call-site slot
+  uint32_t *d_close_end = nullptr;        // and its per-chunk ends
   uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
   unsigned long long *d_work = nullptr;  // kWorkSlots sets of batch queues, zero between launches
   // draw-free static walks (no error draw anywhere): every trace walks alike
@@ -81,6 +84,9 @@ struct isim_handler {
       if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
         (void)hipFree(kv.second.d_prog);
         (void)hipFree(kv.second.d_mult);
+        (void)hipFree(kv.second.d_closes);
+        (void)hipFree(kv.second.d_close_end);
+        (void)hipFree(kv.second.d_close_slot);
         (void)hipFree(kv.second.d_dur);
         (void)hipFree(kv.second.d_work);
         (void)hipFree(kv.second.d_const_stats);
@@ -161,7 +167,9 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   st.kind = p.stream_nodes ? 4u : (p.static_walk ? 0u : 2u) + (p.time_bits == 64 ? 1u : 0u);
   if ((h->params.flags & ISIM_FLAG_NO_STREAM) && st.kind == 4) st.kind = p.time_bits == 64 ? 1u : 0u;
   // mode B on the draw stream: the per-lane bit stack holds 32 stack positions
-  if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B && p.max_depth <= 32) st.kind = 5;
+  // (ISIM_FLAG_BIT_STACK), else the close list (any depth)
+  if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B)
+    st.kind = (h->params.flags & ISIM_FLAG_BIT_STACK) ? (p.max_depth <= 32 ? 5u : 4u) : 6u;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
   if (!p.static_walk) {
     // dynamic walks keep per-lane frame stacks in LDS (waves x frames x 64
@@ -220,6 +228,29 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
   if (svc_dur_rows(h) && p.n_slots > 0) {
     HIPCHK(hipMalloc(&st.d_dur, p.slot_dur.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_dur, p.slot_dur.data(), p.slot_dur.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  if (st.kind == 6) {
+    // zero tail padding: the kernel prefetches blocks of 8 closes past the end
+    auto upload = [&](void *&dst, const void *src, size_t bytes, size_t pad) -> int {
+      HIPCHK(hipMalloc(&dst, bytes + pad));
+      HIPCHK(hipMemset(dst, 0, bytes + pad));
+      if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+      return ISIM_OK;
+    };
+    int rc = upload((void *&)st.d_closes, p.stream_closes.data(), p.stream_closes.size() * sizeof(isim::StreamClose),
+                    isim::kClosePad * sizeof(isim::StreamClose));
+    if (rc == ISIM_OK)
+      rc = upload((void *&)st.d_close_slot, p.stream_close_slot.data(), p.stream_close_slot.size() * sizeof(uint32_t),
+                  64 * sizeof(uint32_t));
+    if (rc == ISIM_OK)
+      rc = upload((void *&)st.d_close_end, p.stream_close_end.data(), p.stream_close_end.size() * sizeof(uint32_t),
+                  2 * sizeof(uint32_t));
+    if (rc != ISIM_OK) {
+      (void)hipFree(st.d_closes);
+      (void)hipFree(st.d_close_slot);
+      (void)hipFree(st.d_close_end);
+      return rc;
+    }
   }
   HIPCHK(hipMalloc(&st.d_work, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   HIPCHK(hipMemset(st.d_work, 0, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
@@ -408,6 +439,9 @@ static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint
   kp.t_static = h->prog.max_latency;
   kp.svc_dur = svc_dur_rows(h) ? 1u : 0u;
   kp.root_dur = h->prog.root_dur;
+  kp.closes = st->d_closes;
+  kp.close_slot = st->d_close_slot;
+  kp.close_end = st->d_close_end;
   const uint64_t per_wave = st->kind >= 4 ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;

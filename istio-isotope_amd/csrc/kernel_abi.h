@@ -48,6 +48,25 @@ constexpr uint32_t kSlotRoot = 0xFFFFFFu;  // the entry invocation (no call site
 constexpr uint32_t kSlotPad = 0xFFFFFEu;   // padding to a multiple of 4 records
 constexpr uint32_t kMaxStreamNodes = 1u << 24;
 
+// Mode B on the draw stream (kernel kind 6): the closes of calling
+// invocations (subtrees with children, the entry excepted), in close order.
+// The stream is walked in chunks of kChunkRecords records; per chunk a lane
+// keeps the error bits of its records (record r of a chunk of n records at
+// bit n-1-r) and, from earlier chunks, the position + 1 of its last erring
+// record.  The invocation at stream position p whose subtree ends at record j
+// responds 500 iff an invocation in [p, j] erred:
+//   (bits & rmask) != 0  ||  last_err1 >= pre1
+// rmask = the chunk bits of records [max(p, chunk start), j]; pre1 = p + 1
+// when p lies before the chunk, else 0xFFFFFFFF (the test is never true).
+struct StreamClose {
+  uint32_t pre1;
+  uint32_t rmask;
+};
+static_assert(sizeof(StreamClose) == 8, "StreamClose must be 8 bytes");
+constexpr uint32_t kClosePad = 16;  // zero StreamClose records after the list (block prefetch)
+constexpr uint32_t kChunkGroups = 8;                  // Philox groups (4 records) per chunk
+constexpr uint32_t kChunkRecords = 4 * kChunkGroups;  // 32: one bit per record per lane
+
 // Per-service duration table word: row (bits 0-23) | bucket of a leaf callee (24-31).
 constexpr uint32_t kDurRowMask = 0xFFFFFFu;
 
@@ -65,6 +84,9 @@ struct KParams {
   uint32_t svc_dur;         // dynamic walks: 1 = record per-service durations
   uint32_t root_dur;        // the entry's duration-table word (row | leaf bucket << 24)
   unsigned long long *work; // batch queues (kWorkWords): zero at launch, zeroed again by the last wave
+  const StreamClose *closes;     // kind 6: close list (+kClosePad zero records of tail padding)
+  const uint32_t *close_slot;    // kind 6: per close, the call-site slot of the closing invocation
+  const uint32_t *close_end;     // kind 6: per chunk, closes up to and including it
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to
@@ -80,7 +102,8 @@ constexpr uint32_t kLdsAccBytes = 64;                 // WgAcc
 constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 
 // walk.hip: kernel pointer for a walk variant.
-// kind: 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream.
+// kind: 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
+// 5 draw stream + mode-B bit stack, 6 draw stream + mode-B close list.
 void *walk_kernel(int kind, bool modeb, bool lds_counters);
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

@@ -323,16 +323,30 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
       nd.meta = (slot & 0xFFFFFFu) | (thr[callee] >= (1ull << 32) ? 0x80000000u : 0u);
       out.stream.push_back(nd);
     };
-    std::vector<std::pair<int32_t, size_t>> stack;
+    struct Frame {
+      int32_t svc;
+      size_t next;  // next call site of the script
+      uint32_t pre;  // stream position of the invocation
+      uint32_t slot;
+    };
+    struct Pop {
+      uint32_t pre, end, slot;  // a calling invocation: its subtree spans records [pre, end]
+    };
+    std::vector<Frame> stack;
+    std::vector<Pop> pops;
     rec(entry, kSlotRoot);
-    stack.push_back({entry, 0});
+    stack.push_back({entry, 0, 0u, kSlotRoot});
     while (!stack.empty()) {
-      auto &top = stack.back();
-      if (top.second < svc_sites[top.first].size()) {
-        const int32_t sid = svc_sites[top.first][top.second++];
-        rec(sites[sid].callee, (uint32_t)out.site_slot[sid]);
-        stack.push_back({sites[sid].callee, 0});
+      Frame &top = stack.back();
+      if (top.next < svc_sites[top.svc].size()) {
+        const int32_t sid = svc_sites[top.svc][top.next++];
+        const uint32_t slot = (uint32_t)out.site_slot[sid];
+        const uint32_t pre = (uint32_t)out.stream.size();
+        rec(sites[sid].callee, slot);
+        stack.push_back({sites[sid].callee, 0, pre, slot});
       } else {
+        const uint32_t end = (uint32_t)out.stream.size() - 1;
+        if (top.pre != end && top.slot != kSlotRoot) pops.push_back({top.pre, end, top.slot});
         stack.pop_back();
         out.stream.back().meta += 1u << 24;  // the subtree ending here closes after this record
       }
@@ -342,6 +356,24 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     for (const Node &nd : out.stream)
       if ((nd.meta & 0xFFFFFFu) != kSlotRoot) out.stream_mult[nd.meta & 0xFFFFFFu] += 1;
     while (out.stream.size() % 4) out.stream.push_back(Node{0u, kSlotPad});
+    // close list of the mode-B stream kernel (kernel_abi.h, StreamClose)
+    const uint32_t n_rec = (uint32_t)out.stream.size();
+    const uint32_t n_chunks = (n_rec + kChunkRecords - 1) / kChunkRecords;
+    out.stream_close_end.assign(n_chunks, 0u);
+    out.stream_closes.clear();
+    out.stream_close_slot.clear();
+    for (const Pop &q : pops) {
+      const uint32_t c = q.end / kChunkRecords, cb = c * kChunkRecords;
+      const uint32_t n = std::min(kChunkRecords, n_rec - cb);  // records walked in the chunk
+      const uint32_t lo = std::max(q.pre, cb);
+      uint32_t m = 0;
+      for (uint32_t r = lo; r <= q.end; ++r) m |= 1u << (n - 1 - (r - cb));
+      out.stream_closes.push_back(StreamClose{q.pre < cb ? q.pre + 1 : 0xFFFFFFFFu, m});
+      out.stream_close_slot.push_back(q.slot);
+      out.stream_close_end[c] = (uint32_t)out.stream_closes.size();
+    }
+    for (uint32_t c = 1; c < n_chunks; ++c)
+      out.stream_close_end[c] = std::max(out.stream_close_end[c], out.stream_close_end[c - 1]);
   }
   if (code.size() >= (1u << 30)) {
     err = "program too large";

@@ -36,6 +36,9 @@ struct Program {
   std::vector<Node> stream;                     // padded to a multiple of 4
   uint32_t stream_nodes = 0;                    // invocations per trace (unpadded)
   std::vector<uint32_t> stream_mult;            // per slot: calls through it per trace
+  std::vector<StreamClose> stream_closes;       // mode B (kind 6): closes of calling invocations
+  std::vector<uint32_t> stream_close_slot;      // per close: call-site slot
+  std::vector<uint32_t> stream_close_end;       // per chunk of kChunkRecords records
   // per-service invocation durations (RecordResponseSent, prometheus/handler.go:101-106)
   std::vector<uint64_t> svc_time;   // per service: T_max; the exact duration when static_walk
   std::vector<int32_t> svc_row;     // per service: row in the duration table (-1: unreachable)

@@ -716,6 +716,12 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
 #ifndef ISIM_EARLY_WAIT
 #define ISIM_EARLY_WAIT 0
 #endif
+#ifndef ISIM_CL_SKIP_CLOSES  // timing experiments only (wrong counts)
+#define ISIM_CL_SKIP_CLOSES 0
+#endif
+#ifndef ISIM_CL_SKIP_LEAVES
+#define ISIM_CL_SKIP_LEAVES 0
+#endif
 #ifndef ISIM_FAST_A
 #define ISIM_FAST_A 1
 #endif
@@ -1000,6 +1006,179 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
   for (int u = 0; u < TPL; ++u) finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st[u], errh[u]);
 }
 
+// m = 2 m + (this lane in mask): one v_addc_co_u32 with the lane mask as carry-in
+__device__ __forceinline__ void shift_in(uint32_t &m, uint64_t mask) {
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %0, %0, %2" : "+v"(m), "=s"(co) : "s"(mask));
+}
+// v += (this lane in mask)
+__device__ __forceinline__ void add_lane(uint32_t &v, uint64_t mask) {
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, 0, %0, %2" : "+v"(v), "=s"(co) : "s"(mask));
+}
+
+typedef const __attribute__((address_space(4))) StreamClose CClose;
+typedef const __attribute__((address_space(4))) uint32_t CU32;
+struct CloseBlk {
+  StreamClose c[8];
+};
+__device__ __forceinline__ CloseBlk load_closes(CClose *p) {  // one s_load_dwordx16
+  CloseBlk r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r.c[k].pre1 = p[k].pre1;
+    r.c[k].rmask = p[k].rmask;
+  }
+  return r;
+}
+
+// Mode B on the draw stream without a stack (kernel kind 6).  An invocation
+// responds 500 iff some invocation of its subtree drew an error (a 500 fails
+// the caller's step, and the caller's step failure is its 500), and a
+// subtree is the contiguous stream range [p, j] (DFS preorder).  So a lane
+// only keeps, per trace, the error bits of the current chunk of 32 records
+// (shifted in, one v_addc per record) and the position + 1 of its last
+// erring record before the chunk; after each chunk the closes that end in it
+// are tested against both (StreamClose, kernel_abi.h) and counted (a lane
+// per close, one ds_add per 64 closes).  Leaves respond with their own draw
+// (a lane per record, one ds_add per chunk); the entry's status is "any
+// error at all".  No call-depth limit, no per-record branching
+// on the stack.
+template <bool LDSC, int TPL, bool FULL>
+__device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict__ stream, uint32_t n_groups,
+                                               uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
+                                               uint64_t n_traces, uint64_t base, CClose *__restrict__ closes,
+                                               const uint32_t *__restrict__ close_slot, CU32 *__restrict__ close_end,
+                                               const uint32_t *__restrict__ stream_w) {
+  const uint32_t lane = lane_id();
+  const bool lane0 = lane == 0;
+  uint64_t idx[TPL], all[TPL];
+  uint32_t t_lo[TPL], t_hi[TPL], t_hi_u[TPL];
+  bool valid[TPL];
+  bool hi_uniform = true;
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    idx[u] = base + 64u * u + lane;
+    valid[u] = idx[u] < n_traces;
+    const uint64_t t = trace_begin + idx[u];
+    t_lo[u] = (uint32_t)t;
+    t_hi[u] = (uint32_t)(t >> 32);
+    t_hi_u[u] = rfl(t_hi[u]);
+    hi_uniform = hi_uniform && ballot(t_hi[u] != t_hi_u[u]) == 0 && t_hi_u[u] == t_hi_u[0];
+    all[u] = ballot(valid[u]);
+  }
+  uint32_t errh[TPL], le[TPL];
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) errh[u] = le[u] = 0;
+
+  Node4 cur = load_group(stream);
+  uint32_t cp = 0;
+  const uint32_t n_chunks = (n_groups + kChunkGroups - 1) / kChunkGroups;
+  for (uint32_t ch = 0; ch < n_chunks; ++ch) {
+    const uint32_t g0 = ch * kChunkGroups;
+    const uint32_t g1 = g0 + kChunkGroups < n_groups ? g0 + kChunkGroups : n_groups;
+    // the chunk's first 64 close slots (one per lane), loaded before its Philox work
+    uint32_t slotv = close_slot[cp + lane];  // zero tail padding
+    const uint32_t nrec = 4u * (g1 - g0);
+    const uint32_t rmeta = lane < nrec ? stream_w[2u * (ch * kChunkRecords + lane) + 1u] : kSlotPad;
+    uint32_t lcnt = 0;
+    uint32_t mb[TPL];
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) mb[u] = 0;
+    for (uint32_t g = g0; g < g1; ++g) {
+      const Node4 nxt = load_group(stream + g + 1);  // zero tail padding
+      uint32_t x[TPL][4];
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
+      if ((cur.n[0].thr | cur.n[1].thr | cur.n[2].thr | cur.n[3].thr) != 0) {
+        if (ISIM_LOCKSTEP && hi_uniform) {
+          philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
+        } else {
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) philox_group(t_lo[u], t_hi[u], t_hi_u[u], hi_uniform, g, c.k0, c.k1, x[u]);
+        }
+      }
+      auto records = [&](bool always) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t thr = cur.n[j].thr, meta = cur.n[j].meta;
+          uint32_t n = 0;
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) {
+            uint64_t own = ballot(x[u][j] < thr);
+            if (always && (meta & 0x80000000u)) own = ~0ull;
+            shift_in(mb[u], own);
+            if constexpr (!FULL) own &= all[u];
+            n += popc(own);
+          }
+          if (!ISIM_CL_SKIP_LEAVES) lcnt = wrl(n, 4u * (g - g0) + j, lcnt);  // lane r: record r's count
+        }
+      };
+      // errorRate-1 records (always 500) are rare: a branch per record only
+      // in the groups that hold one
+      if (((cur.n[0].meta | cur.n[1].meta | cur.n[2].meta | cur.n[3].meta) & 0x80000000u) == 0) records(false);
+      else records(true);
+      cur = nxt;
+    }
+    // leaves respond with their own draw: their error counts (lane r =
+    // record r) go to the site table in one ds_add, their 500s to errh
+    if (!ISIM_CL_SKIP_LEAVES) {
+      const uint32_t rslot = rmeta & 0xFFFFFFu;
+      const bool leaf = (rmeta & 0x7F000000u) != 0 && rslot < kSlotPad;
+      const uint32_t lm = __builtin_bitreverse32((uint32_t)ballot(leaf)) >> (32u - nrec);  // mb's bit order
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) errh[u] += (uint32_t)__builtin_popcount(mb[u] & lm);
+      if (leaf && lcnt) {
+        if constexpr (LDSC) atomicAdd(c.cnt + c.n_slots + rslot, lcnt);
+        else atomicAdd((unsigned long long *)(c.gstats + ISIM_ST_SITES + c.n_slots + rslot), (unsigned long long)lcnt);
+      }
+    }
+    const uint32_t ce = close_end[ch];
+    CloseBlk blk = load_closes(closes + cp);  // the chunk's first 8 closes
+    // calling invocations whose subtree ends in this chunk, in segments of
+    // up to 64: close i of a segment keeps its count in lane i of cntv, and
+    // the segment's counts go to the site table in one ds_add
+    while (!ISIM_CL_SKIP_CLOSES && cp < ce) {
+      const uint32_t nseg = ce - cp < 64u ? ce - cp : 64u;
+      uint32_t cntv = 0;
+      for (uint32_t i = 0; i < nseg; i += 8) {
+        const CloseBlk nb = load_closes(closes + cp + i + 8);  // zero tail padding
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (i + k >= nseg) break;
+          const uint32_t pre1 = blk.c[k].pre1, rmask = blk.c[k].rmask;
+          uint32_t n = 0;
+#pragma unroll
+          for (int u = 0; u < TPL; ++u) {
+            uint64_t st = ballot((mb[u] & rmask) != 0u) | ballot(le[u] >= pre1);
+            if constexpr (!FULL) st &= all[u];
+            add_lane(errh[u], st);
+            n += popc(st);
+          }
+          cntv = wrl(n, i + k, cntv);
+        }
+        blk = nb;
+      }
+      if (lane < nseg) {
+        if constexpr (LDSC) atomicAdd(c.cnt + c.n_slots + slotv, cntv);
+        else if (cntv) atomicAdd((unsigned long long *)(c.gstats + ISIM_ST_SITES + c.n_slots + slotv),
+                                 (unsigned long long)cntv);
+      }
+      cp += nseg;
+      if (cp < ce) slotv = close_slot[cp + lane];  // a chunk with more than 64 closes
+    }
+    const uint32_t top = ch * kChunkRecords + 4u * (g1 - g0);
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) le[u] = mb[u] ? top - (uint32_t)__builtin_ctz(mb[u]) : le[u];
+  }
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    const uint64_t root_st = ballot(le[u] != 0u) & all[u];
+    add_lane(errh[u], root_st);
+    finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st, errh[u]);
+  }
+}
+
 // Executed-call counters of a static walk: every trace makes mult[slot] calls
 // through each reachable call site, so a launch over n_traces adds
 // mult[slot] * n_traces (exact; added once per launch).
@@ -1036,7 +1215,8 @@ __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_
 }
 
 // KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream,
-// 5 draw stream with the mode-B bit stack (call depth <= 32)
+// 5 draw stream with the mode-B bit stack (call depth <= 32), 6 draw stream
+// with the mode-B close list
 // LDSC: per-site counters in the workgroup LDS table (else global atomics)
 template <int KIND, bool MODEB, bool LDSC>
 __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
@@ -1096,7 +1276,16 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
       const uint64_t base = b * 64 * kStreamTPL;
       CNode4 *st = (CNode4 *)(const __attribute__((address_space(1))) Ins *)prog;
       const uint32_t ng = kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0;
-      if (base + 64 * kStreamTPL <= kp.n_traces)  // every lane of every trace slot valid
+      if constexpr (KIND == 6) {
+        CClose *cl = (CClose *)(const __attribute__((address_space(1))) StreamClose *)kp.closes;
+        CU32 *ce = (CU32 *)(const __attribute__((address_space(1))) uint32_t *)kp.close_end;
+        if (base + 64 * kStreamTPL <= kp.n_traces)
+          walk_stream_cl<LDSC, kStreamTPL, true>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces,
+                                                 base, cl, kp.close_slot, ce, (const uint32_t *)prog);
+        else
+          walk_stream_cl<LDSC, kStreamTPL, false>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces,
+                                                  base, cl, kp.close_slot, ce, (const uint32_t *)prog);
+      } else if (base + 64 * kStreamTPL <= kp.n_traces)  // every lane of every trace slot valid
         walk_stream<MODEB, LDSC, kStreamTPL, true, KIND == 5>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin,
                                                    kp.n_traces, base);
       else
@@ -1147,9 +1336,12 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters) {
     case 2: return pick<2>(modeb, lds_counters);
     case 3: return pick<3>(modeb, lds_counters);
     case 4: return pick<4>(modeb, lds_counters);
-    default:  // the bit stack only exists in mode B
+    case 5:  // the bit stack only exists in mode B
       if (!modeb) return pick<4>(false, lds_counters);
       return lds_counters ? (void *)&dev::isim_walk<5, true, true> : (void *)&dev::isim_walk<5, true, false>;
+    default:  // 6: the close list only exists in mode B
+      if (!modeb) return pick<4>(false, lds_counters);
+      return lds_counters ? (void *)&dev::isim_walk<6, true, true> : (void *)&dev::isim_walk<6, true, false>;
   }
 }
 

@@ -26,6 +26,7 @@ ABI_VERSION = 5  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
+FLAG_BIT_STACK = 8  # mode B on the draw stream: the bit-stack kernel (kind 5/4) instead of the close list (6)
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4

@@ -26,7 +26,7 @@ def _fixture_json(path, error_rate=None):
     return j
 
 
-KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM}
+KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM, "bitstack": isim.native.FLAG_BIT_STACK}
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
@@ -37,8 +37,14 @@ def test_reference_topologies(gpu, path, mode, kernel):
     kind = c.handler.launch_info(0)["kernel_kind"]
     tb64 = c.handler.info.time_bits == 64
     if c.handler.info.static_walk:
-        bs = mode == isim.MODE_B and c.handler.info.max_depth <= 32
-        assert kind == ((5 if bs else 4) if kernel == "stream" else int(tb64))
+        if kernel == "interp":
+            assert kind == int(tb64)
+        elif mode == isim.MODE_A:
+            assert kind == 4
+        elif kernel == "stream":
+            assert kind == 6  # mode B: the close list
+        else:
+            assert kind == (5 if c.handler.info.max_depth <= 32 else 4)
     else:
         assert kind == 2 + int(tb64)
     c.compare(0, 3000)
@@ -150,10 +156,22 @@ def _chain(n, fan=2):
 @pytest.mark.parametrize("depth,kind", [(31, 5), (32, 5), (33, 4), (64, 4)])
 def test_mode_b_stack_depths(gpu, depth, kind):
     # the bit-stack kernel (kind 5) holds 32 stack positions; deeper graphs take kind 4
-    c = Case(_chain(depth), None, isim.SimParams(error_mode=isim.MODE_B))
+    c = Case(_chain(depth), None, isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_BIT_STACK))
     assert c.handler.info.max_depth == depth
     assert c.handler.launch_info(0)["kernel_kind"] == kind
     c.compare(5, 3000)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 31, 33, 64])
+@pytest.mark.parametrize("fan", [0, 2, 40])
+def test_mode_b_close_list_depths(gpu, depth, fan):
+    # the close-list kernel (kind 6) has no depth limit; chains whose subtrees
+    # end inside, at and across the 32-record chunk boundaries
+    c = Case(_chain(depth, fan), None, isim.SimParams(error_mode=isim.MODE_B))
+    assert c.handler.info.max_depth == depth
+    assert c.handler.launch_info(0)["kernel_kind"] == 6
+    c.compare(5, 3000)
+    c.compare((1 << 32) - 700, 1500)
 
 
 # ---- batch queues: past the first wave-stride, waves claim batches from
