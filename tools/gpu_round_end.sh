@@ -8,4 +8,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 cat gpurun_out/smoke.log
 bash tools/profile.sh > gpurun_out/profile.log 2>&1 || { echo PROFILE_FAIL; tail gpurun_out/profile.log; exit 7; }
 bash tools/profile_c5.sh > gpurun_out/profile_c5.log 2>&1 || { echo PROFILE_C5_FAIL; tail gpurun_out/profile_c5.log; exit 6; }
+bash tools/profile_modeb.sh > gpurun_out/profile_b.log 2>&1 || { echo PROFILE_B_FAIL; tail gpurun_out/profile_b.log; exit 5; }
 echo round-end done
