@@ -716,12 +716,6 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
 #ifndef ISIM_EARLY_WAIT
 #define ISIM_EARLY_WAIT 0
 #endif
-#ifndef ISIM_CL_SKIP_CLOSES  // timing experiments only (wrong counts)
-#define ISIM_CL_SKIP_CLOSES 0
-#endif
-#ifndef ISIM_CL_SKIP_LEAVES
-#define ISIM_CL_SKIP_LEAVES 0
-#endif
 #ifndef ISIM_FAST_A
 #define ISIM_FAST_A 1
 #endif
@@ -1111,7 +1105,7 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
             if constexpr (!FULL) own &= all[u];
             n += popc(own);
           }
-          if (!ISIM_CL_SKIP_LEAVES) lcnt = wrl(n, 4u * (g - g0) + j, lcnt);  // lane r: record r's count
+          lcnt = wrl(n, 4u * (g - g0) + j, lcnt);  // lane r: record r's count
         }
       };
       // errorRate-1 records (always 500) are rare: a branch per record only
@@ -1122,7 +1116,7 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
     }
     // leaves respond with their own draw: their error counts (lane r =
     // record r) go to the site table in one ds_add, their 500s to errh
-    if (!ISIM_CL_SKIP_LEAVES) {
+    {
       const uint32_t rslot = rmeta & 0xFFFFFFu;
       const bool leaf = (rmeta & 0x7F000000u) != 0 && rslot < kSlotPad;
       const uint32_t lm = __builtin_bitreverse32((uint32_t)ballot(leaf)) >> (32u - nrec);  // mb's bit order
@@ -1138,7 +1132,7 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
     // calling invocations whose subtree ends in this chunk, in segments of
     // up to 64: close i of a segment keeps its count in lane i of cntv, and
     // the segment's counts go to the site table in one ds_add
-    while (!ISIM_CL_SKIP_CLOSES && cp < ce) {
+    while (cp < ce) {
       const uint32_t nseg = ce - cp < 64u ? ce - cp : 64u;
       uint32_t cntv = 0;
       for (uint32_t i = 0; i < nseg; i += 8) {
