@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
                     "fill the records (the library default) instead of walking every trace")
     ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--mean-interarrival-ns", type=int, default=6_000_000,
                     help="c5 (DES): mean gap of the open-loop Poisson arrivals")
     ap.add_argument("--mode", default="A", choices=["A", "B"])
+    ap.add_argument("--no-mode-b", action="store_true", help="c3: skip the extra mode-B legs")
+    ap.add_argument("--mode-b-steps", type=int, default=5, help="c3: timed steps of each extra mode-B leg")
     ap.add_argument("--no-records", action="store_true")
     ap.add_argument("--no-svc-dur", action="store_true",
                     help="dynamic walks: skip the per-service duration histograms")
@@ -60,8 +62,13 @@ def parse():
 
 def build_graph(config: str):
     from isim.generators import config2_topology, config3_topology, mesh_topology
-    from isim.yamljson import obj_to_json
-    if config == "c2":
+    from isim.yamljson import obj_to_json, yaml_to_json
+    if config == "c1":
+        j = yaml_to_json(open(os.path.join(ROOT, "tests", "golden", "topologies", "canonical.yaml"), "rb").read())
+        desc = {"workload": "isotope example-topologies/canonical.yaml as written (4 services, entry d, 6 "
+                            "invocations per trace), 1,000,000 traces",
+                "services": 4}
+    elif config == "c2":
         j = obj_to_json(config2_topology())
         desc = {"workload": "create_tree_topology.py tree depth 4 x fan-out 8, sequential requests (585 services)",
                 "services": 585}
@@ -259,11 +266,91 @@ def compute_roofline(stream: bool, info, B: int, kern_ms: float):
     if not stream or not os.path.exists(path):
         return None
     peak = json.load(open(path))["philox_blocks_per_s"]
-    blocks = B * -(-info.hops_upper // 4)
+    # only the groups of 4 invocations that hold an error draw cost a block
+    # (the kernel skips all-zero-threshold groups)
+    blocks = B * info.draw_groups
+    if blocks == 0:
+        return None
     achieved = blocks / (kern_ms * 1e-3)
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "Philox4x32-10 blocks/s",
             "frac": achieved / peak, "per_launch": blocks,
             "peak_source": "profiles/philox_peak.json (tools/philox_peak.hip)"}
+
+
+def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev):
+    """W untimed + K timed launches of isim_serve_device over B traces per
+    rank (trace ids sharded globally), then the stats all-reduce; returns
+    (max-over-ranks wall seconds of the K steps + merge, mean HIP-event
+    kernel ms on the launch stream)."""
+    import torch
+    import torch.distributed as dist
+
+    from isim.dist import merge_stats, shard_begin
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step(s):
+        begin = shard_begin(rank, world, s, B)
+        h.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), sptr)
+
+    for s in range(warmup):
+        step(s)
+    torch.cuda.synchronize()
+    stats.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        step(warmup + i)
+        ev[i][1].record(stream)
+    if world > 1:
+        merge_stats(stats)  # one RCCL all-reduce (SUM) + the 2-word extrema MAX
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms
+
+
+def mode_b_legs(args, json_text, rank, world, dev):
+    """Config 3 in error mode B (the propagating EXT variant of
+    executable.go:131-143): the same graph (every trace ends 500 at errorRate
+    U[0, 1 %]) and an informative variant (errorRate U[0, 1e-4], entry 500 in
+    ~40 % of the traces), both on the close-list kernel."""
+    import numpy as np
+    import torch
+
+    import isim
+    from isim.generators import realistic_topology
+    from isim.yamljson import obj_to_json
+    out = {}
+    graphs = {"mode_b": json_text,
+              "mode_b_informative": obj_to_json(realistic_topology(10_000, "multitier", 42, concurrent=True,
+                                                                   sleep_ms=(1, 5), error_rate=(0.0, 1e-4)))}
+    B = args.batch
+    recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
+    for key, j in graphs.items():
+        h = isim.Handler(isim.ServiceGraph.from_json(j), None,
+                         isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_WALK_ALL))
+        stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
+        steps = max(1, args.mode_b_steps)
+        elapsed, kern_ms = time_walk(h, steps, 1, B, recs, stats, rank, world, dev)
+        f = h.fold(stats.cpu().numpy().view(np.uint64))
+        total = steps * B * world
+        assert f["n_traces"] == total
+        out[key] = {"value": total / elapsed, "unit": "traces/s", "ms_per_step": elapsed * 1e3 / steps,
+                    "kernel_ms": kern_ms, "steps": steps, "n_500_frac": f["n_500"] / total,
+                    "kernel_kind": h.launch_info(torch.cuda.current_device())["kernel_kind"],
+                    "errorRate": "U[0,1%]" if key == "mode_b" else "U[0,1e-4]"}
+    return out
 
 
 def main():
@@ -295,44 +382,14 @@ def main():
         if args.batch == 1 << 22:
             args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
         return main_des(args, h, json_text, desc, params, rank, world, dev)
+    if args.config == "c1" and args.batch == 1 << 22:
+        args.batch = 1_000_000  # BASELINE config 1: 1M traces
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
     B = args.batch
     stats = torch.zeros(info.stats_words, dtype=torch.int64, device=dev)
     recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-
-    from isim.dist import merge_stats, shard_begin
-
-    def step(s):
-        begin = shard_begin(rank, world, s, B)
-        h.serve_device(begin, B, recs.data_ptr() if recs is not None else 0, stats.data_ptr(), sptr)
-
-    for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize()
-    stats.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step(args.warmup + i)
-        ev[i][1].record(stream)
-    if world > 1:
-        merge_stats(stats)  # one RCCL all-reduce (SUM) + the 2-word extrema MAX
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = time_walk(h, args.steps, args.warmup, B, recs, stats, rank, world, dev)
 
     host_stats = stats.cpu().numpy().view(np.uint64)
     folded = h.fold(host_stats)
@@ -388,8 +445,13 @@ def main():
         "hop_visits_per_s": value * hops_per_trace,
         "n_500_frac": folded["n_500"] / total,
     }
+    if args.config == "c3" and args.mode == "A" and not args.no_mode_b:
+        line.update(mode_b_legs(args, json_text, rank, world, dev))
     if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(json_text, params, args.cpu_traces, 0)
+        # config 1 is defined on the CPU interpreter: time it on the whole
+        # 1M-trace workload; other configs on a bounded sample
+        n_cpu = args.cpu_traces or (B if args.config == "c1" else 0)
+        line["cpu_baseline"] = cpu_baseline(json_text, params, n_cpu, 0)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

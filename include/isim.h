@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 5
+#define ISIM_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -88,6 +88,9 @@ typedef struct {
 #define ISIM_FLAG_WALK_ALL 4u   /* draw-free static walks: walk every trace (default: walk one, fill the rest) */
 #define ISIM_FLAG_BIT_STACK 8u  /* mode B on the draw stream: the bit-stack kernel (kind 5, call depth <= 32;
                                    kind 4 deeper) instead of the close-list kernel (kind 6) */
+#define ISIM_FLAG_DYNAMIC 16u   /* treat every walk as dynamic: the general kernel with per-lane time and hop
+                                   ids (kinds 2/3) even when every trace executes the same invocations
+                                   (parity tests of the general path on static graphs; no DES) */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -150,6 +153,8 @@ typedef struct {
   uint64_t stats_words;      /* u64 words of the stats buffer */
   int32_t svc_dur_rows;      /* rows of the device duration table (0: derived on the host) */
   int32_t n_reachable;       /* services reachable from the entry */
+  uint64_t draw_groups;      /* draw stream: groups of 4 invocations with an error draw (one Philox4x32-10
+                                block per trace each); 0 for draw-free and dynamic walks */
 } isim_handler_info;
 
 /* Launch configuration chosen for a device (filled on first use of that device). */
@@ -210,7 +215,12 @@ ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32
  * default stream).  d_records: device array of n_traces records or NULL.
  * d_stats: device array of info.stats_words u64; ACCUMULATED into (zero it
  * first; ~min word starts at 0).  No host synchronisation, no allocation:
- * graph-capturable after the first call on a device. */
+ * graph-capturable after the first call on a device.
+ * Concurrency limit: the walk kernels claim batches from per-launch queue
+ * sets that rotate over 256 sets per (handler, device); at most 256 launches
+ * of one handler may be in flight on one device at once (launches on ONE
+ * stream are ordered and never collide; with more than 256 streams in
+ * flight, order them with events or use one handler per stream). */
 ISIM_API int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces,
                       isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
 

@@ -50,6 +50,8 @@ struct DevState {
   isim_trace_rec const_rec{};
   uint32_t work_next = 0;                // next queue (launches in flight use distinct queues)
   void *kernel = nullptr;
+  void *kernel_global = nullptr;  // the same kind with per-site counters in global memory (LDS u32 overflow guard)
+  uint64_t max_mult = 0;          // largest per-trace count of one per-site counter (calls through a site)
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
   uint32_t lds_counters = 0;
@@ -62,6 +64,16 @@ struct DevState {
   uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr, *d_des_zero = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
 };
+
+void free_dev(DevState &d) {
+  for (void *q : {(void *)d.d_prog, (void *)d.d_mult, (void *)d.d_closes, (void *)d.d_close_end,
+                  (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_const_stats,
+                  d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
+                  (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
+                  d.d_des_ext, d.d_des_steps})
+    if (q) (void)hipFree(q);
+  d = DevState();
+}
 
 }  // namespace
 
@@ -82,24 +94,7 @@ struct isim_handler {
     for (auto &kv : dev) {
       int cur = 0;
       if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
-        (void)hipFree(kv.second.d_prog);
-        (void)hipFree(kv.second.d_mult);
-        (void)hipFree(kv.second.d_closes);
-        (void)hipFree(kv.second.d_close_end);
-        (void)hipFree(kv.second.d_close_slot);
-        (void)hipFree(kv.second.d_dur);
-        (void)hipFree(kv.second.d_work);
-        (void)hipFree(kv.second.d_const_stats);
-        (void)hipFree(kv.second.d_des_pos);
-        (void)hipFree(kv.second.d_des_child);
-        (void)hipFree(kv.second.d_des_level);
-        (void)hipFree(kv.second.d_des_mult);
-        (void)hipFree(kv.second.d_des_fast);
-        (void)hipFree(kv.second.d_des_zero);
-        (void)hipFree(kv.second.d_des_sort);
-        (void)hipFree(kv.second.d_des_arr);
-        (void)hipFree(kv.second.d_des_ext);
-        (void)hipFree(kv.second.d_des_steps);
+        free_dev(kv.second);
         (void)hipSetDevice(cur);
       }
     }
@@ -134,6 +129,8 @@ uint32_t lds_need(const isim::Program &p, uint32_t waves, bool counters) {
   return b;
 }
 
+int build_device(isim_handler *h, int device, DevState &st);
+
 int prepare_device(isim_handler *h, int device, DevState *&out) {
   std::lock_guard<std::mutex> lk(h->mu);
   auto it = h->dev.find(device);
@@ -141,12 +138,25 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
     out = &it->second;
     return ISIM_OK;
   }
+  DevState st;
+  const int rc = build_device(h, device, st);
+  if (rc != ISIM_OK) {
+    free_dev(st);  // one cleanup path for every allocation made before the failure
+    return rc;
+  }
+  auto res = h->dev.emplace(device, st);
+  out = &res.first->second;
+  return ISIM_OK;
+}
+
+// Chooses the kernel and launch shape for `device` and uploads the program.
+// On failure the caller frees whatever `st` holds.
+int build_device(isim_handler *h, int device, DevState &st) {
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, device));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(ISIM_ENODEV, std::string("libisim is built for gfx950 only; device is ") + prop.gcnArchName);
   const isim::Program &p = h->prog;
-  DevState st;
   // HIP reports 64 KiB per block by default; a gfx950 workgroup may use all
   // 160 KiB of the CU's LDS once the kernel attribute is raised.
   const uint32_t lds_max = (uint32_t)std::max<size_t>(prop.sharedMemPerBlock, prop.maxSharedMemoryPerMultiProcessor);
@@ -245,17 +255,22 @@ int prepare_device(isim_handler *h, int device, DevState *&out) {
     if (rc == ISIM_OK)
       rc = upload((void *&)st.d_close_end, p.stream_close_end.data(), p.stream_close_end.size() * sizeof(uint32_t),
                   2 * sizeof(uint32_t));
-    if (rc != ISIM_OK) {
-      (void)hipFree(st.d_closes);
-      (void)hipFree(st.d_close_slot);
-      (void)hipFree(st.d_close_end);
-      return rc;
-    }
+    if (rc != ISIM_OK) return rc;
   }
   HIPCHK(hipMalloc(&st.d_work, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   HIPCHK(hipMemset(st.d_work, 0, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
-  auto res = h->dev.emplace(device, st);
-  out = &res.first->second;
+  // per-workgroup LDS site counters are u32: a launch whose traces could push
+  // one past 2^32 (n_traces x calls through one site per trace) runs the
+  // global-u64-atomic variant of the same kernel instead (launch_walk)
+  st.max_mult = p.hops_upper;
+  if (st.kind >= 4) {
+    st.max_mult = 1;
+    for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
+  }
+  st.kernel_global = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, false);
+  if (st.lds_counters)
+    HIPCHK(hipFuncSetAttribute((const void *)st.kernel_global, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)st.lds_bytes));
   return ISIM_OK;
 }
 
@@ -395,6 +410,9 @@ int isim_handler_info_get(const isim_handler *h, isim_handler_info *out) {
   out->stats_words = stats_words(h);
   out->svc_dur_rows = (int32_t)svc_dur_rows(h);
   out->n_reachable = (int32_t)p.row_svc.size();
+  out->draw_groups = 0;
+  for (size_t g = 0; g + 3 < p.stream.size(); g += 4)
+    out->draw_groups += (p.stream[g].thr | p.stream[g + 1].thr | p.stream[g + 2].thr | p.stream[g + 3].thr) != 0;
   return ISIM_OK;
 }
 
@@ -425,8 +443,30 @@ int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32_t *slot_
   return ISIM_OK;
 }
 
+static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
+                           isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
+
+// Per-workgroup LDS accumulators are u32: histogram counts (at most the
+// launch's traces) and, with LDS site counters, per-site counts (at most
+// traces x calls through the site per trace).  Launches are split below 2^31
+// traces, and a launch that could wrap a site counter takes the
+// global-atomic kernel.
 static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
                        isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
+  constexpr uint64_t kMaxLaunch = 1ull << 31;
+  for (uint64_t done = 0; done < n_traces;) {
+    const uint64_t n = std::min(n_traces - done, kMaxLaunch);
+    const int rc = launch_walk_one(h, st, trace_begin + done, n, d_records ? d_records + done : nullptr, d_stats,
+                                   hip_stream);
+    if (rc != ISIM_OK) return rc;
+    done += n;
+  }
+  return ISIM_OK;
+}
+
+static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
+                           isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
+  const bool wrap = st->lds_counters && (unsigned __int128)n_traces * st->max_mult >= (1ull << 32);
   isim::KParams kp{};
   kp.trace_begin = trace_begin;
   kp.n_traces = n_traces;
@@ -434,7 +474,7 @@ static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint
   kp.seed_hi = (uint32_t)(h->params.seed >> 32);
   kp.n_slots = (uint32_t)h->prog.n_slots;
   kp.max_frames = (uint32_t)h->prog.max_frames;
-  kp.lds_counters = st->lds_counters;
+  kp.lds_counters = wrap ? 0u : st->lds_counters;
   kp.n_nodes = h->prog.stream_nodes;
   kp.t_static = h->prog.max_latency;
   kp.svc_dur = svc_dur_rows(h) ? 1u : 0u;
@@ -451,7 +491,7 @@ static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
-  HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
+  HIPCHK(hipLaunchKernel(wrap ? st->kernel_global : st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
                          (hipStream_t)hip_stream));
   if (st->kind >= 4 && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;

@@ -199,7 +199,7 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
   out.n_sites = (int32_t)sites.size();
   out.max_depth = depth[entry];
   out.max_frames = std::max(1, frames[entry]);
-  out.static_walk = !any_prob && !(modeb && nonstatic_abort);
+  out.static_walk = !any_prob && !(modeb && nonstatic_abort) && !(p.flags & ISIM_FLAG_DYNAMIC);
   out.max_latency = tmax[entry];
   out.hops_upper = hops[entry];
   out.time_bits = tmax[entry] < (1ull << 32) ? 32 : 64;

@@ -22,11 +22,12 @@ OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = ra
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 5  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 6  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
 FLAG_BIT_STACK = 8  # mode B on the draw stream: the bit-stack kernel (kind 5/4) instead of the close list (6)
+FLAG_DYNAMIC = 16  # every walk on the general (dynamic) kernel, kinds 2/3
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4
@@ -66,7 +67,8 @@ class HandlerInfo(C.Structure):
                 ("entry", C.c_int32), ("max_depth", C.c_int32), ("static_walk", C.c_int32),
                 ("time_bits", C.c_int32), ("program_len", C.c_int32),
                 ("max_latency_ns", C.c_uint64), ("hops_upper", C.c_uint64),
-                ("stats_words", C.c_uint64), ("svc_dur_rows", C.c_int32), ("n_reachable", C.c_int32)]
+                ("stats_words", C.c_uint64), ("svc_dur_rows", C.c_int32), ("n_reachable", C.c_int32),
+                ("draw_groups", C.c_uint64)]
 
 
 class LaunchInfo(C.Structure):

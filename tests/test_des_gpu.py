@@ -104,6 +104,16 @@ def test_config5_slice(gpu):
     c.compare(0, 256)
 
 
+def test_config5_bench_scale(gpu):
+    """The config-5 graph on a batch that crosses the chained look-back of the
+    narrow queue pass (chunks of 4,096 traces) and the arrival scan's blocks
+    (8,192 traces) several times, with a ragged tail: 20,000 traces, bit-exact
+    against the event-driven DES oracle (about 30 s of oracle time)."""
+    c = DesCase(config3_topology(), 6_000_000)
+    recs, _, rows = c.compare(1000, 20_000)
+    assert int(rows[:, isim.native.DES_SUM_WAIT].sum()) > 0  # the queues are contended
+
+
 @pytest.mark.parametrize("wide", [False, True])
 def test_device_entry_accumulates(gpu, wide):
     import torch

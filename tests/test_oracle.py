@@ -9,7 +9,8 @@ import pytest
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
-from conftest import GOLDEN, TOPOLOGIES
+import kat
+from conftest import GOLDEN
 from oracle import executor as oc
 from oracle import executor_py as ex
 from oracle import gounits as gu
@@ -17,7 +18,6 @@ from oracle import graph_ref as gr
 from oracle import philox
 
 VEC = json.load(open(os.path.join(GOLDEN, "go_vectors.json")))
-KAT = json.load(open(os.path.join(GOLDEN, "executor_kat.json")))
 PHX = json.load(open(os.path.join(GOLDEN, "philox_kat.json")))
 
 
@@ -157,33 +157,24 @@ def test_philox_kat(case):
     assert oc.philox(ctr, key) == want
 
 
-def _kat_graph(name):
-    from isim.generators import tree_topology
-    from isim.yamljson import obj_to_json, yaml_to_json
-    if name.startswith("topology:"):
-        return yaml_to_json(open(os.path.join(TOPOLOGIES, name.split(":", 1)[1]), "rb").read())
-    if name.startswith("tree:"):
-        _, shape, kind = name.split(":")
-        lv, br = map(int, shape.split("x"))
-        return obj_to_json(tree_topology(lv, br, sequential=(kind == "sequential")))
-    return KAT["graphs"][name]
-
-
-@pytest.mark.parametrize("case", KAT["cases"], ids=lambda c: f"{c['graph']}-{c['entry']}-{c['hop_ns']}")
+@pytest.mark.parametrize("case", kat.CASES, ids=kat.case_id)
 def test_executor_kat(case):
-    g = gr.unmarshal_service_graph(_kat_graph(case["graph"]))
+    import isim
+    j = kat.graph_json(case["graph"])
+    g = gr.unmarshal_service_graph(j)
     sg = ex.SimGraph(g)
-    p = ex.SimParams(seed=1, hop_base_ns=case["hop_ns"], req_ps_per_byte=0, resp_ps_per_byte=0)
+    hop, req, resp, mode = kat.params(case)
+    p = ex.SimParams(seed=1, hop_base_ns=hop, req_ps_per_byte=req, resp_ps_per_byte=resp, error_mode=mode)
     e = sg.entry(case["entry"])
     recs, st = ex.run(sg, p, e, 0, 1)
-    assert recs[0][0] == case["latency"] and recs[0][1] == case["hops"]
-    crec, cst = oc.run(sg, p, e, 0, 1)
-    assert int(crec[0, 0]) == case["latency"] and int(crec[0, 1]) & 0xFFFFFFFF == case["hops"]
-    calls = {s.name: n for s, n in zip(g.services, st.svc_calls) if n}
-    if "calls" in case:
-        assert calls == case["calls"]
-    else:
-        assert set(calls.values()) == {case["calls_each"]} and len(calls) == case["hops"]
+    kat.check_record(case, *recs[0][:2], recs[0][2], recs[0][3])
+    crec, cst = oc.run(sg, p, e, 0, 3)
+    for r in crec:
+        kat.check_record(case, int(r[0]), int(r[1]) & 0xFFFFFFFF, int(r[1]) >> 63, (int(r[1]) >> 32) & 0x7FFFFFFF)
+    names = [s.name for s in g.services]
+    kat.check_folded(case, names, {"svc_calls": st.svc_calls, "svc_errs": st.svc_errs, "site_calls": st.site_calls}, 1,
+                     isim.ServiceGraph.from_json(j))
+    kat.check_folded(case, names, oc.split_stats(cst, len(g.services), len(sg.sites)), 3)
 
 
 # ---- pure-Python executor vs C executor on random small graphs -------------

@@ -125,6 +125,18 @@ def test_realistic_config3(gpu, kernel):
         Case(j, None, isim.SimParams(error_mode=mode, flags=KERNELS[kernel])).compare(1 << 20, 1024)
 
 
+@pytest.mark.parametrize("kernel", list(KERNELS))
+def test_config3_mode_b_informative(gpu, kernel):
+    """Mode B on config 3's graph with errorRate U[0, 1e-4]: the entry's status
+    is 200 in some traces and 500 in others (20-80 %), so the close-list
+    kernel's subtree tests decide real outcomes at 10k-service scale."""
+    from test_fullsize_gpu import config3_informative
+    c = Case(config3_informative(), None, isim.SimParams(error_mode=isim.MODE_B, flags=KERNELS[kernel]))
+    recs, _ = c.compare(1 << 30, 4096)
+    frac = float((recs["status_err"] >> 31).mean())
+    assert 0.2 < frac < 0.8, frac
+
+
 def test_realistic_sequential_probability(gpu):
     d = realistic_topology(2000, "multitier", seed=3, concurrent=False, sleep_ms=(1, 5), error_rate=(0, 0.05))
     for i, s in enumerate(d["services"]):
@@ -229,3 +241,29 @@ def test_draw_free_fill(gpu, mode, n):
     assert np.array_equal(r1, r2) and np.array_equal(s1, s2)
     if n <= 1000:
         fill.compare(3, n)
+
+
+def test_site_counter_beyond_u32(gpu):
+    """Per-workgroup LDS site counters are u32: a binary DAG chain whose leaf
+    is called 2^22 times per trace pushes one workgroup's leaf-error counter
+    (2,048 traces x 2^22) past 2^32, so the library must run the global-u64
+    counter variant of the kernel (api.hip launch_walk).  Expected numbers are
+    analytic: every trace makes 2^23 - 1 invocations, 2^22 of them the
+    errorRate-1 leaf."""
+    depth = 22
+    svcs = [{"name": f"s{i}", "script": [{"call": f"s{i + 1}"}, {"call": f"s{i + 1}"}]} for i in range(depth)]
+    svcs.append({"name": f"s{depth}", "errorRate": 1.0})
+    svcs[0]["isEntrypoint"] = True
+    h = isim.Handler(isim.ServiceGraph.from_json(json.dumps({"services": svcs})), None,
+                     isim.SimParams(hop_base_ns=1, req_ps_per_byte=0, resp_ps_per_byte=0,
+                                    flags=isim.native.FLAG_WALK_ALL))
+    assert h.launch_info(0)["kernel_kind"] == 4 and h.launch_info(0)["lds_counters"] == 1
+    n = 4200
+    recs, stats = h.serve(0, n)
+    inv, leaf = (1 << (depth + 1)) - 1, 1 << depth
+    assert np.all(recs["hops"] == inv) and np.all(recs["latency_ns"] == inv - 1)
+    assert np.all(recs["status_err"] == leaf)  # entry 200 (mode A), 2^22 erring leaves
+    f = h.fold(stats)
+    assert int(f["svc_calls"][depth]) == n * leaf and int(f["svc_errs"][depth]) == n * leaf
+    assert n * leaf > 1 << 32
+    assert int(f["svc_errs"][:depth].sum()) == 0 and int(f["svc_calls"][0]) == n
