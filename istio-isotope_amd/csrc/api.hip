@@ -50,8 +50,7 @@ struct DevState {
   isim_trace_rec const_rec{};
   uint32_t work_next = 0;                // next queue (launches in flight use distinct queues)
   void *kernel = nullptr;
-  void *kernel_global = nullptr;  // the same kind with per-site counters in global memory (LDS u32 overflow guard)
-  uint64_t max_mult = 0;          // largest per-trace count of one per-site counter (calls through a site)
+  uint64_t max_mult = 0;  // largest per-trace count of one per-site counter (calls through a site)
   uint32_t threads = 0;
   uint32_t lds_bytes = 0;
   uint32_t lds_counters = 0;
@@ -259,18 +258,14 @@ int build_device(isim_handler *h, int device, DevState &st) {
   }
   HIPCHK(hipMalloc(&st.d_work, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   HIPCHK(hipMemset(st.d_work, 0, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
-  // per-workgroup LDS site counters are u32: a launch whose traces could push
-  // one past 2^32 (n_traces x calls through one site per trace) runs the
-  // global-u64-atomic variant of the same kernel instead (launch_walk)
-  st.max_mult = p.hops_upper;
+  // per-workgroup LDS site counters are u32: launch_walk splits a batch so
+  // that no workgroup can count past 2^32 at one site (traces x calls
+  // through the site per trace)
+  st.max_mult = std::max<uint64_t>(1, p.hops_upper);
   if (st.kind >= 4) {
     st.max_mult = 1;
     for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
   }
-  st.kernel_global = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, false);
-  if (st.lds_counters)
-    HIPCHK(hipFuncSetAttribute((const void *)st.kernel_global, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)st.lds_bytes));
   return ISIM_OK;
 }
 
@@ -448,12 +443,15 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
 
 // Per-workgroup LDS accumulators are u32: histogram counts (at most the
 // launch's traces) and, with LDS site counters, per-site counts (at most
-// traces x calls through the site per trace).  Launches are split below 2^31
-// traces, and a launch that could wrap a site counter takes the
-// global-atomic kernel.
+// traces x calls through the site per trace; a workgroup may claim any
+// share of a launch's batches).  Launches are split so neither can wrap:
+// below 2^31 traces, and below 2^32 / max_mult traces with LDS counters (a
+// DAG whose shared callee is reached 2^22 times per trace: 1,023 traces per
+// launch).  Global counters are u64 atomics and need no split.
 static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
                        isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
-  constexpr uint64_t kMaxLaunch = 1ull << 31;
+  uint64_t kMaxLaunch = 1ull << 31;
+  if (st->lds_counters) kMaxLaunch = std::min<uint64_t>(kMaxLaunch, std::max<uint64_t>(1, 0xFFFFFFFFull / st->max_mult));
   for (uint64_t done = 0; done < n_traces;) {
     const uint64_t n = std::min(n_traces - done, kMaxLaunch);
     const int rc = launch_walk_one(h, st, trace_begin + done, n, d_records ? d_records + done : nullptr, d_stats,
@@ -466,7 +464,6 @@ static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint
 
 static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
                            isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
-  const bool wrap = st->lds_counters && (unsigned __int128)n_traces * st->max_mult >= (1ull << 32);
   isim::KParams kp{};
   kp.trace_begin = trace_begin;
   kp.n_traces = n_traces;
@@ -474,7 +471,7 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.seed_hi = (uint32_t)(h->params.seed >> 32);
   kp.n_slots = (uint32_t)h->prog.n_slots;
   kp.max_frames = (uint32_t)h->prog.max_frames;
-  kp.lds_counters = wrap ? 0u : st->lds_counters;
+  kp.lds_counters = st->lds_counters;
   kp.n_nodes = h->prog.stream_nodes;
   kp.t_static = h->prog.max_latency;
   kp.svc_dur = svc_dur_rows(h) ? 1u : 0u;
@@ -491,8 +488,7 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
-  HIPCHK(hipLaunchKernel(wrap ? st->kernel_global : st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes,
-                         (hipStream_t)hip_stream));
+  HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, (hipStream_t)hip_stream));
   if (st->kind >= 4 && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;

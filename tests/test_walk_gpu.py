@@ -246,8 +246,8 @@ def test_draw_free_fill(gpu, mode, n):
 def test_site_counter_beyond_u32(gpu):
     """Per-workgroup LDS site counters are u32: a binary DAG chain whose leaf
     is called 2^22 times per trace pushes one workgroup's leaf-error counter
-    (2,048 traces x 2^22) past 2^32, so the library must run the global-u64
-    counter variant of the kernel (api.hip launch_walk).  Expected numbers are
+    (2,048 traces x 2^22) past 2^32, so the library must split the launch
+    (api.hip launch_walk: 1,023 traces per launch here).  Expected numbers are
     analytic: every trace makes 2^23 - 1 invocations, 2^22 of them the
     errorRate-1 leaf."""
     depth = 22
