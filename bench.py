@@ -131,7 +131,7 @@ def cpu_baseline_des(json_text: str, params, mean_ns: int, n_traces: int):
             "hop_visits_per_s": float(st[2]) / dt}
 
 
-def main_des(args, h, json_text, desc, params, rank, world, dev):
+def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, merge_label=""):
     """BASELINE config 5: one step = one DES batch of --batch traces per rank
     (arrivals from time 0, replicas idle), all kernels on one stream.  The DES
     does not shard a batch: with N ranks each runs an independent replica
@@ -142,7 +142,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
     import torch.distributed as dist
 
     import isim
-    from isim.dist import merge_stats, shard_begin
+    from isim.dist import shard_begin
 
     d = isim.DesHandler(h, args.mean_interarrival_ns)
     B = args.batch
@@ -190,7 +190,9 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
             break
         wide[0] = True  # a timed batch overflowed the 32-bit rows: time the run again with 64-bit rows
     if world > 1:
-        merge_stats(stats)
+        merge(h, multi, stats, sptr)
+        if multi is not None:
+            multi.allreduce_des_table(h, [table.data_ptr()], [sptr])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -235,7 +237,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev):
         "config": dict(desc, global_batch=B * world, traces_per_rank_per_step=B, error_mode=args.mode,
                        hop_visits_per_trace=folded["sum_hops"] / total,
                        mean_interarrival_ns=args.mean_interarrival_ns,
-                       parallelism=f"replicas x{world}", records=not args.no_records,
+                       parallelism=f"replicas x{world}", merge=merge_label, records=not args.no_records,
                        des_levels=d.info.n_levels, des_max_width=d.info.max_width,
                        des_fused_leaves=d.info.n_fused, des_rows="u64" if wide[0] else "u32",
                        workspace_bytes=wsb),
@@ -277,7 +279,34 @@ def compute_roofline(stream: bool, info, B: int, kern_ms: float):
             "peak_source": "profiles/philox_peak.json (tools/philox_peak.hip)"}
 
 
-def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev):
+def make_multi(rank, world, local):
+    """libisim's RCCL communicator for the stats merge (isim_multi_init_rank;
+    the 128-byte id travels over torch.distributed, as a Go host would send it
+    out of band).  Returns (Multi or None, merge label)."""
+    import torch.distributed as dist
+
+    from isim.dist import Multi
+    if world == 1:
+        return None, "none (1 rank)"
+    try:
+        obj = [Multi.get_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return Multi.init_rank(obj[0], world, rank, local), "isim_stats_allreduce_device (libisim RCCL)"
+    except Exception as e:  # reported in the JSON line: the torch RCCL merge is used instead
+        print(f"isim_multi_init_rank failed ({e}); merging with torch.distributed", file=sys.stderr)
+        return None, f"torch.distributed all_reduce (isim_multi_init_rank failed: {e})"
+
+
+def merge(h, multi, stats, sptr):
+    """SUM + extrema MAX of the per-rank stats buffers, on the launch stream."""
+    from isim.dist import merge_stats
+    if multi is not None:
+        multi.allreduce_stats(h, [stats.data_ptr()], [sptr])
+    else:
+        merge_stats(stats)
+
+
+def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev, multi=None):
     """W untimed + K timed launches of isim_serve_device over B traces per
     rank (trace ids sharded globally), then the stats all-reduce; returns
     (max-over-ranks wall seconds of the K steps + merge, mean HIP-event
@@ -285,7 +314,7 @@ def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev):
     import torch
     import torch.distributed as dist
 
-    from isim.dist import merge_stats, shard_begin
+    from isim.dist import shard_begin
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -307,7 +336,7 @@ def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev):
         step(warmup + i)
         ev[i][1].record(stream)
     if world > 1:
-        merge_stats(stats)  # one RCCL all-reduce (SUM) + the 2-word extrema MAX
+        merge(h, multi, stats, sptr)  # one RCCL all-reduce (SUM) + the 2-word extrema MAX
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -320,7 +349,7 @@ def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev):
     return elapsed, kern_ms
 
 
-def mode_b_legs(args, json_text, rank, world, dev):
+def mode_b_legs(args, json_text, rank, world, dev, multi=None):
     """Config 3 in error mode B (the propagating EXT variant of
     executable.go:131-143): the same graph (every trace ends 500 at errorRate
     U[0, 1 %]) and an informative variant (errorRate U[0, 1e-4], entry 500 in
@@ -342,7 +371,7 @@ def mode_b_legs(args, json_text, rank, world, dev):
                          isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_WALK_ALL))
         stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
         steps = max(1, args.mode_b_steps)
-        elapsed, kern_ms = time_walk(h, steps, 1, B, recs, stats, rank, world, dev)
+        elapsed, kern_ms = time_walk(h, steps, 1, B, recs, stats, rank, world, dev, multi)
         f = h.fold(stats.cpu().numpy().view(np.uint64))
         total = steps * B * world
         assert f["n_traces"] == total
@@ -371,6 +400,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    multi, merge_label = make_multi(rank, world, local)
     json_text, desc = build_graph(args.config)
     # every trace is walked unless --fill: a draw-free static walk (config 2)
     # is otherwise walked once and filled, which is not a walk rate
@@ -381,7 +411,7 @@ def main():
     if args.config == "c5":
         if args.batch == 1 << 22:
             args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
-        return main_des(args, h, json_text, desc, params, rank, world, dev)
+        return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
     if args.config == "c1" and args.batch == 1 << 22:
         args.batch = 1_000_000  # BASELINE config 1: 1M traces
     info = h.info
@@ -389,7 +419,7 @@ def main():
     B = args.batch
     stats = torch.zeros(info.stats_words, dtype=torch.int64, device=dev)
     recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
-    elapsed, kern_ms = time_walk(h, args.steps, args.warmup, B, recs, stats, rank, world, dev)
+    elapsed, kern_ms = time_walk(h, args.steps, args.warmup, B, recs, stats, rank, world, dev, multi)
 
     host_stats = stats.cpu().numpy().view(np.uint64)
     folded = h.fold(host_stats)
@@ -433,7 +463,7 @@ def main():
         "data": "synthetic",
         "config": dict(desc, global_batch=B * world, traces_per_rank_per_step=B,
                        error_mode=args.mode, hop_visits_per_trace=hops_per_trace,
-                       parallelism=f"trace-shard x{world}", records=not args.no_records,
+                       parallelism=f"trace-shard x{world}", merge=merge_label, records=not args.no_records,
                        static_walk=bool(info.static_walk), program_len=info.program_len,
                        launch=launch),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -446,7 +476,7 @@ def main():
         "n_500_frac": folded["n_500"] / total,
     }
     if args.config == "c3" and args.mode == "A" and not args.no_mode_b:
-        line.update(mode_b_legs(args, json_text, rank, world, dev))
+        line.update(mode_b_legs(args, json_text, rank, world, dev, multi))
     if rank == 0 and world == 1 and not args.no_cpu:
         # config 1 is defined on the CPU interpreter: time it on the whole
         # 1M-trace workload; other configs on a bounded sample

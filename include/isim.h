@@ -23,6 +23,11 @@
  *                                 run for n_traces independent client requests
  *                                 in virtual integer-nanosecond time
  *   stats words                <- prometheus.Record* isotope/service/pkg/srv/prometheus/handler.go:87-106
+ *   isim_multi_* / isim_stats_allreduce_device / isim_stats_merge
+ *                              <- the per-pod Prometheus scrape of those counters
+ *                                 (prometheus/handler.go:37-69, one registry per
+ *                                 pod): here one RCCL all-reduce over the ranks
+ *                                 that each walked a shard of the traces
  *
  * Semantics: "isim semantics v1" (SURVEY.md Appendix A).
  * Errors: every function returns an isim_status; isim_last_error() gives a
@@ -40,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 6
+#define ISIM_ABI_VERSION 7
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -58,7 +63,8 @@ typedef enum {
   ISIM_EDEPTH = 6,   /* call depth above isim_params.max_depth (<= 64) */
   ISIM_ERANGE = 7,   /* hop cost / latency bound overflows int64 */
   ISIM_ENOTFOUND = 8,/* service name not in graph */
-  ISIM_ENODEV = 9    /* no usable gfx950 device */
+  ISIM_ENODEV = 9,   /* no usable gfx950 device */
+  ISIM_ECOMM = 10    /* RCCL error, or RCCL cannot be loaded (isim_multi_*) */
 } isim_status;
 
 /* Error propagation mode. */
@@ -294,6 +300,48 @@ ISIM_API int isim_serve_des(isim_handler *h, int device, const isim_des_params *
                    uint64_t n_traces, isim_trace_rec *h_records, uint64_t *h_stats, uint64_t *h_des_table);
 /* DES table rows -> svc_rows[n_services][ISIM_DES_ROW_WORDS] (zero for unreachable services). */
 ISIM_API int isim_des_fold(const isim_handler *h, const uint64_t *des_table, uint64_t *svc_rows);
+
+/* ---- multi-device: trace shards + one RCCL all-reduce ----
+ * north_star: traces shard evenly across the GPUs of a node; the histograms
+ * and counters merge with one RCCL all-reduce over xGMI.  An isim_multi is an
+ * RCCL communicator with one or more LOCAL devices: one process per GPU
+ * (isim_multi_init_rank, the id exchanged out of band, e.g. by the Go host)
+ * or one process driving several GPUs (isim_multi_init_all).  Global rank r
+ * walks the shard [trace_begin + r*n_per_rank, +n_per_rank); Philox keys use
+ * the global trace id, so any rank count gives identical per-trace results.
+ * The merge is SUM over every stats word except [~min, max], which merge by
+ * MAX; DES tables (isim_des_table_allreduce_device) SUM except
+ * ISIM_DES_MAX_WAIT (MAX).  RCCL is loaded at run time (dlopen of
+ * librccl.so.1) on the first isim_multi_* call; ISIM_ECOMM if it cannot be. */
+typedef struct isim_multi isim_multi;
+typedef struct {
+  char internal[128];            /* an ncclUniqueId */
+} isim_multi_id;
+/* New communicator id (on ONE process; send its 128 bytes to every rank). */
+ISIM_API int isim_multi_get_id(isim_multi_id *id);
+/* This process is rank `rank` of n_ranks, on HIP device `device` (ncclCommInitRank; collective over the ranks). */
+ISIM_API int isim_multi_init_rank(const isim_multi_id *id, int n_ranks, int rank, int device, isim_multi **out);
+/* One process, n_devices local devices = ranks 0..n-1 in the order given (ncclCommInitAll). */
+ISIM_API int isim_multi_init_all(const int *devices, int n_devices, isim_multi **out);
+ISIM_API void isim_multi_free(isim_multi *m);
+ISIM_API int isim_multi_info(const isim_multi *m, int *n_ranks, int *n_local, int *first_rank);
+/* In-place all-reduce of the stats buffers of the local devices (d_stats[i]
+ * on local device i, enqueued on hip_streams[i]; hip_streams may be NULL =
+ * default streams).  Asynchronous; collective over all ranks. */
+ISIM_API int isim_stats_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *const *d_stats,
+                                void *const *hip_streams);
+/* The same for DES tables (n_reachable * ISIM_DES_ROW_WORDS words each). */
+ISIM_API int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *const *d_tables,
+                                    void *const *hip_streams);
+/* Synchronous sharded batch: every local device walks its rank's shard; the
+ * merged stats (identical on every rank) go to h_stats, the local shards'
+ * records (n_local * n_per_rank, local device order) to h_records; either may
+ * be NULL.  Collective over all ranks. */
+ISIM_API int isim_serve_multi(isim_handler *h, isim_multi *m, uint64_t trace_begin, uint64_t n_per_rank,
+                     isim_trace_rec *h_records, uint64_t *h_stats);
+/* Host-side merges (the same rules): dst += src. */
+ISIM_API int isim_stats_merge(const isim_handler *h, uint64_t *dst, const uint64_t *src);
+ISIM_API int isim_des_table_merge(const isim_handler *h, uint64_t *dst, const uint64_t *src);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,15 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
+}  // namespace
+
+namespace isim {
+// error reporting of the other C-ABI translation units (multi.hip)
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace isim
+
+namespace {
+
 #define HIPCHK(expr)                                                                  \
   do {                                                                                \
     hipError_t e_ = (expr);                                                           \
@@ -85,6 +94,10 @@ struct isim_handler {
   isim_params params{};
   std::mutex mu;
   std::map<int, DevState> dev;
+  // the DES plan is built on first use (des_ensure): it unrolls the whole
+  // invocation tree, which walks never need
+  isim::ServiceGraph graph;
+  std::mutex des_mu;
   bool des_built = false;
   int des_rc = ISIM_OK;
   std::string des_err;
@@ -371,14 +384,7 @@ int isim_handler_create(const isim_graph *g, const char *service_name, const isi
   h->params = *p;
   std::string err;
   int rc = isim::compile_program(g->g, entry, *p, h->prog, err);
-  if (rc == ISIM_OK) {
-    // the DES plan is built from the graph and the program; build it now
-    // (host only, cheap) so the handler does not keep the graph
-    rc = isim::build_des_plan(g->g, h->prog, h->des, h->des_err);
-    h->des_rc = rc;
-    h->des_built = true;
-    rc = ISIM_OK;
-  }
+  if (rc == ISIM_OK) h->graph = g->g;  // for the DES plan (des_ensure); the caller may free g
   if (rc != ISIM_OK) {
     delete h;
     return fail(rc, err);
@@ -647,10 +653,23 @@ int isim_stats_fold_durations(const isim_handler *h, const uint64_t *stats, uint
 // ---- DES (BASELINE config 5) --------------------------------
 namespace {
 
+// Builds the DES plan on first use (host only); ISIM_OK or the reason the
+// graph is outside the DES class.
+int des_ensure(const isim_handler *hc) {
+  isim_handler *h = const_cast<isim_handler *>(hc);
+  std::lock_guard<std::mutex> lk(h->des_mu);
+  if (!h->des_built) {
+    h->des_rc = isim::build_des_plan(h->graph, h->prog, h->des, h->des_err);
+    h->des_built = true;
+  }
+  return h->des_rc == ISIM_OK ? ISIM_OK : fail(h->des_rc, h->des_err);
+}
+
 int des_prepare(isim_handler *h, int device, DevState *&st) {
-  int rc = prepare_device(h, device, st);
+  int rc = des_ensure(h);
   if (rc != ISIM_OK) return rc;
-  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  rc = prepare_device(h, device, st);
+  if (rc != ISIM_OK) return rc;
   std::lock_guard<std::mutex> lk(h->mu);
   if (st->d_des_pos) return ISIM_OK;
   const isim::DesPlan &d = h->des;
@@ -679,7 +698,7 @@ extern "C" {
 int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   if (!h || !out) return fail(ISIM_EINVAL, "null argument");
   std::memset(out, 0, sizeof(*out));
-  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  if (const int drc = des_ensure(h)) return drc;
   out->n_positions = (int32_t)h->des.pos.size();
   out->n_levels = (int32_t)h->des.n_levels;
   out->max_width = (int32_t)h->des.max_width;
@@ -691,7 +710,7 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
 
 int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
   if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
-  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  if (const int drc = des_ensure(h)) return drc;
   *bytes = isim::des_workspace_bytes(h->des, n_traces, stats_words(h), h->prog.row_svc.size());
   return ISIM_OK;
 }
@@ -759,7 +778,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
 int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint64_t trace_begin, uint64_t n_traces,
                    isim_trace_rec *h_records, uint64_t *h_stats, uint64_t *h_des_table) {
   if (!h || !dp) return fail(ISIM_EINVAL, "null argument");
-  if (h->des_rc != ISIM_OK) return fail(h->des_rc, h->des_err);
+  if (const int drc = des_ensure(h)) return drc;
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   HIPCHK(hipSetDevice(device));

@@ -20,6 +20,7 @@ namespace isim {
 
 constexpr uint32_t kDesNoParent = 0xFFFFFFFFu;
 constexpr uint32_t kDesMaxReplicas = 64;  // per-replica carries of a leaf position live in LDS
+constexpr uint32_t kDesMaxRounds = 65536; // schedule length limit (each round is a few launches per batch)
 constexpr uint32_t kDesFlagAlways = 1u;   // errorRate 1
 constexpr uint32_t kDesFlagLeaf = 2u;     // no call step
 constexpr uint32_t kDesFlagFused = 4u;    // fast-path leaf: finished by its queue pass (no up pass)

@@ -283,24 +283,44 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       if (pl.size() != before) out.cyclic = true;
     }
   }
-  // longest path by relaxation (acyclic now)
+  // longest path in topological order (acyclic now): O(ops + edges).  A
+  // relaxation sweep in op-index order needed one sweep per link of the
+  // longest chain, and sequential call steps chain every position of the
+  // tree (quadratic in the positions of a deep DAG)
   std::vector<uint32_t> rnd(n_ops, 0);
-  bool changed = true;
-  uint32_t pass = 0;
-  while (changed) {
-    changed = false;
-    if (++pass > n_ops + 2) {
+  {
+    std::vector<uint32_t> indeg(n_ops, 0), succ_off(n_ops + 1, 0);
+    for (uint32_t o = 0; o < n_ops; ++o)
+      for (auto &e : pred[o]) {
+        ++indeg[o];
+        ++succ_off[e.first + 1];
+      }
+    for (uint32_t o = 0; o < n_ops; ++o) succ_off[o + 1] += succ_off[o];
+    std::vector<std::pair<uint32_t, uint32_t>> succ(succ_off[n_ops]);
+    {
+      std::vector<uint32_t> at(succ_off.begin(), succ_off.end() - 1);
+      for (uint32_t o = 0; o < n_ops; ++o)
+        for (auto &e : pred[o]) succ[at[e.first]++] = {o, e.second};
+    }
+    std::vector<uint32_t> ready;
+    for (uint32_t o = 0; o < n_ops; ++o)
+      if (used[o] && indeg[o] == 0) ready.push_back(o);
+    size_t done = 0;
+    while (!ready.empty()) {
+      const uint32_t o = ready.back();
+      ready.pop_back();
+      ++done;
+      for (uint32_t j = succ_off[o]; j < succ_off[o + 1]; ++j) {
+        const uint32_t w = succ[j].first;
+        rnd[w] = std::max(rnd[w], rnd[o] + succ[j].second);
+        if (--indeg[w] == 0) ready.push_back(w);
+      }
+    }
+    size_t n_used = 0;
+    for (uint32_t o = 0; o < n_ops; ++o) n_used += used[o] ? 1 : 0;
+    if (done != n_used) {
       err = "DES schedule: dependency cycle left after removing back edges (internal error)";
       return ISIM_EINVAL;
-    }
-    for (uint32_t o = 0; o < n_ops; ++o) {
-      if (!used[o]) continue;
-      uint32_t r = 0;
-      for (auto &e : pred[o]) r = std::max(r, rnd[e.first] + e.second);
-      if (r != rnd[o]) {
-        rnd[o] = r;
-        changed = true;
-      }
     }
   }
   uint32_t R = 0;
@@ -311,10 +331,17 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     for (uint32_t v = 0; v < np; ++v) rnd[F(v)] = R;
     R += 1;
   }
+  if (R > kDesMaxRounds) {
+    // every round is a few launches over the whole batch: a schedule this
+    // long (sequential call steps chaining a deep tree) is no batch-parallel
+    // simulation any more
+    err = "DES schedule needs " + std::to_string(R) + " rounds (sequential call steps chain the invocation tree); "
+          "the limit is " + std::to_string(kDesMaxRounds);
+    return ISIM_EINVAL;
+  }
   // ---- lay the rounds out
   std::vector<std::vector<uint32_t>> arr(R), fast(R), zpos(R);
   std::vector<std::vector<int32_t>> srt(R);
-  std::vector<std::vector<std::vector<uint32_t>>> fin(R, std::vector<std::vector<uint32_t>>(out.n_levels));
   for (uint32_t b = 0; b < nb; ++b) arr[rnd[Ab(b)]].push_back(b);
   for (uint32_t v = 0; v < np; ++v)
     if (zero(v)) zpos[rnd[Q(v)]].push_back(v);
@@ -334,8 +361,17 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       if (out.pos[v].flags & kDesFlagLeaf) out.pos[v].flags |= kDesFlagFused;
     }
   }
+  // finish groups: by round, deepest first, most children first within a
+  // depth (the costliest blocks start first)
+  std::vector<uint32_t> fin;
   for (uint32_t v = 0; v < np; ++v)
-    if (!(out.pos[v].flags & kDesFlagFused)) fin[rnd[F(v)]][depth[v]].push_back(v);
+    if (!(out.pos[v].flags & kDesFlagFused)) fin.push_back(v);
+  std::stable_sort(fin.begin(), fin.end(), [&](uint32_t a, uint32_t b) {
+    if (rnd[F(a)] != rnd[F(b)]) return rnd[F(a)] < rnd[F(b)];
+    if (depth[a] != depth[b]) return depth[a] > depth[b];
+    return out.pos[a].child_cnt > out.pos[b].child_cnt;
+  });
+  size_t fi = 0;
   out.arr_off.assign(R + 1, 0);
   out.fast_off.assign(R + 1, 0);
   out.zero_off.assign(R + 1, 0);
@@ -379,12 +415,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       out.sorted.push_back(ss);
     }
     out.sorted_off[r + 1] = (uint32_t)out.sorted.size();
-    for (uint32_t d = out.n_levels; d-- > 0;) {
-      if (fin[r][d].empty()) continue;
-      // most children first: the costliest blocks start first
-      std::stable_sort(fin[r][d].begin(), fin[r][d].end(),
-                       [&](uint32_t a, uint32_t b) { return out.pos[a].child_cnt > out.pos[b].child_cnt; });
-      out.fin_pos.insert(out.fin_pos.end(), fin[r][d].begin(), fin[r][d].end());
+    while (fi < fin.size() && rnd[F(fin[fi])] == r) {
+      const uint32_t d = depth[fin[fi]];
+      while (fi < fin.size() && rnd[F(fin[fi])] == r && depth[fin[fi]] == d) out.fin_pos.push_back(fin[fi++]);
       out.fin_off.push_back((uint32_t)out.fin_pos.size());
     }
     out.fin_round_off[r + 1] = (uint32_t)out.fin_off.size() - 1;

@@ -18,11 +18,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ISIM_LIB") or os.path.join(_HERE, "libisim.so")
 
 # isim_status
-OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV = range(10)
+OK, EINVAL, ENOMEM, EHIP, EPARSE, ECYCLE, EDEPTH, ERANGE, ENOTFOUND, ENODEV, ECOMM = range(11)
 STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "ECYCLE",
-                6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV"}
+                6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV",
+                10: "ECOMM"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 6  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 7  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
@@ -81,6 +82,10 @@ class DesParams(C.Structure):
     _fields_ = [("mean_interarrival_ns", C.c_uint64), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class MultiId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
                 ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32)]
@@ -116,6 +121,16 @@ SIGNATURES = {
                                         _VP, C.c_uint64, _VP]),
     "isim_serve_des": (C.c_int, [_VP, C.c_int, C.POINTER(DesParams), C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
     "isim_des_fold": (C.c_int, [_VP, _VP, _VP]),
+    "isim_multi_get_id": (C.c_int, [C.POINTER(MultiId)]),
+    "isim_multi_init_rank": (C.c_int, [C.POINTER(MultiId), C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
+    "isim_multi_init_all": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(_VP)]),
+    "isim_multi_free": (None, [_VP]),
+    "isim_multi_info": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "isim_stats_allreduce_device": (C.c_int, [_VP, _VP, C.POINTER(_VP), C.POINTER(_VP)]),
+    "isim_des_table_allreduce_device": (C.c_int, [_VP, _VP, C.POINTER(_VP), C.POINTER(_VP)]),
+    "isim_serve_multi": (C.c_int, [_VP, _VP, C.c_uint64, C.c_uint64, _VP, _VP]),
+    "isim_stats_merge": (C.c_int, [_VP, _VP, _VP]),
+    "isim_des_table_merge": (C.c_int, [_VP, _VP, _VP]),
 }
 
 _lib = None

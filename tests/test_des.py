@@ -134,6 +134,33 @@ def test_des_class():
         isim.DesHandler(d.handler, 0).serve(0, 1)
 
 
+def _binary_dag(depth):
+    """s_i calls s_{i+1} twice, in two sequential call steps: 2^(depth+1) - 1
+    invocations per trace, and every step begin waits for the previous step's
+    whole subtree, so the DES schedule chains every position."""
+    svcs = [{"name": f"s{i}", "script": [{"call": f"s{i + 1}"}, {"call": f"s{i + 1}"}]} for i in range(depth)]
+    svcs.append({"name": f"s{depth}", "errorRate": 1.0})
+    svcs[0]["isEntrypoint"] = True
+    return {"services": svcs}
+
+
+def test_des_plan_lazy_and_round_limit():
+    # a walk handler never builds the DES plan (it unrolls the whole tree):
+    # 2^23 invocations per trace compile in about a second
+    import time
+    t0 = time.perf_counter()
+    h = _handler(_binary_dag(22), hop_base_ns=1, req_ps_per_byte=0, resp_ps_per_byte=0)
+    assert h.info.hops_upper == (1 << 23) - 1 and time.perf_counter() - t0 < 20
+    # the plan of a short chain is built in linear time (topological longest
+    # path) and its schedule is one round per link of the chain
+    d = isim.DesHandler(_handler(_binary_dag(10)), 1_000_000)
+    assert d.info.n_positions == (1 << 11) - 1
+    # past kDesMaxRounds rounds the graph is outside the DES class
+    t0 = time.perf_counter()
+    _rejects(_handler(_binary_dag(16)), "rounds")
+    assert time.perf_counter() - t0 < 20
+
+
 def _oracle_case(doc, **kw):
     j = obj_to_json(doc)
     h = isim.Handler(isim.ServiceGraph.from_json(j), None, isim.SimParams(**kw))

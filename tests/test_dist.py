@@ -1,6 +1,8 @@
 """Multi-process path on CPU (gloo, world_size 2): trace sharding and the
-stats merge used by bench.py (isim.dist), with the C oracle producing each
-rank's shard.  The merged buffer must equal one process over the union."""
+stats merge (isim.dist: torch.distributed across ranks, libisim's
+isim_stats_merge across steps), with the C oracle producing each rank's
+shard.  The merged buffer must equal one process over the union.  The same
+with the HIP walk producing the shards: tests/test_multi_gpu.py."""
 import os
 import socket
 
@@ -48,24 +50,52 @@ def _worker(rank, world, port, steps, batch, q):
     sys.path[:0] = [root, os.path.join(root, "istio-isotope_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from isim.dist import merge_stats, shard_begin
+    from isim.dist import merge_stats, shard_begin, stats_merge
+    h = _handler()
     acc = None
     for s in range(steps):
-        st = _to_isim_layout(_oracle_stats(shard_begin(rank, world, s, batch), batch))
-        acc = st if acc is None else _combine(acc, st)
-    t = torch.from_numpy(acc.copy())
+        st = _to_isim_layout(_oracle_stats(shard_begin(rank, world, s, batch), batch)).view(np.uint64)
+        st = st[:h.stats_words]  # the oracle appends per-service duration rows
+        # the per-rank accumulation across steps uses libisim's host merge
+        acc = st.copy() if acc is None else stats_merge(h, acc, st)
+    t = torch.from_numpy(acc.view(np.int64).copy())
     merge_stats(t)
     if rank == 0:
         q.put(t.numpy().copy())
     dist.destroy_process_group()
 
 
-def _combine(a, b):
-    out = a + b
-    ua, ub = a.view(np.uint64), b.view(np.uint64)
-    out.view(np.uint64)[5] = max(ua[5], ub[5])
-    out.view(np.uint64)[6] = max(ua[6], ub[6])
-    return out
+def _handler():
+    import isim
+    return isim.Handler(isim.ServiceGraph.from_json(_graph_json()))
+
+
+def test_stats_merge_host_equals_union():
+    """isim_stats_merge (the product's host merge) of oracle shards equals the
+    oracle run over the union: SUM everywhere, MAX on [~min, max]."""
+    from isim.dist import stats_merge
+    h = _handler()
+    w = h.stats_words  # the oracle appends per-service duration rows
+    a = _to_isim_layout(_oracle_stats(0, 200)).view(np.uint64)[:w].copy()
+    b = _to_isim_layout(_oracle_stats(200, 300)).view(np.uint64)[:w]
+    union = _to_isim_layout(_oracle_stats(0, 500)).view(np.uint64)[:w]
+    assert np.array_equal(stats_merge(h, a, b), union)
+    # merging an all-zero buffer (an idle rank) changes nothing
+    assert np.array_equal(stats_merge(h, a, np.zeros_like(a)), union)
+
+
+def test_des_table_merge_rules():
+    import isim
+    from isim.dist import des_table_merge
+    h = _handler()
+    rows = int(h.info.n_reachable)
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 1 << 40, rows * isim.native.DES_ROW_WORDS, dtype=np.uint64)
+    b = rng.integers(0, 1 << 40, rows * isim.native.DES_ROW_WORDS, dtype=np.uint64)
+    want = (a + b).reshape(rows, -1)
+    want[:, isim.native.DES_MAX_WAIT] = np.maximum(a.reshape(rows, -1)[:, isim.native.DES_MAX_WAIT],
+                                                   b.reshape(rows, -1)[:, isim.native.DES_MAX_WAIT])
+    assert np.array_equal(des_table_merge(h, a.copy(), b).reshape(rows, -1), want)
 
 
 @pytest.mark.parametrize("world", [2])
@@ -81,7 +111,7 @@ def test_sharded_merge_equals_single_process(world):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    single = _to_isim_layout(_oracle_stats(0, steps * world * batch))
+    single = _to_isim_layout(_oracle_stats(0, steps * world * batch))[:merged.size]
     assert np.array_equal(merged.view(np.uint64), single.view(np.uint64))
 
 

@@ -5,11 +5,12 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kat_gpu.py \
+PT="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
+$T 600 $PT tests/test_kat_gpu.py \
   "tests/test_walk_gpu.py::test_config3_mode_b_informative" "tests/test_walk_gpu.py::test_site_counter_beyond_u32" \
   "tests/test_des_gpu.py::test_config5_bench_scale" -m gpu > gpurun_out/new.log 2>&1 || { tail -40 gpurun_out/new.log; exit 11; }
 tail -1 gpurun_out/new.log
-$T 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests -m gpu > gpurun_out/all.log 2>&1 || { tail -40 gpurun_out/all.log; exit 12; }
+$T 900 $PT tests -m gpu > gpurun_out/all.log 2>&1 || { tail -40 gpurun_out/all.log; exit 12; }
 tail -1 gpurun_out/all.log
 $T 300 python bench.py --steps 10 --warmup 3 > gpurun_out/b_c3.log 2>&1 || { tail -5 gpurun_out/b_c3.log; exit 13; }
 tail -1 gpurun_out/b_c3.log
