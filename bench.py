@@ -437,7 +437,7 @@ def main():
     traffic = None
     occupancy = {"launched_waves_per_cu": launch["blocks_per_cu"] * launch["wg_threads"] // 64,
                  "peak_waves_per_cu": 32, "measured": None}
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_summary_{args.config}.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))

@@ -94,9 +94,11 @@ typedef struct {
 #define ISIM_FLAG_WALK_ALL 4u   /* draw-free static walks: walk every trace (default: walk one, fill the rest) */
 #define ISIM_FLAG_BIT_STACK 8u  /* mode B on the draw stream: the bit-stack kernel (kind 5, call depth <= 32;
                                    kind 4 deeper) instead of the close-list kernel (kind 6) */
-#define ISIM_FLAG_DYNAMIC 16u   /* treat every walk as dynamic: the general kernel with per-lane time and hop
-                                   ids (kinds 2/3) even when every trace executes the same invocations
+#define ISIM_FLAG_DYNAMIC 16u   /* treat every walk as dynamic: the general kernels with per-lane time and hop
+                                   ids (kind 7, or 2/3) even when every trace executes the same invocations
                                    (parity tests of the general path on static graphs; no DES) */
+#define ISIM_FLAG_WAVE_WALK 32u /* dynamic walks on the wave-walk interpreter (kinds 2/3: a wave walks the union
+                                   of its 64 traces' call paths) instead of the lane tree walk (kind 7) */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -172,7 +174,9 @@ typedef struct {
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
   int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
                                 5 draw stream with the mode-B bit stack (call depth <= 32),
-                                6 draw stream with the mode-B close list (the default in mode B) */
+                                6 draw stream with the mode-B close list (the default in mode B),
+                                7 lane tree walk (dynamic walks whose unrolled tree of potential
+                                invocations and LDS tables fit; else 2/3) */
   int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
 } isim_launch_info;

@@ -71,6 +71,9 @@ struct DevState {
   uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
   uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr, *d_des_zero = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
+  isim::TreeExt *d_tree_ext = nullptr;  // kind 7: per position (the nodes are d_prog)
+  isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
+  bool tree_ext_lds = false;            // kind 7: TreeExt copied to LDS
 };
 
 void free_dev(DevState &d) {
@@ -78,7 +81,7 @@ void free_dev(DevState &d) {
                   (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_const_stats,
                   d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
                   (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
-                  d.d_des_ext, d.d_des_steps})
+                  d.d_des_ext, d.d_des_steps, (void *)d.d_tree_ext, (void *)d.d_tree_dyn})
     if (q) (void)hipFree(q);
   d = DevState();
 }
@@ -114,6 +117,9 @@ struct isim_handler {
 };
 
 namespace {
+
+// Kernel kinds 4-6 walk the draw stream (static walks).
+bool is_stream(uint32_t kind) { return kind >= 4 && kind <= 6; }
 
 // Rows of the device per-service duration table (dynamic walks only).
 uint64_t svc_dur_rows(const isim_handler *h) {
@@ -193,7 +199,28 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B)
     st.kind = (h->params.flags & ISIM_FLAG_BIT_STACK) ? (p.max_depth <= 32 ? 5u : 4u) : 6u;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
-  if (!p.static_walk) {
+  // dynamic walks: the lane tree walk (kind 7) when the unrolled tree and its
+  // LDS tables fit (one 1024-thread workgroup per CU); else the wave walk
+  bool tree = false;
+  if (!p.static_walk && !p.tree_nodes.empty() && !(h->params.flags & ISIM_FLAG_WAVE_WALK)) {
+    const uint32_t P = (uint32_t)p.tree_nodes.size(), S = (uint32_t)p.n_slots, R = (uint32_t)p.row_svc.size();
+    // the TreeExt records in LDS too when they fit (their reads are on the
+    // per-lane dependency chain; from HBM they left the waves waiting)
+    const uint32_t D = p.tree_dyn_words;
+    bool ext_lds = isim::tree_lds_bytes(P, S, R, D, true) <= lds_max;
+    if (const char *e = std::getenv("ISIM_TREE_EXT_HBM"); e && e[0] == '1') ext_lds = false;  // A/B experiments
+    const uint32_t need = isim::tree_lds_bytes(P, S, R, D, ext_lds);
+    if (need <= lds_max) {
+      tree = true;
+      st.kind = 7;
+      st.tree_ext_lds = ext_lds;
+      st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames, ext_lds);
+      st.threads = isim::kWgThreads;
+      st.lds_bytes = need;
+      st.lds_counters = 1;
+    }
+  }
+  if (!p.static_walk && !tree) {
     // dynamic walks keep per-lane frame stacks in LDS (waves x frames x 64
     // lanes): the workgroup size with the most resident waves per CU, not the
     // largest that fits
@@ -222,7 +249,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
     st.lds_bytes = lds_need(p, waves, counters);
     st.lds_counters = counters ? 1u : 0u;
   }
-  if (st.kind >= 4) {
+  if (is_stream(st.kind)) {
     st.draw_free = true;
     for (const isim::Node &nd : p.stream) st.draw_free = st.draw_free && nd.thr == 0;
   }
@@ -234,20 +261,37 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (per_cu < 1) return fail(ISIM_EHIP, "walk kernel cannot be resident (occupancy 0)");
   st.per_cu = (uint32_t)per_cu;
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-  const void *src = st.kind >= 4 ? (const void *)p.stream.data() : (const void *)p.code.data();
-  const size_t bytes = st.kind >= 4 ? p.stream.size() * sizeof(isim::Node) : p.code.size() * sizeof(isim::Ins);
+  const void *src = is_stream(st.kind) ? (const void *)p.stream.data()
+                    : tree                ? (const void *)p.tree_nodes.data()
+                                          : (const void *)p.code.data();
+  const size_t bytes = is_stream(st.kind) ? p.stream.size() * sizeof(isim::Node)
+                       : tree             ? p.tree_nodes.size() * sizeof(isim::TreeNode)
+                                          : p.code.size() * sizeof(isim::Ins);
   // the draw-stream kernel prefetches group g+1 unconditionally: two zero
   // groups (32 B each) of tail padding keep those reads inside the buffer
-  const size_t tail = st.kind >= 4 ? 2 * 4 * sizeof(isim::Node) : 0;
+  const size_t tail = is_stream(st.kind) ? 2 * 4 * sizeof(isim::Node) : 0;
   HIPCHK(hipMalloc(&st.d_prog, bytes + tail));
   HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
   if (tail) HIPCHK(hipMemset((char *)st.d_prog + bytes, 0, tail));
-  if (st.kind >= 4 && p.n_slots > 0) {
+  if (tree) {
+    HIPCHK(hipMalloc(&st.d_tree_ext, p.tree_ext.size() * sizeof(isim::TreeExt)));
+    HIPCHK(hipMemcpy(st.d_tree_ext, p.tree_ext.data(), p.tree_ext.size() * sizeof(isim::TreeExt),
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&st.d_tree_dyn, std::max<size_t>(1, p.tree_dyn.size()) * sizeof(isim::TreeDynRow)));
+    if (!p.tree_dyn.empty())
+      HIPCHK(hipMemcpy(st.d_tree_dyn, p.tree_dyn.data(), p.tree_dyn.size() * sizeof(isim::TreeDynRow),
+                       hipMemcpyHostToDevice));
+    if (p.n_slots > 0) {  // per slot: callee row | static bucket (the kernel's duration flush)
+      HIPCHK(hipMalloc(&st.d_dur, p.slot_tbkt.size() * sizeof(uint32_t)));
+      HIPCHK(hipMemcpy(st.d_dur, p.slot_tbkt.data(), p.slot_tbkt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+  }
+  if (is_stream(st.kind) && p.n_slots > 0) {
     HIPCHK(hipMalloc(&st.d_mult, p.stream_mult.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_mult, p.stream_mult.data(), p.stream_mult.size() * sizeof(uint32_t),
                      hipMemcpyHostToDevice));
   }
-  if (svc_dur_rows(h) && p.n_slots > 0) {
+  if (!tree && svc_dur_rows(h) && p.n_slots > 0) {
     HIPCHK(hipMalloc(&st.d_dur, p.slot_dur.size() * sizeof(uint32_t)));
     HIPCHK(hipMemcpy(st.d_dur, p.slot_dur.data(), p.slot_dur.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   }
@@ -275,7 +319,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
   // that no workgroup can count past 2^32 at one site (traces x calls
   // through the site per trace)
   st.max_mult = std::max<uint64_t>(1, p.hops_upper);
-  if (st.kind >= 4) {
+  if (tree) st.max_mult = std::max<uint32_t>(1, p.tree_mult);
+  if (is_stream(st.kind)) {
     st.max_mult = 1;
     for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
   }
@@ -485,7 +530,13 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.closes = st->d_closes;
   kp.close_slot = st->d_close_slot;
   kp.close_end = st->d_close_end;
-  const uint64_t per_wave = st->kind >= 4 ? isim::stream_traces_per_wave() : 64u;
+  kp.tree_ext = st->d_tree_ext;
+  kp.tree_dyn = st->d_tree_dyn;
+  kp.n_pos = (uint32_t)h->prog.tree_nodes.size();
+  kp.n_rows = (uint32_t)h->prog.row_svc.size();
+  kp.n_dyn = (uint32_t)h->prog.tree_dyn.size();
+  kp.dyn_words = h->prog.tree_dyn_words;
+  const uint64_t per_wave = is_stream(st->kind) ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
@@ -495,7 +546,7 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
   HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, (hipStream_t)hip_stream));
-  if (st->kind >= 4 && h->prog.n_slots > 0) {
+  if (is_stream(st->kind) && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;
     void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};
@@ -583,7 +634,10 @@ int isim_serve(isim_handler *h, int device, uint64_t trace_begin, uint64_t n_tra
     }
     rc = isim_serve_device(h, trace_begin, n_traces, d_rec, d_stats, s);
     if (rc != ISIM_OK) break;
-    if (hipStreamSynchronize(s) != hipSuccess) { rc = fail(ISIM_EHIP, "walk kernel failed"); break; }
+    if (const hipError_t e = hipStreamSynchronize(s); e != hipSuccess) {
+      rc = fail(ISIM_EHIP, std::string("walk kernel failed: ") + hipGetErrorName(e) + ": " + hipGetErrorString(e));
+      break;
+    }
     if (h_stats && hipMemcpy(h_stats, d_stats, words * 8, hipMemcpyDeviceToHost) != hipSuccess) {
       rc = fail(ISIM_EHIP, "copy stats failed");
       break;

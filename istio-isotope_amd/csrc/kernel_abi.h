@@ -70,6 +70,48 @@ constexpr uint32_t kChunkRecords = 4 * kChunkGroups;  // 32: one bit per record 
 // Per-service duration table word: row (bits 0-23) | bucket of a leaf callee (24-31).
 constexpr uint32_t kDurRowMask = 0xFFFFFFu;
 
+// DYNAMIC walks on the lane tree walk (kernel kind 7, tree_walk.h): the
+// invocation tree unrolled over every POTENTIAL invocation (each reachable
+// call command, probabilistic or not) in preorder; a trace walks it on its
+// own lane, skipping the subtree of a call its draw skips.  Position 0 is the
+// entry.  Nodes live in LDS (16 B); the rest of a position in HBM (TreeExt).
+enum TreeFlag : uint8_t {
+  TF_STEP = 1,        // first call of its step in the caller's script (the step begins here)
+  TF_CONC = 2,        // the step is concurrent
+  TF_LEAF = 4,        // the callee makes no calls
+  TF_ERR_ALWAYS = 8,  // callee errorRate 1
+  TF_ERR_DRAW = 16,   // 0 < callee errorRate < 1: draw against thr
+};
+struct TreeNode {
+  uint16_t size;   // positions in the subtree (itself included): a skipped call jumps over them
+  uint16_t k;      // index of the call command in the caller's script (skip-draw block and word)
+  uint8_t prob;    // 1..99: draw to skip; 0: always called
+  uint8_t flags;   // TF_*
+  uint16_t slot;   // stats slot of the call site
+  uint32_t thr;    // callee error threshold (TF_ERR_DRAW)
+  uint32_t pre;    // TF_STEP: time the caller spends between its previous call step and this step
+};
+static_assert(sizeof(TreeNode) == 16, "TreeNode must be 16 bytes");
+struct TreeExt {
+  uint32_t H;      // hop cost of the call
+  uint32_t tc;     // leaf callee: its latency; else the time after its last call step
+  uint32_t cmax0;  // TF_STEP|TF_CONC: the longest sleep sub-command of the step
+  uint32_t row;    // callee duration-table row (bits 0-15) | LDS word offset of the row's bucket table
+                   // (bits 16-31; kTreeStaticRow: the row's duration bucket never varies)
+};
+static_assert(sizeof(TreeExt) == 16, "TreeExt must be 16 bytes");
+constexpr uint32_t kTreeDynBucket = 0xFFu;   // slot_tbkt: the callee's bucket varies per invocation
+constexpr uint32_t kTreeStaticRow = 0xFFFFu;
+// A row whose invocation durations span several duration buckets
+// (prom_bucket(tmin) < prom_bucket(tmax)) counts them in an LDS table of the
+// workgroup: a header word (b_lo | width << 8), then [code 200|500][width]
+// u32 counts of buckets b_lo .. b_lo + width - 1; flushed once per workgroup.
+struct TreeDynRow {
+  uint32_t row, off, b_lo, width;  // off: word offset of the header in the LDS tables
+};
+constexpr uint32_t kTreeMaxPositions = 0xFFFFu;  // u16 sizes and slots
+constexpr uint32_t kTreeMaxFrames = 16;          // open calling invocations below the current one
+
 // Scalar kernel arguments (the program, records and stats pointers are
 // separate __restrict__ kernel arguments so program fetches become s_load).
 struct KParams {
@@ -87,6 +129,12 @@ struct KParams {
   const StreamClose *closes;     // kind 6: close list (+kClosePad zero records of tail padding)
   const uint32_t *close_slot;    // kind 6: per close, the call-site slot of the closing invocation
   const uint32_t *close_end;     // kind 6: per chunk, closes up to and including it
+  const TreeExt *tree_ext;       // kind 7: per position (the nodes are the `prog` argument)
+  const TreeDynRow *tree_dyn;    // kind 7: rows with an LDS bucket table
+  uint32_t n_pos;                // kind 7: positions of the unrolled tree
+  uint32_t n_rows;               // kind 7: duration-table rows (LDS sums)
+  uint32_t n_dyn;                // kind 7: entries of tree_dyn
+  uint32_t dyn_words;            // kind 7: LDS words of the bucket tables
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to
@@ -103,8 +151,27 @@ constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 
 // walk.hip: kernel pointer for a walk variant.
 // kind: 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
-// 5 draw stream + mode-B bit stack, 6 draw stream + mode-B close list.
+// 5 draw stream + mode-B bit stack, 6 draw stream + mode-B close list,
+// 7 lane tree walk (dynamic walks, tree.hip; `frames` = register stack depth).
 void *walk_kernel(int kind, bool modeb, bool lds_counters);
+void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds);
+// LDS layout of the kind-7 kernel: accumulators, histograms, per-slot
+// counters (u32 calls, u32 500s), per-row u64 duration sums (code 200), the
+// bucket tables of the varying rows, the nodes, and (ext_lds) the TreeExt
+// records.
+constexpr uint32_t tree_lds_sums_offset(uint32_t n_slots) {
+  return (kLdsAccBytes + kHistWords * 4u + 8u * n_slots + 7u) & ~7u;
+}
+constexpr uint32_t tree_lds_dyn_offset(uint32_t n_slots, uint32_t n_rows) {
+  return tree_lds_sums_offset(n_slots) + 8u * n_rows;
+}
+constexpr uint32_t tree_lds_nodes_offset(uint32_t n_slots, uint32_t n_rows, uint32_t dyn_words) {
+  return (tree_lds_dyn_offset(n_slots, n_rows) + 4u * dyn_words + 15u) & ~15u;
+}
+constexpr uint32_t tree_lds_bytes(uint32_t n_pos, uint32_t n_slots, uint32_t n_rows, uint32_t dyn_words,
+                                  bool ext_lds) {
+  return tree_lds_nodes_offset(n_slots, n_rows, dyn_words) + (ext_lds ? 32u : 16u) * n_pos;
+}
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)
 uint32_t stream_traces_per_wave();

@@ -27,7 +27,189 @@ uint64_t sat_add(uint64_t a, uint64_t b) {
 
 uint64_t sleep_ns(int64_t d) { return d > 0 ? (uint64_t)d : 0; }
 
+// Shape of a script for the lane tree walk: per call command (document
+// order) its step's facts; the time outside call steps.
+struct CallShape {
+  bool step_first, conc;
+  uint64_t pre;    // step_first: non-call step time since the previous call step
+  uint64_t cmax0;  // conc: the step's longest sleep sub-command
+};
+struct ScriptTimes {
+  std::vector<CallShape> calls;
+  uint64_t tail = 0;  // non-call step time after the last call step (the whole script for a leaf)
+};
+
+ScriptTimes script_times(const Service &sv) {
+  ScriptTimes r;
+  uint64_t pending = 0;  // non-call step time not yet assigned
+  for (const Command &c : sv.script) {
+    if (c.kind == Command::Sleep) {
+      pending = sat_add(pending, sleep_ns(c.sleep_ns));
+    } else if (c.kind == Command::Request) {
+      r.calls.push_back(CallShape{true, false, pending, 0});
+      pending = 0;
+    } else {
+      uint64_t m = 0;
+      size_t first = r.calls.size();
+      for (const Command &x : c.commands) {
+        if (x.kind == Command::Request) r.calls.push_back(CallShape{r.calls.size() == first, true, 0, 0});
+        else m = std::max(m, sleep_ns(x.sleep_ns));
+      }
+      if (r.calls.size() == first) {  // a concurrent step of sleeps only: a timed step
+        pending = sat_add(pending, m);
+      } else {
+        r.calls[first].pre = pending;
+        r.calls[first].cmax0 = m;
+        pending = 0;
+      }
+    }
+  }
+  r.tail = pending;
+  return r;
+}
+
 }  // namespace
+
+// The unrolled tree of potential invocations for the lane tree walk
+// (kernel_abi.h TreeNode/TreeExt, tree_walk.h); leaves out.tree_nodes empty
+// with the reason in out.tree_why when the walk does not fit it.
+static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Site> &sites,
+                const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
+                const std::vector<uint64_t> &tmin, const std::vector<char> &leaf) {
+  out.tree_nodes.clear();
+  out.tree_ext.clear();
+  if (out.max_latency >= (1ull << 32)) {
+    out.tree_why = "latency bound >= 2^32 ns (the tree walk keeps u32 time)";
+    return;
+  }
+  if (out.n_slots > (int32_t)kTreeMaxPositions) {
+    out.tree_why = "more than 65535 call sites";
+    return;
+  }
+  const int32_t n = (int32_t)g.services.size();
+  std::vector<ScriptTimes> shape(n);
+  std::vector<char> shaped(n, 0);
+  auto shape_of = [&](int32_t s) -> const ScriptTimes & {
+    if (!shaped[s]) {
+      shape[s] = script_times(g.services[s]);
+      shaped[s] = 1;
+    }
+    return shape[s];
+  };
+  if (out.row_svc.size() > kTreeStaticRow) {
+    out.tree_why = "more than 65534 reachable services";
+    return;
+  }
+  // rows whose durations may fall in several buckets get an LDS bucket table
+  // (the entry's row is the end-to-end histogram: no table)
+  out.tree_dyn.clear();
+  out.tree_dyn_words = 0;
+  std::vector<uint32_t> dyn_off(out.row_svc.size(), kTreeStaticRow);
+  for (size_t r = 1; r < out.row_svc.size(); ++r) {
+    const int32_t s = out.row_svc[r];
+    const uint32_t lo = prom_bucket_ns(tmin[s]), hi = prom_bucket_ns(out.svc_time[s]);
+    if (lo == hi) continue;
+    if (out.tree_dyn_words + 1 + 2 * (hi - lo + 1) >= kTreeStaticRow) {
+      out.tree_why = "too many duration-bucket table words";
+      return;
+    }
+    dyn_off[r] = out.tree_dyn_words;
+    out.tree_dyn.push_back(TreeDynRow{(uint32_t)r, out.tree_dyn_words, lo, hi - lo + 1});
+    out.tree_dyn_words += 1 + 2 * (hi - lo + 1);
+  }
+  auto row_word = [&](int32_t s) -> uint32_t {
+    return (uint32_t)out.svc_row[s] | (dyn_off[out.svc_row[s]] << 16);
+  };
+  auto slot_word = [&](int32_t s) -> uint32_t {
+    const uint32_t b = prom_bucket_ns(tmin[s]) == prom_bucket_ns(out.svc_time[s]) ? prom_bucket_ns(tmin[s])
+                                                                                   : kTreeDynBucket;
+    return (uint32_t)out.svc_row[s] | (b << 24);
+  };
+  auto err_flags = [&](int32_t s) -> uint8_t {
+    if (thr[s] >= (1ull << 32)) return TF_ERR_ALWAYS;
+    return thr[s] > 0 ? (uint8_t)TF_ERR_DRAW : (uint8_t)0;
+  };
+  out.slot_tbkt.assign(out.n_slots, 0);
+  for (int32_t sl = 0; sl < out.n_slots; ++sl) out.slot_tbkt[sl] = slot_word(out.slot_callee[sl]);
+  std::vector<uint32_t> through(out.n_slots, 0);
+  // preorder DFS over call sites; frame = (service, next call index, position, open calling invocations)
+  struct Frame {
+    int32_t svc;
+    size_t next;
+    uint32_t pos;
+  };
+  std::vector<Frame> stack;
+  const int32_t e = out.entry;
+  TreeNode root{};
+  root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e));
+  root.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
+  TreeExt rx{};
+  rx.tc = (uint32_t)shape_of(e).tail;
+  rx.row = (uint32_t)out.svc_row[e] | (kTreeStaticRow << 16);  // the entry's row is filled from the histograms
+  out.tree_nodes.push_back(root);
+  out.tree_ext.push_back(rx);
+  uint32_t max_open = leaf[e] ? 0u : 1u;
+  if (!leaf[e]) stack.push_back({e, 0, 0});
+  while (!stack.empty()) {
+    Frame &top = stack.back();
+    if (top.next < svc_sites[top.svc].size()) {
+      const size_t j = top.next++;
+      const Site &st = sites[svc_sites[top.svc][j]];
+      const CallShape &cs = shape_of(top.svc).calls[j];
+      const int32_t c = st.callee;
+      if (out.tree_nodes.size() >= kTreeMaxPositions) {
+        out.tree_nodes.clear();
+        out.tree_ext.clear();
+        out.tree_why = "more than 65535 potential invocations";
+        return;
+      }
+      TreeNode nd{};
+      nd.k = (uint16_t)std::min<uint32_t>(st.k, 0xFFFFu);
+      if (st.k > 0xFFFFu) {
+        out.tree_nodes.clear();
+        out.tree_ext.clear();
+        out.tree_why = "a script with more than 65536 calls";
+        return;
+      }
+      nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
+      nd.flags = (uint8_t)((cs.step_first ? TF_STEP : 0) | (cs.conc ? TF_CONC : 0) | (leaf[c] ? TF_LEAF : 0) |
+                           err_flags(c));
+      const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
+      nd.slot = (uint16_t)slot;
+      through[slot] += 1;
+      nd.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
+      nd.pre = (uint32_t)cs.pre;
+      TreeExt x{};
+      x.H = (uint32_t)st.hop;
+      x.tc = (uint32_t)shape_of(c).tail;
+      x.cmax0 = (uint32_t)cs.cmax0;
+      x.row = row_word(c);
+      const uint32_t pos = (uint32_t)out.tree_nodes.size();
+      out.tree_nodes.push_back(nd);
+      out.tree_ext.push_back(x);
+      if (!leaf[c]) {
+        stack.push_back({c, 0, pos});
+        max_open = std::max<uint32_t>(max_open, (uint32_t)stack.size());
+      }
+    } else {
+      out.tree_nodes[top.pos].size = (uint16_t)(out.tree_nodes.size() - top.pos);
+      stack.pop_back();
+    }
+  }
+  if (out.tree_nodes.size() == 1) out.tree_nodes[0].size = 1;
+  for (size_t i = 0; i < out.tree_nodes.size(); ++i)
+    if (out.tree_nodes[i].size == 0) out.tree_nodes[i].size = 1;  // leaf positions
+  out.tree_frames = max_open ? max_open - 1 : 0;
+  if (out.tree_frames > kTreeMaxFrames) {
+    out.tree_nodes.clear();
+    out.tree_ext.clear();
+    out.tree_why = "more than 17 nested calling invocations";
+    return;
+  }
+  out.tree_mult = 1;
+  for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
+  out.tree_why.clear();
+}
 
 uint32_t prom_bucket_ns(uint64_t t) {
   static const uint64_t edges_ms[32] = {7,  8,  9,  10, 11,  12,  14,  16,  18,  20,  25,  30,  35,  40,  45,  50,
@@ -134,12 +316,17 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
 
   // ---- per-service static facts, children before parents
   std::vector<uint64_t> tmax(n, 0), hops(n, 0);
+  // tmin: a lower bound of any invocation's duration (sleeps, always-made
+  // calls, and in mode B nothing after a step that can fail); tree-walk
+  // rows whose bound and tmax share a duration bucket never vary in bucket
+  std::vector<uint64_t> tmin(n, 0);
   std::vector<int32_t> depth(n, 0), frames(n, 0);
   std::vector<char> leaf(n, 1), can_fail(n, 0);
   bool any_prob = false, nonstatic_abort = false;
   for (int32_t s : post) {
     const Service &sv = g.services[s];
-    uint64_t T = 0, H = 1;
+    uint64_t T = 0, H = 1, Tl = 0;
+    bool lb_open = true;  // no step that can fail (mode B) seen yet: later steps always run
     int32_t d = 1, fr = 0;
     bool fail = thr[s] > 0;
     size_t si = 0;  // walks svc_sites[s] in document order
@@ -147,37 +334,45 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     for (size_t step = 0; step < nsteps; ++step) {
       const Command &c = sv.script[step];
       bool step_fallible = false;
-      auto visit_call = [&](uint64_t &dt) {
+      auto visit_call = [&](uint64_t &dt, uint64_t &dl) {
         const Site &st = sites[svc_sites[s][si++]];
         leaf[s] = 0;
-        if (st.prob >= 1 && st.prob <= 99) any_prob = true;
+        const bool maybe = st.prob >= 1 && st.prob <= 99;
+        if (maybe) any_prob = true;
         dt = sat_add(st.hop, tmax[st.callee]);
+        dl = maybe ? 0 : sat_add(st.hop, tmin[st.callee]);
         H = std::min<uint64_t>(H + hops[st.callee], kTimeCap);
         d = std::max(d, 1 + depth[st.callee]);
         fr = std::max(fr, frames[st.callee]);
         if (modeb && can_fail[st.callee]) step_fallible = true;
       };
+      uint64_t dl = 0;
       if (c.kind == Command::Sleep) {
         T = sat_add(T, sleep_ns(c.sleep_ns));
+        dl = sleep_ns(c.sleep_ns);
       } else if (c.kind == Command::Request) {
         uint64_t dt;
-        visit_call(dt);
+        visit_call(dt, dl);
         T = sat_add(T, dt);
       } else {
         uint64_t m = 0;
         for (const Command &x : c.commands) {
-          uint64_t dt = 0;
-          if (x.kind == Command::Request) visit_call(dt);
-          else dt = sleep_ns(x.sleep_ns);
+          uint64_t dt = 0, xl = 0;
+          if (x.kind == Command::Request) visit_call(dt, xl);
+          else dt = xl = sleep_ns(x.sleep_ns);
           m = std::max(m, dt);
+          dl = std::max(dl, xl);
         }
         T = sat_add(T, m);
       }
+      if (lb_open) Tl = sat_add(Tl, dl);
       if (step_fallible) {
         fail = true;
+        lb_open = false;
         if (step + 1 < nsteps) nonstatic_abort = true;  // a failure would skip later steps
       }
     }
+    tmin[s] = Tl;
     tmax[s] = T;
     hops[s] = H;
     depth[s] = d;
@@ -282,7 +477,7 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
         int32_t sid = svc_sites[s][si++];
         const Site &st = sites[sid];
         uint32_t prob = (st.prob >= 1 && st.prob <= 99) ? (uint32_t)st.prob : 0;
-        code.push_back(make_invoke(st.callee, st.hop, prob ? F_PROB : 0, prob, st.k,
+        code.push_back(make_invoke(st.callee, st.hop, prob ? (uint32_t)F_PROB : 0u, prob, st.k,
                                    (uint32_t)out.site_slot[sid]));
       } else {
         in.opf = OP_CBEGIN;
@@ -379,6 +574,7 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     err = "program too large";
     return ISIM_EINVAL;
   }
+  if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf);
   return ISIM_OK;
 }
 

@@ -45,6 +45,16 @@ struct Program {
   std::vector<int32_t> row_svc;     // per row: service (rows = reachable services, preorder)
   std::vector<uint32_t> slot_dur;   // per slot: callee row | leaf-callee bucket << 24
   uint32_t root_dur = 0;            // the entry: row 0 | bucket << 24 when the entry is a leaf
+  // lane tree walk (kernel kind 7, dynamic walks): the unrolled tree of potential
+  // invocations when it fits (tree_nodes empty otherwise; tree_why says why)
+  std::vector<TreeNode> tree_nodes;
+  std::vector<TreeExt> tree_ext;
+  std::vector<uint32_t> slot_tbkt;  // per slot: callee row | static duration bucket << 24 (kTreeDynBucket)
+  std::vector<TreeDynRow> tree_dyn; // rows whose duration bucket varies: their LDS bucket tables
+  uint32_t tree_dyn_words = 0;
+  uint32_t tree_frames = 0;         // register-stack frames the walk needs (open calling invocations - 1)
+  uint32_t tree_mult = 0;           // most positions through one slot (LDS counter overflow guard)
+  std::string tree_why;
 };
 
 // Bucket of an invocation duration on the service_request_duration_seconds

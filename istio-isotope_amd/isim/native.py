@@ -28,7 +28,8 @@ FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
 FLAG_BIT_STACK = 8  # mode B on the draw stream: the bit-stack kernel (kind 5/4) instead of the close list (6)
-FLAG_DYNAMIC = 16  # every walk on the general (dynamic) kernel, kinds 2/3
+FLAG_DYNAMIC = 16  # every walk on the general (dynamic) kernels, kind 7 (or 2/3)
+FLAG_WAVE_WALK = 32  # dynamic walks on the wave-walk interpreter (kinds 2/3) instead of the lane tree walk (7)
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4

@@ -1,0 +1,172 @@
+// CPU run of the lane tree walk (tree_walk.h, kernel kind 7) over the
+// product's own loader and program compiler: the per-lane code the HIP
+// kernel executes, with the kernel's accounting of the statistics (per-slot
+// counters, per-row duration sums, static-bucket rows derived from the
+// counters at the end, the entry's row from the trace results).  Prints the
+// results in the oracle's terms so tests/test_tree_walk.py can compare them
+// with oracle/executor.py bit for bit.  Test infrastructure only.
+//   tree_walk_check <graph.json> <mode 0|1> <seed> <hop_base> <req_ps> <resp_ps> <begin> <n>
+// Output (one line each): "why <reason>" and exit 3 if no tree; else
+//   rec <lat> <hops> <status500> <err_hops>          per trace
+//   site <calls...>                                   per call site
+//   svc <calls...> / err <errs...>                    per service
+//   dur <svc> <68 words>                              per reachable service
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <vector>
+
+#include "graph.h"
+#include "kernel_abi.h"
+#include "program.h"
+#include "tree_walk.h"
+
+using namespace isim;
+
+namespace {
+
+struct Sink {
+  std::vector<uint64_t> calls, errs;                // per slot
+  std::vector<uint64_t> sum200, sum500;             // per row
+  std::vector<uint32_t> dyn;                        // the LDS bucket tables (tree_dyn layout)
+  bool out_of_table = false;
+  void call(uint32_t slot) { calls[slot] += 1; }
+  void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
+    const uint32_t row = roww & 0xFFFFu, off = roww >> 16;
+    if (st) errs[slot] += 1;
+    if (off != kTreeStaticRow) {  // as tree.hip TreeSink::resp, with the range check made an error
+      const uint32_t lo = dyn[off] & 0xFFu, w = dyn[off] >> 8, b = prom_bucket_ns(T);
+      if (b < lo || b >= lo + w) out_of_table = true;
+      else dyn[off + 1 + (st ? w : 0) + (b - lo)] += 1;
+    }
+    (st ? sum500 : sum200)[row] += T;
+  }
+};
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  if (argc < 9) return 2;
+  std::ifstream f(argv[1]);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string js = ss.str();
+  ServiceGraph g;
+  std::string err;
+  if (!unmarshal_service_graph(js.data(), js.size(), g, err)) {
+    std::fprintf(stderr, "parse: %s\n", err.c_str());
+    return 2;
+  }
+  int32_t entry = -1;
+  for (size_t i = 0; i < g.services.size() && entry < 0; ++i)
+    if (g.services[i].is_entrypoint) entry = (int32_t)i;
+  isim_params p{};
+  p.error_mode = (uint32_t)std::atoi(argv[2]);
+  p.seed = std::strtoull(argv[3], nullptr, 0);
+  p.hop_base_ns = std::strtoull(argv[4], nullptr, 0);
+  p.req_ps_per_byte = std::strtoull(argv[5], nullptr, 0);
+  p.resp_ps_per_byte = std::strtoull(argv[6], nullptr, 0);
+  p.flags = ISIM_FLAG_DYNAMIC;  // static graphs too: the tree walk is the general path
+  const uint64_t begin = std::strtoull(argv[7], nullptr, 0), n = std::strtoull(argv[8], nullptr, 0);
+  Program prog;
+  if (compile_program(g, entry, p, prog, err) != ISIM_OK) {
+    std::fprintf(stderr, "compile: %s\n", err.c_str());
+    return 2;
+  }
+  if (prog.tree_nodes.empty()) {
+    std::printf("why %s\n", prog.tree_why.c_str());
+    return 3;
+  }
+  std::fprintf(stderr, "positions %zu frames %u\n", prog.tree_nodes.size(), prog.tree_frames);
+  const uint32_t S = (uint32_t)prog.n_slots, R = (uint32_t)prog.row_svc.size();
+  Sink sk;
+  sk.calls.assign(S, 0);
+  sk.errs.assign(S, 0);
+  sk.sum200.assign(R, 0);
+  sk.sum500.assign(R, 0);
+  sk.dyn.assign(prog.tree_dyn_words, 0);
+  for (const TreeDynRow &d : prog.tree_dyn) sk.dyn[d.off] = d.b_lo | (d.width << 8);
+  std::vector<uint64_t> root_hist(2 * ISIM_N_PROM, 0), root_sum(2, 0);
+  const bool modeb = p.error_mode == ISIM_MODE_B;
+  // one Lane per depth variant, reused trace after trace as a GPU lane is
+  // (tree.hip hands a lane its next trace as soon as one responds)
+  tw::Lane<4, true> b4;
+  tw::Lane<8, true> b8;
+  tw::Lane<16, true> b16;
+  tw::Lane<4, false> a4;
+  tw::Lane<8, false> a8;
+  tw::Lane<16, false> a16;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t lat = 0, hops = 0, errh = 0;
+    bool r500 = false;
+    auto run = [&](auto &L) {
+      L.start(begin + i, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), prog.tree_nodes.data(), prog.tree_ext.data());
+      while (!L.done) L.step(prog.tree_nodes.data(), prog.tree_ext.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      lat = L.lat;
+      hops = L.hopn;
+      errh = L.errh;
+      r500 = L.root500;
+    };
+    // the register-stack depth the device compiles for this graph (tree.hip tree_kernel)
+    const uint32_t fr = prog.tree_frames;
+    if (modeb) {
+      if (fr <= 4) run(b4);
+      else if (fr <= 8) run(b8);
+      else run(b16);
+    } else {
+      if (fr <= 4) run(a4);
+      else if (fr <= 8) run(a8);
+      else run(a16);
+    }
+    std::printf("rec %u %u %d %u\n", lat, hops, r500 ? 1 : 0, errh);
+    root_hist[(r500 ? ISIM_N_PROM : 0) + prom_bucket_ns(lat)] += 1;
+    root_sum[r500 ? 1 : 0] += lat;
+  }
+  // per call site and per service, as isim_stats_fold
+  std::vector<uint64_t> site(prog.n_sites, 0), svc_calls(prog.n_services, 0), svc_errs(prog.n_services, 0);
+  for (uint32_t s = 0; s < S; ++s) {
+    site[prog.slot_site[s]] += sk.calls[s];
+    svc_calls[prog.slot_callee[s]] += sk.calls[s];
+    svc_errs[prog.slot_callee[s]] += sk.errs[s];
+  }
+  uint64_t n500 = 0;
+  for (uint32_t b = 0; b < ISIM_N_PROM; ++b) n500 += root_hist[ISIM_N_PROM + b];
+  svc_calls[prog.entry] += n;
+  svc_errs[prog.entry] += n500;
+  std::printf("site");
+  for (uint64_t v : site) std::printf(" %llu", (unsigned long long)v);
+  std::printf("\nsvc");
+  for (uint64_t v : svc_calls) std::printf(" %llu", (unsigned long long)v);
+  std::printf("\nerr");
+  for (uint64_t v : svc_errs) std::printf(" %llu", (unsigned long long)v);
+  std::printf("\n");
+  // duration rows: the kernel's flush (static buckets from the slot counters)
+  std::vector<std::vector<uint64_t>> row(R, std::vector<uint64_t>(ISIM_SVC_DUR_WORDS, 0));
+  if (sk.out_of_table) {
+    std::fprintf(stderr, "a duration fell outside its row's bucket table (tmin/tmax bounds wrong)\n");
+    return 4;
+  }
+  for (uint32_t r = 0; r < R; ++r) {
+    row[r][2 * ISIM_N_PROM] = sk.sum200[r];
+    row[r][2 * ISIM_N_PROM + 1] = sk.sum500[r];
+  }
+  for (const TreeDynRow &d : prog.tree_dyn)
+    for (uint32_t code = 0; code < 2; ++code)
+      for (uint32_t j = 0; j < d.width; ++j) row[d.row][code * ISIM_N_PROM + d.b_lo + j] += sk.dyn[d.off + 1 + code * d.width + j];
+  for (uint32_t s = 0; s < S; ++s) {
+    const uint32_t w = prog.slot_tbkt[s], r = w & kDurRowMask, b = w >> 24;
+    if (b == kTreeDynBucket) continue;
+    row[r][b] += sk.calls[s] - sk.errs[s];
+    row[r][ISIM_N_PROM + b] += sk.errs[s];
+  }
+  for (uint32_t w = 0; w < 2 * ISIM_N_PROM; ++w) row[0][w] += root_hist[w];
+  row[0][2 * ISIM_N_PROM] += root_sum[0];
+  row[0][2 * ISIM_N_PROM + 1] += root_sum[1];
+  for (uint32_t r = 0; r < R; ++r) {
+    std::printf("dur %d", prog.row_svc[r]);
+    for (uint64_t v : row[r]) std::printf(" %llu", (unsigned long long)v);
+    std::printf("\n");
+  }
+  return 0;
+}

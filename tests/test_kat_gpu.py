@@ -24,8 +24,9 @@ KERNELS = {
     "stream_walk": N.FLAG_WALK_ALL,                # kinds 4 (mode A) / 6 (mode B close list)
     "bitstack": N.FLAG_WALK_ALL | N.FLAG_BIT_STACK,  # mode B: kind 5
     "interp": N.FLAG_NO_STREAM,                    # static interpreter, kinds 0/1
-    "dynamic": N.FLAG_DYNAMIC,                     # general kernel, kinds 2/3 (per-lane time)
+    "dynamic": N.FLAG_DYNAMIC,                     # general path: the lane tree walk, kind 7
     "dynamic_nodur": N.FLAG_DYNAMIC | N.FLAG_NO_SVC_DUR,
+    "dynamic_wave": N.FLAG_DYNAMIC | N.FLAG_WAVE_WALK,  # the wave walk, kinds 2/3 (per-lane time)
 }
 
 
@@ -41,8 +42,10 @@ def test_kat_hip(gpu, case, kernel):
     h = isim.Handler(g, case["entry"], isim.SimParams(seed=1, hop_base_ns=hop, req_ps_per_byte=req,
                                                       resp_ps_per_byte=resp, error_mode=mode, flags=flags))
     kind = h.launch_info(0)["kernel_kind"]
-    if kernel.startswith("dynamic"):
+    if kernel == "dynamic_wave":
         assert kind in (2, 3)
+    elif kernel.startswith("dynamic"):
+        assert kind == (7 if h.info.time_bits == 32 else 3)
     elif kernel == "interp":
         assert kind in (0, 1) or not h.info.static_walk
     n = 3000

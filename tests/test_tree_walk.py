@@ -1,0 +1,157 @@
+"""The lane tree walk (kernel kind 7, csrc/tree_walk.h) on the CPU: the
+per-lane code the HIP kernel runs, over the product's own loader and program
+compiler (built here with g++ by tests/cpp/tree_walk_check.cpp), with the
+kernel's accounting of the statistics, against the C oracle bit for bit —
+records, per-site / per-service counters and the per-service duration
+table.  This pins the tree encoding (TreeNode/TreeExt: step starts,
+concurrent maxima, skipped subtrees, mode-B aborts, static duration buckets)
+before the GPU runs it; tests/test_walk_gpu.py runs the kernel itself."""
+import glob
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import kat
+from conftest import ROOT, TOPOLOGIES
+from isim.generators import mesh_topology, realistic_topology
+from isim.yamljson import obj_to_json, yaml_to_json
+from oracle import executor as oc
+from oracle import graph_ref as gr
+from oracle.executor_py import SimGraph, SimParams
+from parity import with_defaults
+from test_oracle import random_graph
+
+CSRC = os.path.join(ROOT, "istio-isotope_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    out = str(tmp_path_factory.mktemp("twc") / "tree_walk_check")
+    srcs = [os.path.join(ROOT, "tests", "cpp", "tree_walk_check.cpp")] + \
+        [os.path.join(CSRC, f) for f in ("json.cpp", "gounits.cpp", "graph.cpp", "program.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs,
+                    "-o", out], check=True)
+    return out
+
+
+def run_check(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80, resp=80, begin=0, n=500):
+    path = tmp_path / "g.json"
+    path.write_text(j)
+    r = subprocess.run([checker, str(path), str(mode), str(seed), str(hop), str(req), str(resp), str(begin), str(n)],
+                       capture_output=True, text=True)
+    if r.returncode == 3:
+        return None
+    assert r.returncode == 0, r.stderr + r.stdout
+    recs, out = [], {"dur": {}}
+    for line in r.stdout.splitlines():
+        f = line.split()
+        if f[0] == "rec":
+            recs.append(tuple(int(x) for x in f[1:]))
+        elif f[0] == "dur":
+            out["dur"][int(f[1])] = [int(x) for x in f[2:]]
+        else:
+            out[f[0]] = [int(x) for x in f[1:]]
+    return recs, out
+
+
+def compare(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80, resp=80, begin=0, n=500):
+    got = run_check(checker, tmp_path, j, mode, seed, hop, req, resp, begin, n)
+    if got is None:
+        return False
+    recs, out = got
+    sg = SimGraph(gr.unmarshal_service_graph(j))
+    p = SimParams(seed, hop, req, resp, mode)
+    orec, ost = oc.run(sg, p, sg.entry(), begin, n, records=True, n_threads=1)
+    want = [(int(r[0]), int(r[1]) & 0xFFFFFFFF, int(r[1]) >> 63, (int(r[1]) >> 32) & 0x7FFFFFFF) for r in orec]
+    bad = [i for i, (a, b) in enumerate(zip(recs, want)) if a != b]
+    assert not bad, f"{len(bad)} records differ; first {bad[0]}: tree {recs[bad[0]]} oracle {want[bad[0]]}"
+    o = oc.split_stats(ost, len(sg.g.services), len(sg.sites))
+    assert out["site"] == [int(x) for x in o["site_calls"]]
+    assert out["svc"] == [int(x) for x in o["svc_calls"]]
+    assert out["err"] == [int(x) for x in o["svc_errs"]]
+    for s, row in out["dur"].items():
+        assert row == [int(x) for x in o["svc_dur"][s]], f"duration row of service {s}"
+    # services the tree never reaches have empty rows in the oracle too
+    reached = set(out["dur"])
+    for s in range(len(sg.g.services)):
+        if s not in reached:
+            assert not np.any(o["svc_dur"][s]), s
+    return True
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_mesh(checker, tmp_path, mode):
+    """Config-4-shaped meshes: probabilistic fan-out, replicas, response sizes;
+    with and without error rates."""
+    j = obj_to_json(mesh_topology(1200, 6, seed=3))
+    assert compare(checker, tmp_path, j, mode, n=2000)
+    assert compare(checker, tmp_path, with_defaults(j, errorRate=0.05), mode, n=2000)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(TOPOLOGIES, "*.yaml"))),
+                         ids=lambda p: os.path.basename(p))
+@pytest.mark.parametrize("mode", [0, 1])
+def test_reference_topologies(checker, tmp_path, path, mode):
+    j = with_defaults(yaml_to_json(open(path, "rb").read()), errorRate=0.1)
+    compare(checker, tmp_path, j, mode, n=400)
+
+
+@pytest.mark.parametrize("case", kat.CASES, ids=kat.case_id)
+def test_kat_graphs(checker, tmp_path, case):
+    hop, req, resp, mode = kat.params(case)
+    j = kat.graph_json(case["graph"])
+    if case["entry"] is not None:
+        doc = json.loads(j)
+        for s in doc["services"]:
+            s.pop("isEntrypoint", None)
+            if s["name"] == case["entry"]:
+                s["isEntrypoint"] = True
+        j = json.dumps(doc)
+    got = run_check(checker, tmp_path, j, mode, 1, hop, req, resp, 0, 3)
+    if got is None:
+        pytest.skip("no tree")
+    for r in got[0]:
+        kat.check_record(case, *r)
+
+
+def test_probability_and_concurrency(checker, tmp_path):
+    """Concurrent steps whose calls may be skipped, sleeps inside and between
+    steps, negative sleeps, nested fan-out, mode-B aborts after a failing
+    sequential call and after a failing concurrent step."""
+    svcs = [
+        {"name": "e", "isEntrypoint": True, "errorRate": 0.05,
+         "script": [{"sleep": "3ms"}, [{"call": {"service": "a", "probability": 60}}, {"sleep": "2ms"},
+                                      {"call": {"service": "b", "probability": 40}}],
+                    {"sleep": "-5ms"}, {"call": {"service": "c", "probability": 70}}, {"sleep": "1ms"},
+                    [{"sleep": "4ms"}, {"sleep": "7ms"}], {"call": "d"}, {"sleep": "2ms"}]},
+        {"name": "a", "errorRate": 0.3, "script": [{"call": {"service": "d", "probability": 50}}, {"sleep": "1ms"}]},
+        {"name": "b", "errorRate": 0.2, "script": [[{"call": "d"}, {"call": {"service": "c", "probability": 30}}]]},
+        {"name": "c", "errorRate": 0.4, "script": [{"sleep": "6ms"}]},
+        {"name": "d", "errorRate": 0.25},
+    ]
+    j = json.dumps({"services": svcs})
+    for mode in (0, 1):
+        assert compare(checker, tmp_path, j, mode, n=3000)
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                  HealthCheck.function_scoped_fixture])
+@given(random_graph(), st.sampled_from([0, 1]), st.integers(0, 2 ** 64 - 1), st.integers(0, 2 ** 40))
+def test_random_graphs(checker, tmp_path, j, mode, seed, begin):
+    compare(checker, tmp_path, j, mode, seed=seed, begin=begin, n=60)
+
+
+def test_realistic_static(checker, tmp_path):
+    """A static graph on the general path (ISIM_FLAG_DYNAMIC): concurrent
+    fan-out over a Barabasi tree with sleeps and error rates."""
+    j = obj_to_json(realistic_topology(300, "multitier", 5, concurrent=True, sleep_ms=(1, 5), error_rate=(0, 0.1)))
+    for mode in (0, 1):
+        assert compare(checker, tmp_path, j, mode, n=300)

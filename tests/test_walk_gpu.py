@@ -26,7 +26,20 @@ def _fixture_json(path, error_rate=None):
     return j
 
 
-KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM, "bitstack": isim.native.FLAG_BIT_STACK}
+KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM, "bitstack": isim.native.FLAG_BIT_STACK,
+           # the general path on every graph: the lane tree walk (kind 7) and the wave walk (kinds 2/3)
+           "tree": isim.native.FLAG_DYNAMIC,
+           "wave": isim.native.FLAG_DYNAMIC | isim.native.FLAG_WAVE_WALK}
+STREAM_KINDS = (4, 5, 6)
+
+
+def dynamic_kind(handler, flags):
+    """Kernel kind a dynamic walk takes: 7 (lane tree walk) unless the wave
+    walk is asked for or the tree does not fit (u64 time), else 2/3."""
+    tb64 = handler.info.time_bits == 64
+    if (flags & isim.native.FLAG_WAVE_WALK) or tb64:
+        return 2 + int(tb64)
+    return 7
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
@@ -36,7 +49,9 @@ def test_reference_topologies(gpu, path, mode, kernel):
     c = Case(_fixture_json(path, error_rate=0.05), None, isim.SimParams(error_mode=mode, flags=KERNELS[kernel]))
     kind = c.handler.launch_info(0)["kernel_kind"]
     tb64 = c.handler.info.time_bits == 64
-    if c.handler.info.static_walk:
+    if not c.handler.info.static_walk:
+        assert kind == dynamic_kind(c.handler, KERNELS[kernel])
+    elif c.handler.info.static_walk:
         if kernel == "interp":
             assert kind == int(tb64)
         elif mode == isim.MODE_A:
@@ -45,8 +60,6 @@ def test_reference_topologies(gpu, path, mode, kernel):
             assert kind == 6  # mode B: the close list
         else:
             assert kind == (5 if c.handler.info.max_depth <= 32 else 4)
-    else:
-        assert kind == 2 + int(tb64)
     c.compare(0, 3000)
 
 
@@ -97,6 +110,20 @@ def test_probability_and_mode_b_abort(gpu):
         c = Case(j, None, isim.SimParams(error_mode=mode, seed=99))
         assert not c.handler.info.static_walk
         c.compare(5, 20000)
+
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_tree_walk_lane_refill(gpu, mode):
+    """Kind 7 hands a lane its next trace as soon as one responds: the config-4
+    graph over more traces than the resident waves' first batches (every lane
+    walks many traces of different lengths), bit-exact against the oracle —
+    per-trace state (Philox caches, the frame stack) must not leak between a
+    lane's traces."""
+    c = Case(with_defaults(obj_to_json(mesh_topology()), errorRate=0.01), None, isim.SimParams(error_mode=mode))
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7
+    n = 3 * li["max_blocks"] * li["wg_threads"] + 777  # three batches of 64 per wave, and a ragged one
+    c.compare((1 << 32) - 5000, n)
 
 
 def test_large_latency_u64(gpu):
@@ -196,7 +223,7 @@ def test_batch_queue_claims(gpu, kernel):
     c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
              isim.SimParams(flags=KERNELS[kernel]))
     li = c.handler.launch_info(0)
-    per = 128 if li["kernel_kind"] >= 4 else 64
+    per = 128 if li["kernel_kind"] in STREAM_KINDS else 64
     n = 3 * li["max_blocks"] * li["wg_threads"] // 64 * per + 4097
     c.compare(11, n)
 
@@ -207,7 +234,7 @@ def test_batch_queue_rearms(gpu, kernel):
     c = Case(_fixture_json(os.path.join(TOPOLOGIES, "canonical.yaml"), 0.3), None,
              isim.SimParams(flags=KERNELS[kernel]))
     li = c.handler.launch_info(0)
-    per = 128 if li["kernel_kind"] >= 4 else 64
+    per = 128 if li["kernel_kind"] in STREAM_KINDS else 64
     n = 2 * li["max_blocks"] * li["wg_threads"] // 64 * per + 999
     _, one = c.gpu(0, n, records=False)
     dev = torch.device("cuda", 0)

@@ -1,0 +1,4 @@
+#!/bin/bash
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+bash tools/profile_cfg.sh c4 "--config c4" || exit $?

@@ -1,7 +1,8 @@
-"""Summarise a rocprofv3 profile set of bench.py (produced by tools/profile.sh)
-into profiles/pmc_summary.json and copy the CSVs judged into profiles/<round>/.
+"""Summarise a rocprofv3 profile set of bench.py (produced by
+tools/profile_cfg.sh) into profiles/pmc_summary_<name>.json and copy the
+CSVs judged into profiles/<round>/<name>/.
 
-    python tools/pmc_summary.py gpurun_out/prof3 r01
+    python tools/pmc_summary.py gpurun_out/prof_c4 r02 c4
 
 HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3): the
 FETCH_SIZE and WRITE_SIZE passes run separately; FETCH_SIZE (KiB) is doubled
@@ -16,7 +17,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "isim_walk"
+KERNEL = "isim_walk"  # replaced in main() by the profile's dominant isim kernel (isim_walk / isim_tree)
 
 
 def counters(path):
@@ -44,15 +45,18 @@ def occupancy(wave_cycles, grbm_gui_active, xcds=8):
             "formula": "4*SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE/8) / 256 CUs"}
 
 
-def main(src, rnd):
-    dst = os.path.join(ROOT, "profiles", rnd)
+def main(src, rnd, name):
+    dst = os.path.join(ROOT, "profiles", rnd, name)
     os.makedirs(dst, exist_ok=True)
+    global KERNEL
     stats_rows = list(csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv"))))
-    walk = [r for r in stats_rows if KERNEL in r["Name"]][0]
+    walk = max((r for r in stats_rows if "isim::dev::isim_" in r["Name"]), key=lambda r: float(r["TotalDurationNs"]))
+    KERNEL = walk["Name"].split("(")[0]
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "stats", "run_kernel_trace.csv"), os.path.join(dst, "kernel_trace.csv"))
-    for p in ("fetch", "write", "sq1", "sq2"):
-        shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
+    for p in ("fetch", "write", "sq1", "sq2", "sq3"):
+        if os.path.exists(os.path.join(src, p, "run_counter_collection.csv")):
+            shutil.copy(os.path.join(src, p, "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
     bench_line = [l for l in open(os.path.join(src, "stats.log")) if l.startswith("{")][-1]
     with open(os.path.join(dst, "bench_under_rocprof.json"), "w") as f:
         f.write(bench_line)
@@ -69,10 +73,11 @@ def main(src, rnd):
     xcds = 8
     out = {
         "round": int(rnd.lstrip("r")),
-        "config": bench["config"].get("name", "c3"),
+        "config": name,
         "batch": n,
-        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py ; PMC passes: --pmc FETCH_SIZE | "
-                   "WRITE_SIZE | SQ_* (bench.py --steps 3 --warmup 1 --no-cpu)",
+        "command": f"tools/profile_cfg.sh {name}: rocprofv3 --kernel-trace --stats -- python3 bench.py "
+                   f"{bench_args(src)}; PMC passes: --pmc FETCH_SIZE | WRITE_SIZE | SQ_* (bench.py ... --steps 3 "
+                   "--warmup 1 --no-cpu)",
         "kernel": walk["Name"],
         "kernel_avg_ns": kernel_ns,
         "kernel_calls": int(walk["Calls"]),
@@ -97,10 +102,22 @@ def main(src, rnd):
         "valu_issue_frac": sq1["SQ_INSTS_VALU"] / (sq2["GRBM_GUI_ACTIVE"] / xcds * CUS),
         "salu_issue_frac": sq1["SQ_INSTS_SALU"] / (sq2["GRBM_GUI_ACTIVE"] / xcds * CUS),
     }
-    with open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w") as f:
+    sq3_path = os.path.join(src, "sq3", "run_counter_collection.csv")
+    if os.path.exists(sq3_path):
+        sq3, _ = counters(sq3_path)
+        if sq3.get("SQ_ACTIVE_INST_VALU"):
+            # lanes doing work per VALU instruction (SQ_THREAD_CYCLES_VALU counts
+            # thread-cycles, SQ_ACTIVE_INST_VALU instruction-cycles; x64 lanes)
+            out["valu_lane_utilisation"] = sq3["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq3["SQ_ACTIVE_INST_VALU"])
+        out["sq3"] = sq3
+    with open(os.path.join(ROOT, "profiles", f"pmc_summary_{name}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
 
+def bench_args(src):
+    return open(os.path.join(src, "args")).read().strip() if os.path.exists(os.path.join(src, "args")) else ""
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3])
