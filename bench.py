@@ -306,6 +306,14 @@ def merge(h, multi, stats, sptr):
         merge_stats(stats)
 
 
+def kernel_name(launch) -> str:
+    """The dominant kernel of a walk launch: the lane tree walk (kind 7) or
+    the walk kernels (kinds 0-6)."""
+    if launch["kernel_kind"] == 7:
+        return "isim_tree"
+    return f"isim_walk<{launch['kernel_kind']}"
+
+
 def time_walk(h, steps, warmup, B, recs, stats, rank, world, dev, multi=None):
     """W untimed + K timed launches of isim_serve_device over B traces per
     rank (trace ids sharded globally), then the stats all-reduce; returns
@@ -441,7 +449,9 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            if pmc.get("config") == args.config and pmc.get("batch") == B:
+            # only a profile of the same kernel (name and template) describes this run
+            if pmc.get("config") == args.config and pmc.get("batch") == B and \
+                    kernel_name(launch) in str(pmc.get("kernel", "")):
                 traffic = pmc.get("hbm_bytes_per_launch")
                 occupancy["measured"] = pmc.get("occupancy")
         except Exception:
@@ -469,7 +479,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "isim_fill_const (draw-free walk: one trace walked, records filled)"
-                     if launch["fill"] else "isim_walk", "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
+                     if launch["fill"] else kernel_name(launch), "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes},
         "compute_roofline": None if launch["fill"] else compute_roofline(stream, info, B, kern_ms),
         "occupancy": occupancy,
         "hop_visits_per_s": value * hops_per_trace,

@@ -50,7 +50,11 @@ def main(src, rnd, name):
     os.makedirs(dst, exist_ok=True)
     global KERNEL
     stats_rows = list(csv.DictReader(open(os.path.join(src, "stats", "run_kernel_stats.csv"))))
-    walk = max((r for r in stats_rows if "isim::dev::isim_" in r["Name"]), key=lambda r: float(r["TotalDurationNs"]))
+    # the bench line's own kernel (its launch kind), not other legs' (c3 also times mode B)
+    line = json.loads([l for l in open(os.path.join(src, "stats.log")) if l.startswith("{")][-1])
+    kind = line["config"]["launch"]["kernel_kind"]
+    prefix = "isim::dev::isim_tree<" if kind == 7 else f"isim::dev::isim_walk<{kind},"
+    walk = max((r for r in stats_rows if prefix in r["Name"]), key=lambda r: float(r["TotalDurationNs"]))
     KERNEL = walk["Name"].split("(")[0]
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     shutil.copy(os.path.join(src, "stats", "run_kernel_trace.csv"), os.path.join(dst, "kernel_trace.csv"))
