@@ -118,10 +118,10 @@ __device__ __forceinline__ uint64_t des_exp_q24(uint32_t u) {
 // >= t.  The edges are whole milliseconds in six arithmetic runs (7..12 by 1,
 // 14..20 by 2, 25..50 by 5, 60..100 by 10, 120..200 by 20, 250..500 by 50), so
 // with m = ceil(t / 1 ms) (t <= e ms  <=>  m <= e) the bucket is the run's
-// base + ceil((m - run start) / step): ~20 integer ops instead of 32 compares.
-__device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
-  if (t > 500000000ull) return 32;
-  const uint32_t m = ((uint32_t)t + 999999u) / 1000000u;
+// base + ceil((m - run start) / step).  The kernels look m up in a 501-byte
+// LDS table built from this formula (des_bucket_lut: 7 VALU per duration
+// instead of 57).
+__device__ __forceinline__ uint32_t des_prom_bucket_m(uint32_t m) {
   const uint32_t lo = m <= 12 ? 7 : m <= 20 ? 12 : m <= 50 ? 20 : m <= 100 ? 50 : m <= 200 ? 100 : 200;
   const uint32_t base = m <= 12 ? 0 : m <= 20 ? 5 : m <= 50 ? 9 : m <= 100 ? 15 : m <= 200 ? 20 : 25;
   const uint32_t d = m <= 12 ? 1 : m <= 20 ? 2 : m <= 50 ? 5 : m <= 100 ? 10 : m <= 200 ? 20 : 50;
@@ -129,6 +129,14 @@ __device__ __forceinline__ uint32_t des_prom_bucket(uint64_t t) {
   const uint32_t M = m <= 12 ? 65536 : m <= 20 ? 32768 : m <= 50 ? 13108 : m <= 100 ? 6554 : m <= 200 ? 3277 : 1311;
   const uint32_t n = m > lo ? m - lo : 0;
   return base + (((n + d - 1) * M) >> 16);
+}
+constexpr uint32_t kBucketLut = 501;  // m = ceil(t / 1 ms) in 0..500
+// fills the workgroup's table (the caller's barrier publishes it)
+__device__ __forceinline__ void des_bucket_lut_init(uint8_t *lut) {
+  for (uint32_t m = threadIdx.x; m < kBucketLut; m += blockDim.x) lut[m] = (uint8_t)des_prom_bucket_m(m);
+}
+__device__ __forceinline__ uint32_t des_prom_bucket(const uint8_t *lut, uint64_t t) {
+  return t > 500000000ull ? 32u : lut[((uint32_t)t + 999999u) / 1000000u];
 }
 
 struct ChainState;
@@ -586,6 +594,7 @@ template <typename T, bool FUSED>
 __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uint64_t base, uint64_t N,
                                              uint64_t x, const uint64_t (&a)[kPer], const T (&r)[kPer],
                                              uint64_t off, uint32_t mask, uint32_t stm, T (&out)[kPer], uint32_t *hist,
+                                             const uint8_t *lut,
                                              uint64_t &wsum, uint64_t &wmax, uint64_t &d0, uint64_t &d1,
                                              uint64_t &n5, bool &bad) {
   uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
@@ -606,7 +615,7 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
         n5 += st;
         d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
         d0 += st ? 0 : dur;
-        bin[i] = st * ISIM_N_PROM + des_prom_bucket(dur);
+        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
         bad |= !Row<T>::fits(F);
         val = F | ((uint64_t)st << Row<T>::kTop);
       } else {
@@ -643,11 +652,14 @@ __device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
   __shared__ uint64_t red[3 * kDownThreads / 64];
   __shared__ MaxPlus xs[kDownThreads];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint8_t lut[kBucketLut];
   const DesPos P = k.pos[v];
   const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
-  if constexpr (FUSED)
+  if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
+    des_bucket_lut_init(lut);
+  }
   __syncthreads();
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
@@ -686,7 +698,7 @@ __device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
       const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
       const uint64_t cin = carry[r];
       const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
-      queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+      queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, lut, wsum, wmax, d0, d1, n5, bad);
       __syncthreads();  // every thread has read carry[r]
       if (threadIdx.x == kDownThreads - 1) {
         uint64_t xe = x;
@@ -762,9 +774,11 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   __shared__ MaxPlus xs[kDesThreads];
   __shared__ uint64_t red[3 * kDesThreads / 64];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint8_t lut[kBucketLut];
   __shared__ uint64_t s_carry;
   if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
+    des_bucket_lut_init(lut);
     __syncthreads();
   }
   const DesPos P = k.pos[v];
@@ -852,7 +866,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   T o[kPer] = {0, 0, 0, 0};
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;
-  queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, wsum, wmax, d0, d1, n5, bad);
+  queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, lut, wsum, wmax, d0, d1, n5, bad);
   if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
   store4t<T>(out, base, N, o);
   flag_overflow(k, bad);
@@ -884,7 +898,9 @@ template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
+  __shared__ uint8_t lut[kBucketLut];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hist[i] = 0;
+  des_bucket_lut_init(lut);
   __syncthreads();
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.y];
   const DesPos P = k.pos[v];
@@ -971,7 +987,7 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
         n500 += st;
         dsum1 += st ? dur : 0;
         dsum0 += st ? 0 : dur;
-        bin[i] = st * ISIM_N_PROM + des_prom_bucket(dur);
+        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
       }
     }
     hist_add4(hist, bin);
@@ -993,8 +1009,10 @@ template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
   __shared__ uint64_t red[5 * kDesUpThreads / 64];
+  __shared__ uint8_t lut[kBucketLut];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hp[i] = 0;
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads) hl[i] = 0;
+  des_bucket_lut_init(lut);
   __syncthreads();
   const uint64_t N = k.N;
   // an overflowed narrow batch is dropped (des_commit): records untouched
@@ -1019,7 +1037,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
     n5 += st;
     mn = L < mn ? L : mn;
     mx = L > mx ? L : mx;
-    atomicAdd(&hp[st * ISIM_N_PROM + des_prom_bucket(L)], 1u);
+    atomicAdd(&hp[st * ISIM_N_PROM + des_prom_bucket(lut, L)], 1u);
     atomicAdd(&hl[st * ISIM_N_LOG2 + (L ? 64u - (uint32_t)__builtin_clzll(L) : 0u)], 1u);
   }
 #pragma unroll
