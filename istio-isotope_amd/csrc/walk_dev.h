@@ -95,15 +95,25 @@ __device__ __forceinline__ void count(uint64_t *__restrict__ gstats, uint32_t *c
 
 // service_request_duration_seconds buckets (srv/prometheus/handler.go:26-31):
 // bucket = first i with t <= edge_i ms  <=>  ceil(t / 1ms) <= edge_i.
+// A 512-byte table of buckets by m = ceil(t / 1 ms) (0..500), built at
+// compile time; per-lane lookups hit L1 (the LDS of the lane tree walk is
+// full): 7 VALU per duration instead of a 32-compare chain.
+struct BucketTable {
+  uint8_t b[512];
+  constexpr BucketTable() : b() {
+    const uint32_t e[32] = {7, 8, 9, 10, 11, 12, 14, 16, 18, 20, 25, 30, 35, 40, 45, 50,
+                            60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
+    for (uint32_t m = 0; m < 512; ++m) {
+      uint32_t k = 0;
+      for (uint32_t i = 0; i < 32; ++i) k += e[i] < m ? 1u : 0u;
+      b[m] = (uint8_t)k;
+    }
+  }
+};
+__device__ constexpr BucketTable kBucketTable{};
 __device__ __forceinline__ uint32_t prom_bucket(uint64_t t) {
   if (t > 500000000ull) return 32;
-  const uint32_t c = (uint32_t)((t + 999999ull) / 1000000ull);  // <= 500
-  const uint32_t e[32] = {7, 8, 9, 10, 11, 12, 14, 16, 18, 20, 25, 30, 35, 40, 45, 50,
-                          60, 70, 80, 90, 100, 120, 140, 160, 180, 200, 250, 300, 350, 400, 450, 500};
-  uint32_t b = 0;
-#pragma unroll
-  for (int i = 0; i < 32; ++i) b += e[i] < c ? 1u : 0u;
-  return b;
+  return kBucketTable.b[((uint32_t)t + 999999u) / 1000000u];  // ceil(t / 1ms) <= 500
 }
 
 // Wave-aggregated LDS histogram add: one ds_add per distinct key.
