@@ -787,6 +787,10 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   const isim::DesPlan &d = h->des;
   if (n_traces * (uint64_t)std::max<uint32_t>(1, d.max_sort_pos) > 0xFFFFFFFFull)
     return fail(ISIM_EINVAL, "n_traces x positions of one service above 2^32 per DES batch");
+  // the queue scans' keys a_t - t * hold are signed 64-bit (des.hip down passes)
+  if ((long double)n_traces * (long double)d.max_hold +
+          (long double)n_traces * dp->mean_interarrival_ns * 17.0L >= std::ldexp(1.0L, 62))
+    return fail(ISIM_EINVAL, "DES batch too long for its worker hold times (n_traces x hold above 2^62 ns)");
   if (d.max_rep_bits) {
     // sort keys hold replica | arrival: the batch's arrival span (an exponential
     // gap is at most 24 ln 2 = 16.6 means) plus the static latency must fit

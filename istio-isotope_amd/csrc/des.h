@@ -96,6 +96,7 @@ struct DesPlan {
   std::vector<uint32_t> fin_round_off;           // [rounds + 1] into the finish groups
   uint32_t max_sort_pos = 0;         // most positions of one sort-path service
   uint32_t max_rep_bits = 0;         // sort keys: bits of the largest replica index of a sort-path service
+  uint64_t max_hold = 0;             // longest worker hold time of any position (queue scan keys)
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 

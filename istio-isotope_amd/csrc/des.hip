@@ -390,6 +390,74 @@ __device__ __forceinline__ uint64_t block_scan_add(uint64_t v, uint64_t *wtot, u
   return v;  // inclusive
 }
 
+// ---- single-replica queues in closed form.  A FIFO worker with hold h fed
+// arrivals a_t in trace order starts trace t at
+//   S_t = max(S_{t-1} + h, a_t) = t h + max_{s <= t} (a_s - s h)
+// (an idle worker at time 0 contributes 0), so the queue is ONE running max
+// of the signed keys a_t - t h: a wave max-scan by DPP row shifts and row
+// broadcasts, wave totals through LDS, the carry across chunks a running max
+// (the host bounds n_traces x hold below 2^62, api.hip).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int64_t dpp_i64(int64_t old, int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)v, CTRL, ROW_MASK,
+                                                           0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)((uint64_t)old >> 32),
+                                                           (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROW_MASK, 0xF,
+                                                           false);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t max_i64(int64_t a, int64_t b) { return a > b ? a : b; }
+constexpr int64_t kKeyMin = INT64_MIN;
+// inclusive max-scan over the wave's 64 lanes
+__device__ __forceinline__ int64_t wave_max_scan(int64_t v) {
+  v = max_i64(v, dpp_i64<0x111, 0xF>(kKeyMin, v));  // row_shr:1
+  v = max_i64(v, dpp_i64<0x112, 0xF>(kKeyMin, v));  // row_shr:2
+  v = max_i64(v, dpp_i64<0x114, 0xF>(kKeyMin, v));  // row_shr:4
+  v = max_i64(v, dpp_i64<0x118, 0xF>(kKeyMin, v));  // row_shr:8
+  v = max_i64(v, dpp_i64<0x142, 0xA>(kKeyMin, v));  // row_bcast:15 into rows 1, 3
+  v = max_i64(v, dpp_i64<0x143, 0xC>(kKeyMin, v));  // row_bcast:31 into rows 2, 3
+  return v;
+}
+// the previous lane's value (lane 0: kKeyMin)
+__device__ __forceinline__ int64_t wave_shr1(int64_t v) { return dpp_i64<0x138, 0xF>(kKeyMin, v); }
+__device__ __forceinline__ int64_t read_lane(int64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// the block's wave totals (LDS, NW <= 16): pre = max(carry, totals of the
+// waves before `wave`), carry = max(carry, all totals); both wave-uniform
+template <uint32_t NW>
+__device__ __forceinline__ void fold_totals(const int64_t *wtot, uint32_t wave, int64_t &carry, int64_t &pre) {
+  static_assert(NW >= 2 && NW <= 16, "one DPP row of wave totals");
+  const uint32_t lane = threadIdx.x & 63u;
+  int64_t v = lane < NW ? wtot[lane] : kKeyMin;
+  v = max_i64(v, dpp_i64<0x111, 0xF>(kKeyMin, v));
+  v = max_i64(v, dpp_i64<0x112, 0xF>(kKeyMin, v));
+  v = max_i64(v, dpp_i64<0x114, 0xF>(kKeyMin, v));
+  if constexpr (NW > 8) v = max_i64(v, dpp_i64<0x118, 0xF>(kKeyMin, v));
+  const int64_t before = wave ? read_lane(v, wave - 1) : kKeyMin;
+  pre = max_i64(carry, before);
+  carry = max_i64(carry, read_lane(v, NW - 1));
+}
+// the largest key a_t - t h of this thread's (up to) 4 traces from `base`
+// (kKeyMin: none), and their mask
+__device__ __forceinline__ int64_t queue_keys(const uint64_t (&a)[kPer], uint64_t base, uint64_t N, uint64_t hold,
+                                              uint32_t &mask) {
+  int64_t kt = kKeyMin;
+  uint64_t th = base * hold;
+  mask = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    if (base + i < N) {
+      kt = max_i64(kt, (int64_t)(a[i] - th));
+      mask |= 1u << i;
+    }
+    th += hold;
+  }
+  return kt;
+}
+
 // ---- arrivals: per chunk inclusive prefix of the inter-arrival times
 __global__ void __launch_bounds__(kDesThreads) des_arrivals(DesK k) {
   __shared__ uint64_t wtot[kDesThreads / 64];
@@ -645,8 +713,65 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 
 // ---- queue pass, one workgroup per position (wide groups; replicated
 // services: per-replica scans, the routing draw per trace)
+// single-replica services: the closed form, one barrier per chunk (the wave
+// totals double-buffered; every thread folds them into its prefix and into the
+// carry itself)
+template <typename T, bool FUSED>
+__device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
+  constexpr uint32_t NW = kDownThreads / 64;
+  __shared__ int64_t wtot[2][NW];
+  __shared__ uint64_t red[3 * NW];
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint8_t lut[kBucketLut];
+  const DesPos P = k.pos[v];
+  if constexpr (FUSED) {
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
+    des_bucket_lut_init(lut);
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t N = k.N;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
+  T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
+  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
+  bool bad = false;
+  int64_t carry = 0;  // max key of the chunks before (0: the idle start)
+  uint32_t buf = 0;
+  for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
+    const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+    uint64_t a[kPer];
+    T o[kPer] = {0, 0, 0, 0};
+    T ar[kPer];
+    load_arrivals<T>(k, par, off, base, N, a, ar);
+    const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
+    uint32_t mask;
+    const int64_t inc = wave_max_scan(queue_keys(a, base, N, P.hold, mask));
+    const int64_t exc = wave_shr1(inc);
+    if (lane == 63) wtot[buf][wave] = inc;
+    __syncthreads();
+    // lanes 0..NW-1 scan the wave totals: the waves before this one and all
+    int64_t pre;
+    fold_totals<NW>(wtot[buf], wave, carry, pre);
+    pre = max_i64(pre, exc);
+    buf ^= 1u;
+    const uint64_t x = base * P.hold + (uint64_t)pre;  // the worker's ready time before trace `base`
+    queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, lut, wsum, wmax, d0, d1, n5, bad);
+    if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
+    store4t<T>(out, base, N, o);
+  }
+  flag_overflow(k, bad);
+  if (k.quiet) return;
+  des_flush_waits<kDownThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
+  if constexpr (FUSED) {
+    __syncthreads();
+    des_flush_durations<kDownThreads>(k, P, hist, d0, d1, n5, red);
+  }
+}
+
+// replicated services: per-replica max-plus scans
 template <typename T, bool MULTI, bool FUSED>
-__device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
+__device__ __forceinline__ void downr_body(const DesK &k, uint32_t v) {
   __shared__ MaxPlus wtot[kDownThreads / 64];
   __shared__ uint64_t carry[kDesMaxReplicas];
   __shared__ uint64_t red[3 * kDownThreads / 64];
@@ -722,6 +847,12 @@ __device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
 }
 
 template <typename T, bool MULTI, bool FUSED>
+__device__ __forceinline__ void down_body(const DesK &k, uint32_t v) {
+  if constexpr (MULTI) downr_body<T, true, FUSED>(k, v);
+  else down1_body<T, FUSED>(k, v);
+}
+
+template <typename T, bool MULTI, bool FUSED>
 __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down(DesK k) {
   down_body<T, MULTI, FUSED>(k, k.level_pos[k.level_begin + blockIdx.x]);
 }
@@ -741,8 +872,8 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_mi
 // launch order (position-major, chunk-minor), so every chunk they wait on
 // has started.
 struct ChainState {
-  uint64_t B, C;   // the chunk's max-plus map (flag >= 1)
-  uint64_t P;      // the queue's carry after the chunk (flag 2)
+  uint64_t B, C;   // B: the chunk's largest key a_t - t h, as int64 (flag >= 1); C unused
+  uint64_t P;      // the largest key up to and including the chunk (flag 2)
   uint32_t flag, pad;
 };
 static_assert(sizeof(ChainState) == 32, "ChainState is 32 bytes");
@@ -770,16 +901,15 @@ __device__ __forceinline__ uint32_t chain_ticket(const DesK &k) {
 
 template <typename T, bool FUSED>
 __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t chunk) {
-  __shared__ MaxPlus wtot[kDesThreads / 64];
-  __shared__ MaxPlus xs[kDesThreads];
+  constexpr uint32_t NW = kDesThreads / 64;
+  __shared__ int64_t wtot[NW];
   __shared__ uint64_t red[3 * kDesThreads / 64];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint8_t lut[kBucketLut];
-  __shared__ uint64_t s_carry;
+  __shared__ int64_t s_carry;
   if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
     des_bucket_lut_init(lut);
-    __syncthreads();
   }
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
@@ -787,38 +917,32 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   const uint64_t off = par ? P.off : 0;
   T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
   ChainState *cs = k.chain + (uint64_t)v * k.n_chunks;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
   uint64_t a[kPer];
   T ar[kPer];
   load_arrivals<T>(k, par, off, base, N, a, ar);
   const uint32_t stm = FUSED && base < N ? des_status4(k, v, base) : 0u;
-  MaxPlus f{0, 0};
-  uint32_t mask = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i)
-    if (base + i < N) {
-      f = mp_then(f, MaxPlus{P.hold, a[i] + P.hold});
-      mask |= 1u << i;
-    }
-  const MaxPlus inc = mp_block_scan(f, wtot);
-  xs[threadIdx.x] = inc;
+  uint32_t mask;
+  const int64_t inc = wave_max_scan(queue_keys(a, base, N, P.hold, mask));
+  const int64_t exc = wave_shr1(inc);
+  if (lane == 63) wtot[wave] = inc;
   __syncthreads();
   if (threadIdx.x < 64) {
-    // wave 0: publish this chunk's map, then look back (64 chunks per step)
-    // for the carry into it.  Hand-offs between workgroups (other XCDs
-    // included) use sc1 stores drained before the flag store and sc1 loads
-    // (no L2 writeback / invalidate).
-    const uint32_t lane = threadIdx.x;
-    const MaxPlus agg = xs[kDesThreads - 1];
+    // wave 0: publish this chunk's largest key, then look back (64 chunks
+    // per step) for the largest key before it.  Hand-offs between workgroups
+    // (other XCDs included) use sc1 stores drained before the flag store and
+    // sc1 loads (no L2 writeback / invalidate).
+    int64_t agg = kKeyMin, unused;
+    fold_totals<NW>(wtot, 0, agg, unused);
     if (chunk > 0 && lane == 0) {
-      st_relaxed(&cs[chunk].B, agg.B);
-      st_relaxed(&cs[chunk].C, agg.C);
+      st_relaxed(&cs[chunk].B, (uint64_t)agg);
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
       st_flag(&cs[chunk].flag, 1u);
     }
-    uint64_t cin = 0;  // chunk 0 starts from an idle worker
+    int64_t cin = 0;  // chunk 0 starts from an idle worker
     if (chunk > 0) {
-      MaxPlus tot{0, 0};  // maps of the windows already passed (applied last)
+      int64_t run = kKeyMin;  // the windows already passed
       int64_t top = (int64_t)chunk - 1;
       uint32_t spins = 0;
       for (;;) {
@@ -832,37 +956,31 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
           if (++spins > (1u << 26)) break;  // never expected: tickets order the chunks
           continue;
         }
-        MaxPlus m{0, 0};
-        uint64_t pv = 0;
-        if (lane < f2 && j >= 0) m = MaxPlus{ld_relaxed(&cs[j].B), ld_relaxed(&cs[j].C)};
-        if (lane == f2 && j >= 0) pv = ld_relaxed(&cs[j].P);
-        // the window's maps, the farthest (highest lane) applied first
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-          const MaxPlus o{__shfl_xor(m.B, d, 64), __shfl_xor(m.C, d, 64)};
-          m = (lane & d) ? mp_then(m, o) : mp_then(o, m);
-        }
-        tot = mp_then(m, tot);
+        // chunks nearer than the first inclusive prefix give their own key,
+        // that chunk its prefix (the order does not matter for a max)
+        int64_t m = kKeyMin;
+        if (lane < f2 && j >= 0) m = (int64_t)ld_relaxed(&cs[j].B);
+        if (lane == f2) m = j >= 0 ? (int64_t)ld_relaxed(&cs[j].P) : 0;
+        run = max_i64(run, read_lane(wave_max_scan(m), 63));
         if (f2 < 64) {
-          const uint64_t x = __shfl(pv, f2, 64);
-          cin = x + tot.B > tot.C ? x + tot.B : tot.C;
+          cin = run;
           break;
         }
         top -= 64;
       }
     }
     if (lane == 0) {
-      const uint64_t pout = cin + agg.B > agg.C ? cin + agg.B : agg.C;
-      st_relaxed(&cs[chunk].P, pout);
+      st_relaxed(&cs[chunk].P, (uint64_t)max_i64(cin, agg));
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
       st_flag(&cs[chunk].flag, 2u);
       s_carry = cin;
     }
   }
   __syncthreads();
-  const MaxPlus pre = threadIdx.x ? xs[threadIdx.x - 1] : MaxPlus{0, 0};
-  const uint64_t cin = s_carry;
-  const uint64_t x = cin + pre.B > pre.C ? cin + pre.B : pre.C;
+  int64_t cin = s_carry, pre;
+  fold_totals<NW>(wtot, wave, cin, pre);
+  pre = max_i64(pre, exc);
+  const uint64_t x = base * P.hold + (uint64_t)pre;  // the worker's ready time before trace `base`
   T o[kPer] = {0, 0, 0, 0};
   uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
   bool bad = false;

@@ -107,6 +107,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     ps.slot = slot;
     ps.reps = (uint32_t)std::max<int32_t>(1, g.services[svc].num_replicas);
     ps.hold = sh.hold;
+    out.max_hold = std::max(out.max_hold, sh.hold);
     // one call step: F = max(S + floor, max_c F_c) + post; several: F =
     // max(BK_last + floor, max_c(last step) F_c) + post
     ps.floor = sh.leaf() ? sh.pre : (sh.smax.size() == 1 ? sh.pre + sh.smax[0] : sh.smax.back());

@@ -865,7 +865,6 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
                                                const uint32_t *__restrict__ close_slot, CU32 *__restrict__ close_end,
                                                const uint32_t *__restrict__ stream_w) {
   const uint32_t lane = lane_id();
-  const bool lane0 = lane == 0;
   uint64_t idx[TPL], all[TPL];
   uint32_t t_lo[TPL], t_hi[TPL], t_hi_u[TPL];
   bool valid[TPL];
