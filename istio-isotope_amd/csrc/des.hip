@@ -440,19 +440,17 @@ __device__ __forceinline__ void fold_totals(const int64_t *wtot, uint32_t wave, 
   pre = max_i64(carry, before);
   carry = max_i64(carry, read_lane(v, NW - 1));
 }
-// the largest key a_t - t h of this thread's (up to) 4 traces from `base`
-// (kKeyMin: none), and their mask
+// the keys a_t - t h of this thread's (up to) 4 traces from `base`
+// (kKeyMin past N) and their largest
+template <bool FULL>
 __device__ __forceinline__ int64_t queue_keys(const uint64_t (&a)[kPer], uint64_t base, uint64_t N, uint64_t hold,
-                                              uint32_t &mask) {
+                                              int64_t (&key)[kPer]) {
   int64_t kt = kKeyMin;
   uint64_t th = base * hold;
-  mask = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
-    if (base + i < N) {
-      kt = max_i64(kt, (int64_t)(a[i] - th));
-      mask |= 1u << i;
-    }
+    key[i] = FULL || base + i < N ? (int64_t)(a[i] - th) : kKeyMin;
+    kt = max_i64(kt, key[i]);
     th += hold;
   }
   return kt;
@@ -695,14 +693,57 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
   if constexpr (FUSED) hist_add4(hist, bin);
 }
 
+// Single-replica queues (closed form): from the thread's exclusive prefix p
+// the running max of the keys gives the wait of each trace, S_t - a_t =
+// p_t - key_t; the stored value (S or, fused, F | status, relative to A_t),
+// waits and durations as queue_finish.
+struct QAcc {
+  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
+  bool bad = false;
+};
+template <typename T, bool FUSED, bool FULL>
+__device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, uint64_t base, uint64_t N, int64_t p,
+                                              const int64_t (&key)[kPer], const T (&r)[kPer], uint64_t off,
+                                              uint32_t stm, T (&out)[kPer], uint32_t *hist, const uint8_t *lut,
+                                              QAcc &q) {
+  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    if (FULL || base + i < N) {
+      p = max_i64(p, key[i]);
+      const uint64_t w = (uint64_t)(p - key[i]);
+      q.wsum += w;
+      q.wmax = w > q.wmax ? w : q.wmax;
+      uint64_t val = w + (uint64_t)r[i] + off;  // S - A_t (off is 0 for the entry: r = 0)
+      if constexpr (FUSED) {
+        const uint64_t F = val + P.floor;
+        const uint32_t st = (stm >> i) & 1u;
+        const uint64_t dur = w + P.floor;  // F - a
+        if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
+        q.n5 += st;
+        q.d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
+        q.d0 += st ? 0 : dur;
+        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
+        q.bad |= !Row<T>::fits(F);
+        val = F | ((uint64_t)st << Row<T>::kTop);
+      } else {
+        q.bad |= !Row<T>::fits(val);
+      }
+      out[i] = (T)val;
+    }
+  }
+  if constexpr (FUSED) hist_add4(hist, bin);
+}
+
 // this thread's 4 traces: absolute arrivals a = A_t + relative arrival, and
 // the relative arrivals' row values r (S relative = wait + r + off)
-template <typename T>
+template <typename T, bool FULL = false>
 __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint64_t off, uint64_t base,
                                               uint64_t N, uint64_t (&a)[kPer], T (&r)[kPer]) {
-  load4a(k.A, base, N, a);
+  const uint64_t n = FULL ? base + kPer : N;  // whole: one vector access each
+  load4n<uint64_t>(k.A, base, n, a);
   if (par) {
-    load4t<T>(par, base, N, r);
+    load4t<T>(par, base, n, r);
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)r[i] + off;
   } else {
@@ -716,6 +757,36 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 // single-replica services: the closed form, one barrier per chunk (the wave
 // totals double-buffered; every thread folds them into its prefix and into the
 // carry itself)
+// one chunk of kPer x kDownThreads traces from c0 (FULL: all below N)
+template <typename T, bool FUSED, bool FULL>
+__device__ __forceinline__ void down1_chunk(const DesK &k, const DesPos &P, uint32_t v, const T *par, uint64_t off,
+                                            T *out, uint64_t c0, int64_t *wtot, int64_t &carry, uint32_t *hist,
+                                            const uint8_t *lut, QAcc &q) {
+  constexpr uint32_t NW = kDownThreads / 64;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t N = k.N;
+  uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+  // opaque to loop strength reduction, which otherwise keeps a dozen 64-bit
+  // induction variables ((base + i) * hold, ...) live across the chunk loop
+  __asm__ volatile("" : "+v"(base));
+  uint64_t a[kPer];
+  T ar[kPer];
+  load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
+  const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
+  int64_t key[kPer];
+  const int64_t inc = wave_max_scan(queue_keys<FULL>(a, base, N, P.hold, key));
+  const int64_t exc = wave_shr1(inc);
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  // lanes 0..NW-1 scan the wave totals: the waves before this one and all
+  int64_t pre;
+  fold_totals<NW>(wtot, wave, carry, pre);
+  T o[kPer] = {0, 0, 0, 0};
+  queue_finish1<T, FUSED, FULL>(k, P, base, N, max_i64(pre, exc), key, ar, off, stm, o, hist, lut, q);
+  if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
+  store4t<T>(out, base, FULL ? base + kPer : N, o);
+}
+
 template <typename T, bool FUSED>
 __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   constexpr uint32_t NW = kDownThreads / 64;
@@ -729,43 +800,27 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
     des_bucket_lut_init(lut);
     __syncthreads();
   }
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t N = k.N;
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
   T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
-  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
-  bool bad = false;
+  QAcc q;
   int64_t carry = 0;  // max key of the chunks before (0: the idle start)
   uint32_t buf = 0;
-  for (uint64_t c0 = 0; c0 < N; c0 += (uint64_t)kPer * kDownThreads) {
-    const uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
-    uint64_t a[kPer];
-    T o[kPer] = {0, 0, 0, 0};
-    T ar[kPer];
-    load_arrivals<T>(k, par, off, base, N, a, ar);
-    const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
-    uint32_t mask;
-    const int64_t inc = wave_max_scan(queue_keys(a, base, N, P.hold, mask));
-    const int64_t exc = wave_shr1(inc);
-    if (lane == 63) wtot[buf][wave] = inc;
-    __syncthreads();
-    // lanes 0..NW-1 scan the wave totals: the waves before this one and all
-    int64_t pre;
-    fold_totals<NW>(wtot[buf], wave, carry, pre);
-    pre = max_i64(pre, exc);
+  constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
+  uint64_t c0 = 0;
+#pragma unroll 1
+  for (; c0 + CH <= N; c0 += CH) {
+    down1_chunk<T, FUSED, true>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q);
     buf ^= 1u;
-    const uint64_t x = base * P.hold + (uint64_t)pre;  // the worker's ready time before trace `base`
-    queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, lut, wsum, wmax, d0, d1, n5, bad);
-    if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
-    store4t<T>(out, base, N, o);
   }
-  flag_overflow(k, bad);
+  if (c0 < N) down1_chunk<T, FUSED, false>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q);
+  flag_overflow(k, q.bad);
   if (k.quiet) return;
-  des_flush_waits<kDownThreads>(k, P.row, wsum, wmax, N, N * P.hold, red);
+  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.wmax, N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
-    des_flush_durations<kDownThreads>(k, P, hist, d0, d1, n5, red);
+    des_flush_durations<kDownThreads>(k, P, hist, q.d0, q.d1, q.n5, red);
   }
 }
 
@@ -923,8 +978,8 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   T ar[kPer];
   load_arrivals<T>(k, par, off, base, N, a, ar);
   const uint32_t stm = FUSED && base < N ? des_status4(k, v, base) : 0u;
-  uint32_t mask;
-  const int64_t inc = wave_max_scan(queue_keys(a, base, N, P.hold, mask));
+  int64_t key[kPer];
+  const int64_t inc = wave_max_scan(queue_keys<false>(a, base, N, P.hold, key));
   const int64_t exc = wave_shr1(inc);
   if (lane == 63) wtot[wave] = inc;
   __syncthreads();
@@ -979,20 +1034,17 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   __syncthreads();
   int64_t cin = s_carry, pre;
   fold_totals<NW>(wtot, wave, cin, pre);
-  pre = max_i64(pre, exc);
-  const uint64_t x = base * P.hold + (uint64_t)pre;  // the worker's ready time before trace `base`
   T o[kPer] = {0, 0, 0, 0};
-  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
-  bool bad = false;
-  queue_finish<T, FUSED>(k, P, base, N, x, a, ar, off, mask, stm, o, hist, lut, wsum, wmax, d0, d1, n5, bad);
+  QAcc q;
+  queue_finish1<T, FUSED, false>(k, P, base, N, max_i64(pre, exc), key, ar, off, stm, o, hist, lut, q);
   if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
   store4t<T>(out, base, N, o);
-  flag_overflow(k, bad);
+  flag_overflow(k, q.bad);
   if (k.quiet) return;
-  des_flush_waits<kDesThreads>(k, P.row, wsum, wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
+  des_flush_waits<kDesThreads>(k, P.row, q.wsum, q.wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
   if constexpr (FUSED) {
     __syncthreads();
-    des_flush_durations<kDesThreads>(k, P, hist, d0, d1, n5, red);
+    des_flush_durations<kDesThreads>(k, P, hist, q.d0, q.d1, q.n5, red);
   }
 }
 
