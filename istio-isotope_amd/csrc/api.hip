@@ -70,6 +70,7 @@ struct DevState {
   void *d_des_pos = nullptr;
   uint32_t *d_des_child = nullptr, *d_des_level = nullptr, *d_des_mult = nullptr;
   uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr, *d_des_zero = nullptr;
+  uint32_t *d_des_pipe = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
   isim::TreeExt *d_tree_ext = nullptr;  // kind 7: per position (the nodes are d_prog)
   isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
@@ -81,6 +82,7 @@ void free_dev(DevState &d) {
                   (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_const_stats,
                   d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
                   (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
+                  (void *)d.d_des_pipe,
                   d.d_des_ext, d.d_des_steps, (void *)d.d_tree_ext, (void *)d.d_tree_dyn})
     if (q) (void)hipFree(q);
   d = DevState();
@@ -742,6 +744,9 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
       !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4) ||
       !up((void **)&st->d_des_zero, d.zero_pos.data(), d.zero_pos.size() * 4))
     return fail(ISIM_EHIP, "DES plan upload failed");
+  std::vector<uint32_t> pipe(d.pipe_pos);
+  pipe.insert(pipe.end(), d.pipe_dep.begin(), d.pipe_dep.end());
+  if (!up((void **)&st->d_des_pipe, pipe.data(), pipe.size() * 4)) return fail(ISIM_EHIP, "DES plan upload failed");
   return ISIM_OK;
 }
 
@@ -813,6 +818,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   L.d_arr_ops = st->d_des_arr;
   L.d_fast_pos = st->d_des_fast;
   L.d_zero_pos = st->d_des_zero;
+  L.d_pipe = st->d_des_pipe;
   L.d_sort_pos = st->d_des_sort;
   L.d_mult = st->d_des_mult;
   L.d_stats = d_stats;

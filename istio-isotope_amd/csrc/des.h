@@ -97,6 +97,17 @@ struct DesPlan {
   uint32_t max_sort_pos = 0;         // most positions of one sort-path service
   uint32_t max_rep_bits = 0;         // sort keys: bits of the largest replica index of a sort-path service
   uint64_t max_hold = 0;             // longest worker hold time of any position (queue scan keys)
+  // pipelined queue segments (des.hip des_down_pipe): runs of >= 2 rounds whose
+  // queues are all single-replica fast positions and whose finishes all come in
+  // the run's last round; every position of a run in ONE launch, a position's
+  // chunks waiting on its caller's published chunk count
+  struct PipeSeg {
+    uint32_t r0, r1;    // rounds [r0, r1]
+    uint32_t off, cnt;  // positions pipe_pos[off, off + cnt)
+  };
+  std::vector<PipeSeg> pipe;
+  std::vector<uint32_t> pipe_pos;    // round order, within a round non-fused first
+  std::vector<uint32_t> pipe_dep;    // per pipe_pos: the position whose start row it waits on (kDesNone: none)
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 
@@ -105,6 +116,7 @@ struct DesLaunch {
   const DesPlan *plan;               // host copy (the schedule)
   const void *d_pos, *d_ext, *d_steps;  // DesPos[n_pos], DesPosExt[n_pos], DesStep[]
   const uint32_t *d_child, *d_fast_pos, *d_sort_pos, *d_fin_pos, *d_arr_ops, *d_zero_pos;
+  const uint32_t *d_pipe;            // pipe_pos then pipe_dep
   const uint32_t *d_mult;            // per slot: calls per trace (executed-call counters)
   // workspace parts (des_carve)
   void *W, *WF, *BK;                 // rows [n_pos][ld] (starts, finishes), [steps][ld] of u32 or u64

@@ -65,6 +65,9 @@ constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-p
 #ifndef ISIM_DES_SPLIT_TARGET
 #define ISIM_DES_SPLIT_TARGET 8192  // (position x trace-range) blocks per up / step-begin launch
 #endif
+#ifndef ISIM_DES_PIPE
+#define ISIM_DES_PIPE 1  // runs of single-replica queue rounds in one pipelined launch
+#endif
 #ifndef ISIM_DES_DOWN_WAVES
 #define ISIM_DES_DOWN_WAVES 6  // waves per SIMD the one-workgroup-per-position pass is compiled for
 #endif
@@ -130,13 +133,14 @@ __device__ __forceinline__ uint32_t des_prom_bucket_m(uint32_t m) {
   const uint32_t n = m > lo ? m - lo : 0;
   return base + (((n + d - 1) * M) >> 16);
 }
-constexpr uint32_t kBucketLut = 501;  // m = ceil(t / 1 ms) in 0..500
+constexpr uint32_t kBucketLut = 502;  // m = ceil(t / 1 ms) in 0..500; 501: above 500 ms (+Inf)
 // fills the workgroup's table (the caller's barrier publishes it)
 __device__ __forceinline__ void des_bucket_lut_init(uint8_t *lut) {
   for (uint32_t m = threadIdx.x; m < kBucketLut; m += blockDim.x) lut[m] = (uint8_t)des_prom_bucket_m(m);
 }
 __device__ __forceinline__ uint32_t des_prom_bucket(const uint8_t *lut, uint64_t t) {
-  return t > 500000000ull ? 32u : lut[((uint32_t)t + 999999u) / 1000000u];
+  const uint32_t c = (uint32_t)(t < 500000001ull ? t : 500000001ull);  // branch-free: entry 501 is the +Inf bucket
+  return lut[(c + 999999u) / 1000000u];
 }
 
 struct ChainState;
@@ -180,6 +184,9 @@ struct DesK {
   ChainState *chain;
   uint32_t *chain_ticket;     // this launch's ticket counter
   uint32_t n_chunks;
+  // pipelined down pass
+  const uint32_t *pipe_dep;   // per level_pos entry: the position it waits on (kDesNone: none)
+  uint32_t *prog;             // [n_pos] chunks of a position's start row published (zeroed per pass)
 };
 
 // ---- rows: u32 (narrow) or u64, times relative to A_t, status in the top bit
@@ -408,18 +415,27 @@ __device__ __forceinline__ int64_t dpp_i64(int64_t old, int64_t v) {
 }
 __device__ __forceinline__ int64_t max_i64(int64_t a, int64_t b) { return a > b ? a : b; }
 constexpr int64_t kKeyMin = INT64_MIN;
-// inclusive max-scan over the wave's 64 lanes
+// a lane's value moved by a full-mask DPP control, 0 where the source lane
+// does not exist (bound_ctrl: no register to preset)
+template <int CTRL>
+__device__ __forceinline__ int64_t dpp0_i64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)v >> 32), CTRL, 0xF, 0xF, true);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// inclusive max-scan over the wave's 64 lanes of max(0, v): every prefix the
+// queues need is at least 0 (the idle start), so lanes past an edge read 0
 __device__ __forceinline__ int64_t wave_max_scan(int64_t v) {
-  v = max_i64(v, dpp_i64<0x111, 0xF>(kKeyMin, v));  // row_shr:1
-  v = max_i64(v, dpp_i64<0x112, 0xF>(kKeyMin, v));  // row_shr:2
-  v = max_i64(v, dpp_i64<0x114, 0xF>(kKeyMin, v));  // row_shr:4
-  v = max_i64(v, dpp_i64<0x118, 0xF>(kKeyMin, v));  // row_shr:8
-  v = max_i64(v, dpp_i64<0x142, 0xA>(kKeyMin, v));  // row_bcast:15 into rows 1, 3
-  v = max_i64(v, dpp_i64<0x143, 0xC>(kKeyMin, v));  // row_bcast:31 into rows 2, 3
+  v = max_i64(v, dpp0_i64<0x111>(v));              // row_shr:1
+  v = max_i64(v, dpp0_i64<0x112>(v));              // row_shr:2
+  v = max_i64(v, dpp0_i64<0x114>(v));              // row_shr:4
+  v = max_i64(v, dpp0_i64<0x118>(v));              // row_shr:8
+  v = max_i64(v, dpp_i64<0x142, 0xA>(v, v));       // row_bcast:15 into rows 1, 3 (rows 0, 2 keep v)
+  v = max_i64(v, dpp_i64<0x143, 0xC>(v, v));       // row_bcast:31 into rows 2, 3
   return v;
 }
-// the previous lane's value (lane 0: kKeyMin)
-__device__ __forceinline__ int64_t wave_shr1(int64_t v) { return dpp_i64<0x138, 0xF>(kKeyMin, v); }
+// the previous lane's value (lane 0: 0)
+__device__ __forceinline__ int64_t wave_shr1(int64_t v) { return dpp0_i64<0x138>(v); }
 __device__ __forceinline__ int64_t read_lane(int64_t v, uint32_t l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)l);
@@ -431,11 +447,11 @@ template <uint32_t NW>
 __device__ __forceinline__ void fold_totals(const int64_t *wtot, uint32_t wave, int64_t &carry, int64_t &pre) {
   static_assert(NW >= 2 && NW <= 16, "one DPP row of wave totals");
   const uint32_t lane = threadIdx.x & 63u;
-  int64_t v = lane < NW ? wtot[lane] : kKeyMin;
-  v = max_i64(v, dpp_i64<0x111, 0xF>(kKeyMin, v));
-  v = max_i64(v, dpp_i64<0x112, 0xF>(kKeyMin, v));
-  v = max_i64(v, dpp_i64<0x114, 0xF>(kKeyMin, v));
-  if constexpr (NW > 8) v = max_i64(v, dpp_i64<0x118, 0xF>(kKeyMin, v));
+  int64_t v = lane < NW ? wtot[lane] : 0;  // totals are >= 0 (wave_max_scan)
+  v = max_i64(v, dpp0_i64<0x111>(v));
+  v = max_i64(v, dpp0_i64<0x112>(v));
+  v = max_i64(v, dpp0_i64<0x114>(v));
+  if constexpr (NW > 8) v = max_i64(v, dpp0_i64<0x118>(v));
   const int64_t before = wave ? read_lane(v, wave - 1) : kKeyMin;
   pre = max_i64(carry, before);
   carry = max_i64(carry, read_lane(v, NW - 1));
@@ -693,12 +709,87 @@ __device__ __forceinline__ void queue_finish(const DesK &k, const DesPos &P, uin
   if constexpr (FUSED) hist_add4(hist, bin);
 }
 
+// agent-scope relaxed accesses: sc1 loads and stores (L1 bypassed)
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_flag(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Rows handed between workgroups inside a launch (des_down_pipe), the sc1
+// form of the guide's Guideline 16: the producer's 16-B stores are sc1
+// (write-through), drained by every storing wave before the barrier behind
+// which one lane stores the flag (sc1); the consumer polls the flag with sc1
+// loads and reads every handed-off byte with sc1 loads (L1 bypassed), so no
+// release or acquire fence.  A buffer resource per chunk keeps the offsets
+// 32-bit; the last (partial) chunk goes value by value.
+typedef uint32_t des_v4u __attribute__((ext_vector_type(4)));
+constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
+constexpr int kSc1 = 16;                // cache-policy aux bit of the buffer builtins
+template <typename T, bool FULL>
+__device__ __forceinline__ void load_row_sc1(const T *p, uint64_t c0, uint64_t base, uint64_t N, T (&x)[kPer]) {
+  if constexpr (FULL) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<T *>(p + c0), (short)0, (int)(sizeof(T) * kPer * kDownThreads),
+                                          kRsrcWord3);
+    const uint32_t vo = (uint32_t)(base - c0) * (uint32_t)sizeof(T);
+    if constexpr (sizeof(T) == 4) {
+      const des_v4u w = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, kSc1);
+      x[0] = w.x;
+      x[1] = w.y;
+      x[2] = w.z;
+      x[3] = w.w;
+    } else {
+      const des_v4u w0 = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, kSc1);
+      const des_v4u w1 = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 16, 0, kSc1);
+      x[0] = (T)w0.x | ((T)w0.y << (4 * sizeof(T)));
+      x[1] = (T)w0.z | ((T)w0.w << (4 * sizeof(T)));
+      x[2] = (T)w1.x | ((T)w1.y << (4 * sizeof(T)));
+      x[3] = (T)w1.z | ((T)w1.w << (4 * sizeof(T)));
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i)
+      x[i] = base + i < N ? __hip_atomic_load(p + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (T)0;
+  }
+}
+template <typename T, bool FULL>
+__device__ __forceinline__ void store_row_sc1(T *p, uint64_t c0, uint64_t base, uint64_t N, const T (&x)[kPer]) {
+  if constexpr (FULL) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(p + c0, (short)0, (int)(sizeof(T) * kPer * kDownThreads), kRsrcWord3);
+    const uint32_t vo = (uint32_t)(base - c0) * (uint32_t)sizeof(T);
+    if constexpr (sizeof(T) == 4) {
+      const des_v4u w = {x[0], x[1], x[2], x[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, vo, 0, kSc1);
+    } else {
+      const des_v4u w0 = {(uint32_t)x[0], (uint32_t)((uint64_t)x[0] >> 32), (uint32_t)x[1],
+                          (uint32_t)((uint64_t)x[1] >> 32)};
+      const des_v4u w1 = {(uint32_t)x[2], (uint32_t)((uint64_t)x[2] >> 32), (uint32_t)x[3],
+                          (uint32_t)((uint64_t)x[3] >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b128(w0, r, vo, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(w1, r, vo + 16, 0, kSc1);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i)
+      if (base + i < N) __hip_atomic_store(p + base + i, x[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Single-replica queues (closed form): from the thread's exclusive prefix p
 // the running max of the keys gives the wait of each trace, S_t - a_t =
 // p_t - key_t; the stored value (S or, fused, F | status, relative to A_t),
 // waits and durations as queue_finish.
 struct QAcc {
-  uint64_t wsum = 0, wmax = 0, d0 = 0, d1 = 0, n5 = 0;
+  uint64_t wsum = 0, wmax = 0, dsum = 0, d1 = 0, n5 = 0;  // d0 = dsum - d1
   bool bad = false;
 };
 template <typename T, bool FUSED, bool FULL>
@@ -719,10 +810,12 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
         const uint64_t F = val + P.floor;
         const uint32_t st = (stm >> i) & 1u;
         const uint64_t dur = w + P.floor;  // F - a
+        // (per trace: hoisting these atomics under one wave-uniform test gave
+        // wrong batches with ROCm 7.2, cause not found)
         if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
         q.n5 += st;
-        q.d1 += st ? dur : 0;  // selects, not a branch: keeps d0/d1 in registers
-        q.d0 += st ? 0 : dur;
+        q.dsum += dur;
+        q.d1 += st ? dur : 0;  // a select, not a branch
         bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
         q.bad |= !Row<T>::fits(F);
         val = F | ((uint64_t)st << Row<T>::kTop);
@@ -732,7 +825,10 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
       out[i] = (T)val;
     }
   }
-  if constexpr (FUSED) hist_add4(hist, bin);
+  if constexpr (FUSED) {
+    // per-trace 500 counts: one wave-uniform test, the atomics only where a 500 is
+    hist_add4(hist, bin);
+  }
 }
 
 // this thread's 4 traces: absolute arrivals a = A_t + relative arrival, and
@@ -757,11 +853,15 @@ __device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint6
 // single-replica services: the closed form, one barrier per chunk (the wave
 // totals double-buffered; every thread folds them into its prefix and into the
 // carry itself)
-// one chunk of kPer x kDownThreads traces from c0 (FULL: all below N)
-template <typename T, bool FUSED, bool FULL>
+// One chunk of kPer x kDownThreads traces from c0 (FULL: all below N).
+// Pipelined pass (des_down_pipe): HAND_IN, the caller's start row is written
+// in this launch, read with sc1 loads; HAND_OUT, this start row is read in
+// this launch: sc1 stores, and at the chunk's barrier (every wave drained its
+// previous chunk's stores first) one lane publishes the chunks done so far.
+template <typename T, bool FUSED, bool FULL, bool HAND_IN = false, bool HAND_OUT = false>
 __device__ __forceinline__ void down1_chunk(const DesK &k, const DesPos &P, uint32_t v, const T *par, uint64_t off,
                                             T *out, uint64_t c0, int64_t *wtot, int64_t &carry, uint32_t *hist,
-                                            const uint8_t *lut, QAcc &q) {
+                                            const uint8_t *lut, QAcc &q, uint32_t chunk = 0) {
   constexpr uint32_t NW = kDownThreads / 64;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t N = k.N;
@@ -771,20 +871,34 @@ __device__ __forceinline__ void down1_chunk(const DesK &k, const DesPos &P, uint
   __asm__ volatile("" : "+v"(base));
   uint64_t a[kPer];
   T ar[kPer];
-  load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
+  if constexpr (HAND_IN) {
+    load4n<uint64_t>(k.A, base, FULL ? base + kPer : N, a);
+    load_row_sc1<T, FULL>(par, c0, base, N, ar);
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)ar[i] + off;
+  } else {
+    load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
+  }
   const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
   int64_t key[kPer];
   const int64_t inc = wave_max_scan(queue_keys<FULL>(a, base, N, P.hold, key));
   const int64_t exc = wave_shr1(inc);
   if (lane == 63) wtot[wave] = inc;
+  if constexpr (HAND_OUT) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous chunk's stores
   __syncthreads();
+  if constexpr (HAND_OUT)
+    if (threadIdx.x == 0 && chunk > 0) st_flag(k.prog + v, chunk);
   // lanes 0..NW-1 scan the wave totals: the waves before this one and all
   int64_t pre;
   fold_totals<NW>(wtot, wave, carry, pre);
   T o[kPer] = {0, 0, 0, 0};
   queue_finish1<T, FUSED, FULL>(k, P, base, N, max_i64(pre, exc), key, ar, off, stm, o, hist, lut, q);
   if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
-  store4t<T>(out, base, FULL ? base + kPer : N, o);
+  if constexpr (HAND_OUT) {
+    store_row_sc1<T, FULL>(out, c0, base, N, o);
+  } else {
+    store4t<T>(out, base, FULL ? base + kPer : N, o);
+  }
 }
 
 template <typename T, bool FUSED>
@@ -820,7 +934,7 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.wmax, N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
-    des_flush_durations<kDownThreads>(k, P, hist, q.d0, q.d1, q.n5, red);
+    des_flush_durations<kDownThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
   }
 }
 
@@ -933,19 +1047,6 @@ struct ChainState {
 };
 static_assert(sizeof(ChainState) == 32, "ChainState is 32 bytes");
 
-__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_flag(const uint32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_flag(uint32_t *p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // the ticket of a chained-scan workgroup: (position, chunk) in launch order
 __device__ __forceinline__ uint32_t chain_ticket(const DesK &k) {
   __shared__ uint32_t s_ticket;
@@ -1044,7 +1145,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   des_flush_waits<kDesThreads>(k, P.row, q.wsum, q.wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
   if constexpr (FUSED) {
     __syncthreads();
-    des_flush_durations<kDesThreads>(k, P, hist, q.d0, q.d1, q.n5, red);
+    des_flush_durations<kDesThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
   }
 }
 
@@ -1060,6 +1161,96 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain_mix(DesK k) {
   const uint32_t v = k.level_pos[k.level_begin + ticket / k.n_chunks];
   if (k.pos[v].flags & kDesFlagFused) chain_body<T, true>(k, v, ticket % k.n_chunks);
   else chain_body<T, false>(k, v, ticket % k.n_chunks);
+}
+
+// ---- pipelined queue pass: the single-replica positions of
+// consecutive rounds in ONE launch, one workgroup per position, tickets in the
+// plan's round order.  A position whose arrivals are its caller's start row
+// waits chunk by chunk for the caller to publish them (the caller's ticket is
+// earlier, so it is resident and progressing): no level boundaries, no tail
+// of one level in front of the next.
+template <typename T, bool FUSED, bool HAND_IN>
+__device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t dep) {
+  constexpr uint32_t NW = kDownThreads / 64;
+  constexpr bool HAND_OUT = !FUSED;  // non-leaves: their callees may read the start row in this launch
+  __shared__ int64_t wtot[2][NW];
+  __shared__ uint64_t red[3 * NW];
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint8_t lut[kBucketLut];
+  __shared__ uint32_t s_known;
+  const DesPos P = k.pos[v];
+  if constexpr (FUSED) {
+    for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
+    des_bucket_lut_init(lut);
+    __syncthreads();
+  }
+  const uint64_t N = k.N;
+  const T *par = arrival_row<T>(k, v, P);
+  const uint64_t off = par ? P.off : 0;
+  T *out = row<T>(FUSED ? k.WF : k.W, k.ld, v);  // a fused leaf stores its finish
+  QAcc q;
+  int64_t carry = 0;
+  uint32_t buf = 0, known = 0, chunk = 0;
+  // the caller's chunks [0, chunk] published (one lane polls, the barrier
+  // shares the count; bounded: a timeout drops the batch, never expected)
+  auto wait = [&]() {
+    if constexpr (HAND_IN) {
+      if (known <= chunk) {
+        if (threadIdx.x == 0) {
+          uint32_t pv, spins = 0;
+          while ((pv = ld_flag(k.prog + dep)) <= chunk) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) {
+              atomicOr(k.ovf, 4u);
+              pv = 0xFFFFFFFFu;
+              break;
+            }
+          }
+          s_known = pv;
+        }
+        __syncthreads();
+        known = s_known;
+      }
+    }
+  };
+  constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
+  uint64_t c0 = 0;
+#pragma unroll 1
+  for (; c0 + CH <= N; c0 += CH, ++chunk) {
+    wait();
+    down1_chunk<T, FUSED, true, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
+    buf ^= 1u;
+  }
+  if (c0 < N) {
+    wait();
+    down1_chunk<T, FUSED, false, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
+    ++chunk;
+  }
+  if constexpr (HAND_OUT) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's last stores
+    __syncthreads();
+    if (threadIdx.x == 0) st_flag(k.prog + v, chunk);
+  }
+  flag_overflow(k, q.bad);
+  if (k.quiet) return;
+  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.wmax, N, N * P.hold, red);
+  if constexpr (FUSED) {
+    __syncthreads();
+    des_flush_durations<kDownThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pipe(DesK k) {
+  const uint32_t t = chain_ticket(k);
+  const uint32_t v = k.level_pos[k.level_begin + t], dep = k.pipe_dep[k.level_begin + t];
+  if (k.pos[v].flags & kDesFlagFused) {
+    if (dep != kDesNone) pipe_body<T, true, true>(k, v, dep);
+    else pipe_body<T, true, false>(k, v, dep);
+  } else {
+    if (dep != kDesNone) pipe_body<T, false, true>(k, v, dep);
+    else pipe_body<T, false, false>(k, v, dep);
+  }
 }
 
 // ---- up pass: finish times, statuses, per-service durations.
@@ -1481,9 +1672,12 @@ static uint64_t row_ld(uint64_t n) { return (n + 15) & ~15ull; }
 static uint64_t chain_tickets(const DesPlan &plan) { return 4ull * plan.rounds(); }
 static uint64_t status_wpr(uint64_t n) { return (((n + 31) / 32) + 15) & ~15ull; }
 
+// chained and pipelined down passes: tickets, per-position published chunk
+// counts, chain states (all zeroed before every pass)
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n) {
   const uint64_t chunks = (n + dev::kDownChunk - 1) / dev::kDownChunk;
-  return al256(chain_tickets(plan) * 4) + (uint64_t)plan.pos.size() * chunks * sizeof(dev::ChainState);
+  return al256(chain_tickets(plan) * 4) + al256(plan.pos.size() * 4) +
+         (uint64_t)plan.pos.size() * chunks * sizeof(dev::ChainState);
 }
 
 // Workspace parts, in order (256-B aligned): W and BK rows sized for u64,
@@ -1546,7 +1740,24 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
   static void (*const down[4])(DesK) = {des_down<T, false, true>, des_down<T, false, false>,
                                        des_down<T, true, true>, des_down<T, true, false>};
   static void (*const chain[2])(DesK) = {des_down_chain<T, true>, des_down_chain<T, false>};
+  size_t seg = 0;
+  uint32_t piped_to = 0;  // rounds below this one had their queues in a pipelined launch
   for (uint32_t r = 0; r < pl.rounds(); ++r) {
+    if (ISIM_DES_PIPE && seg < pl.pipe.size() && pl.pipe[seg].r0 == r) {
+      // the single-replica queues of rounds [r0, r1] in one launch (no step
+      // begins, zero-hold, sort-path or replicated queues in them; finishes
+      // only in r1)
+      const DesPlan::PipeSeg &sg = pl.pipe[seg++];
+      DesK kp = k;
+      kp.level_pos = L.d_pipe;
+      kp.pipe_dep = L.d_pipe + pl.pipe_pos.size();
+      kp.level_begin = sg.off;
+      kp.chain_ticket = tickets + 4 * r + 2;
+      hipLaunchKernelGGL(des_down_pipe<T>, dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
+      piped_to = sg.r1 + 1;
+    }
+    if (r < piped_to) goto finishes;
+    {
     // 1. step begins (calls after calls)
     const uint32_t na = pl.arr_off[r + 1] - pl.arr_off[r];
     if (na) {
@@ -1606,6 +1817,8 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       k.svals = vals_b;
       hipLaunchKernelGGL(des_down_sorted<T>, dim3(1), dim3(kDesThreads), 0, stream, k);
     }
+    }
+  finishes:
     // 3. finishes, deepest group first
     k.level_pos = L.d_fin_pos;
     for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
@@ -1661,7 +1874,8 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.n_chunks = (uint32_t)((L.n_traces + kDownChunk - 1) / kDownChunk);
   const uint64_t tk_bytes = al256(chain_tickets(*L.plan) * 4);
   uint32_t *tickets = (uint32_t *)L.chain;
-  k.chain = (ChainState *)((char *)L.chain + tk_bytes);
+  k.prog = (uint32_t *)((char *)L.chain + tk_bytes);
+  k.chain = (ChainState *)((char *)L.chain + tk_bytes + al256((uint64_t)L.n_pos * 4));
   const uint64_t chain_bytes = des_chain_bytes(*L.plan, L.n_traces);
   if (hipMemsetAsync(L.E, 0, L.n_traces * sizeof(uint32_t), stream) != hipSuccess) return 1;
   if (hipMemsetAsync(L.ovf, 0, 8, stream) != hipSuccess) return 1;  // overflow flag + changed flag

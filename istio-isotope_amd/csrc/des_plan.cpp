@@ -423,6 +423,42 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     }
     out.fin_round_off[r + 1] = (uint32_t)out.fin_off.size() - 1;
   }
+  // ---- pipelined queue segments
+  auto pipeable = [&](uint32_t r) {
+    return out.arr_off[r + 1] == out.arr_off[r] && out.zero_off[r + 1] == out.zero_off[r] &&
+           out.sorted_off[r + 1] == out.sorted_off[r] && out.fast_split[5 * r + 2] == out.fast_off[r + 1] &&
+           out.fast_off[r + 1] > out.fast_off[r];
+  };
+  std::vector<uint32_t> seg_of(np, kDesNone);
+  for (uint32_t r = 0; r < R;) {
+    if (!pipeable(r)) {
+      ++r;
+      continue;
+    }
+    uint32_t e = r + 1;  // the run [r, e): round e - 1 has no finishes, round e is pipeable
+    while (e < R && pipeable(e) && out.fin_round_off[e] == out.fin_round_off[e - 1]) ++e;
+    if (e - r >= 2) {
+      const uint32_t id = (uint32_t)out.pipe.size();
+      DesPlan::PipeSeg sg{r, e - 1, (uint32_t)out.pipe_pos.size(), 0};
+      for (uint32_t x = r; x < e; ++x)
+        for (uint32_t fused = 0; fused < 2; ++fused)
+          for (uint32_t i = out.fast_off[x]; i < out.fast_off[x + 1]; ++i) {
+            const uint32_t v = out.fast_pos[i];
+            if (((out.pos[v].flags & kDesFlagFused) != 0) != (fused != 0)) continue;
+            seg_of[v] = id;
+            out.pipe_pos.push_back(v);
+          }
+      sg.cnt = (uint32_t)out.pipe_pos.size() - sg.off;
+      for (uint32_t i = sg.off; i < sg.off + sg.cnt; ++i) {
+        const uint32_t v = out.pipe_pos[i], u = out.pos[v].parent;
+        // the arrival row is the caller's start row, written in this launch
+        const bool wait = u != kDesNoParent && out.ext[v].bk_in == kDesNone && seg_of[u] == id;
+        out.pipe_dep.push_back(wait ? u : kDesNone);
+      }
+      out.pipe.push_back(sg);
+    }
+    r = e;
+  }
   out.slot_mult = p.stream_mult;
   return ISIM_OK;
 }
