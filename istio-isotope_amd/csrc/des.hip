@@ -124,7 +124,7 @@ __device__ __forceinline__ uint64_t des_exp_q24(uint32_t u) {
 // base + ceil((m - run start) / step).  The kernels look m up in a 501-byte
 // LDS table built from this formula (des_bucket_lut: 7 VALU per duration
 // instead of 57).
-__device__ __forceinline__ uint32_t des_prom_bucket_m(uint32_t m) {
+__host__ __device__ constexpr uint32_t des_prom_bucket_m(uint32_t m) {
   const uint32_t lo = m <= 12 ? 7 : m <= 20 ? 12 : m <= 50 ? 20 : m <= 100 ? 50 : m <= 200 ? 100 : 200;
   const uint32_t base = m <= 12 ? 0 : m <= 20 ? 5 : m <= 50 ? 9 : m <= 100 ? 15 : m <= 200 ? 20 : 25;
   const uint32_t d = m <= 12 ? 1 : m <= 20 ? 2 : m <= 50 ? 5 : m <= 100 ? 10 : m <= 200 ? 20 : 50;
@@ -134,9 +134,20 @@ __device__ __forceinline__ uint32_t des_prom_bucket_m(uint32_t m) {
   return base + (((n + d - 1) * M) >> 16);
 }
 constexpr uint32_t kBucketLut = 502;  // m = ceil(t / 1 ms) in 0..500; 501: above 500 ms (+Inf)
-// fills the workgroup's table (the caller's barrier publishes it)
+constexpr uint32_t kBucketLutWords = 128;
+struct DesBucketLut {
+  uint32_t w[kBucketLutWords];  // byte m of the table: the bucket of m (m <= 501), little-endian
+  constexpr DesBucketLut() : w() {
+    for (uint32_t m = 0; m < 4 * kBucketLutWords; ++m)
+      w[m / 4] |= (m < kBucketLut ? des_prom_bucket_m(m) : 32u) << (8 * (m % 4));
+  }
+};
+__device__ constexpr DesBucketLut kDesBucketLut{};
+// copies the table into the workgroup's LDS (the caller's barrier publishes
+// it): one 4-byte word per thread instead of computing 502 entries
 __device__ __forceinline__ void des_bucket_lut_init(uint8_t *lut) {
-  for (uint32_t m = threadIdx.x; m < kBucketLut; m += blockDim.x) lut[m] = (uint8_t)des_prom_bucket_m(m);
+  for (uint32_t i = threadIdx.x; i < kBucketLutWords; i += blockDim.x)
+    reinterpret_cast<uint32_t *>(lut)[i] = kDesBucketLut.w[i];
 }
 __device__ __forceinline__ uint32_t des_prom_bucket(const uint8_t *lut, uint64_t t) {
   const uint32_t c = (uint32_t)(t < 500000001ull ? t : 500000001ull);  // branch-free: entry 501 is the +Inf bucket
@@ -907,7 +918,7 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   __shared__ int64_t wtot[2][NW];
   __shared__ uint64_t red[3 * NW];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   const DesPos P = k.pos[v];
   if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
@@ -946,7 +957,7 @@ __device__ __forceinline__ void downr_body(const DesK &k, uint32_t v) {
   __shared__ uint64_t red[3 * kDownThreads / 64];
   __shared__ MaxPlus xs[kDownThreads];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   const DesPos P = k.pos[v];
   const uint32_t reps = MULTI ? P.reps : 1u;
   if (threadIdx.x < reps) carry[threadIdx.x] = 0;
@@ -1061,7 +1072,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   __shared__ int64_t wtot[NW];
   __shared__ uint64_t red[3 * kDesThreads / 64];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   __shared__ int64_t s_carry;
   if constexpr (FUSED) {
     for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesThreads) hist[i] = 0;
@@ -1176,7 +1187,7 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   __shared__ int64_t wtot[2][NW];
   __shared__ uint64_t red[3 * NW];
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   __shared__ uint32_t s_known;
   const DesPos P = k.pos[v];
   if constexpr (FUSED) {
@@ -1259,7 +1270,7 @@ template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hist[i] = 0;
   des_bucket_lut_init(lut);
   __syncthreads();
@@ -1370,7 +1381,7 @@ template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
   __shared__ uint64_t red[5 * kDesUpThreads / 64];
-  __shared__ uint8_t lut[kBucketLut];
+  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hp[i] = 0;
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads) hl[i] = 0;
   des_bucket_lut_init(lut);
