@@ -1264,6 +1264,95 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pi
   }
 }
 
+// one thread's 4 consecutive traces of the up pass (FULL: all below te, so
+// every row access is one vector load and the loads issue back to back)
+template <typename T, bool FULL>
+__device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t v, uint64_t b0, uint64_t te,
+                                        const T *mine, T *fin, const T *par, uint64_t off, bool leaf, const T *base_t,
+                                        uint32_t c_max_from, uint32_t *hist, const uint8_t *lut, uint64_t &dsum0,
+                                        uint64_t &dsum1, uint64_t &n500, bool &bad) {
+  __asm__ volatile("" : "+v"(b0));  // opaque to loop strength reduction (down1_chunk)
+  const uint64_t n = FULL ? b0 + kPer : te;
+  uint64_t S[kPer], a[kPer], m[kPer];
+  uint32_t sto = 0;  // children's 500s, bit i
+  load4n<T>(mine, b0, n, S);
+  if (par) {
+    load4n<T>(par, b0, n, a);
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) a[i] += off;
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) a[i] = 0;
+  }
+  if (base_t) load4n<T>(base_t, b0, n, m);
+  else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) m[i] = S[i];
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) m[i] += P.floor;
+  if (!leaf) {
+    // children's finishes: several rows in flight per step (each child row is a
+    // full memory latency; one at a time left the hubs latency-bound)
+    T cm[kPer] = {0, 0, 0, 0};
+    auto take = [&](const T (&f)[kPer], bool in_max) {
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) {
+        const T tc = f[i] & (T)Row<T>::kMask;
+        if (in_max) cm[i] = tc > cm[i] ? tc : cm[i];
+        sto |= (uint32_t)(f[i] >> Row<T>::kTop) << i;
+      }
+    };
+    const uint32_t *ch = k.child + P.child_off;
+    const uint32_t cnt = P.child_cnt;
+    constexpr uint32_t CB = sizeof(T) == 4 ? 4 : 2;  // rows in flight (VGPR budget of 8 waves/SIMD)
+    uint32_t c = 0;
+    for (; c + CB <= cnt; c += CB) {
+      T f[CB][kPer];
+#pragma unroll
+      for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, n, f[j]);
+#pragma unroll
+      for (uint32_t j = 0; j < CB; ++j) take(f[j], c + j >= c_max_from);
+    }
+    for (; c < cnt; ++c) {
+      T f[kPer];
+      load4t<T>(row<T>(k.WF, k.ld, ch[c]), b0, n, f);
+      take(f, c >= c_max_from);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) m[i] = (uint64_t)cm[i] > m[i] ? (uint64_t)cm[i] : m[i];
+  }
+  uint64_t o[kPer];
+  const uint32_t stm = des_status4(k, v, b0);
+  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint64_t t = b0 + i;
+    o[i] = 0;
+    if (FULL || t < te) {
+      const uint64_t F = leaf ? m[i] : m[i] + P.post;
+      const uint32_t own = (stm >> i) & 1u;
+      const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
+      const uint64_t dur = F - a[i];
+      bad |= !Row<T>::fits(F);
+      o[i] = F | ((uint64_t)st << Row<T>::kTop);
+      if (st && !k.quiet) atomicAdd(k.E + t, 1u);
+      n500 += st;
+      dsum1 += st ? dur : 0;
+      dsum0 += st ? 0 : dur;
+      bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
+    }
+  }
+  hist_add4(hist, bin);
+  if (k.changed) {
+    T ot[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) ot[i] = (T)o[i];
+    track4<T>(k, fin, b0, n, ot);
+  }
+  store4n<T>(fin, b0, n, o);
+}
+
 // ---- up pass: finish times, statuses, per-service durations.
 // (position, trace-range) blocks; 4 consecutive traces per thread.
 template <typename T>
@@ -1292,84 +1381,11 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
   bool bad = false;
   for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
-    uint64_t S[kPer], a[kPer], m[kPer];
-    uint32_t sto = 0;  // children's 500s, bit i
-    load4n<T>(mine, b0, te, S);
-    if (par) {
-      load4n<T>(par, b0, te, a);
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) a[i] += off;
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) a[i] = 0;
-    }
-    if (base_t) load4n<T>(base_t, b0, te, m);
-    else {
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) m[i] = S[i];
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) m[i] += P.floor;
-    if (!leaf) {
-      // children's finishes: several rows in flight per step (each child row is a
-      // full memory latency; one at a time left the hubs latency-bound)
-      T cm[kPer] = {0, 0, 0, 0};
-      auto take = [&](const T (&f)[kPer], bool in_max) {
-#pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i) {
-          const T tc = f[i] & (T)Row<T>::kMask;
-          if (in_max) cm[i] = tc > cm[i] ? tc : cm[i];
-          sto |= (uint32_t)(f[i] >> Row<T>::kTop) << i;
-        }
-      };
-      const uint32_t *ch = k.child + P.child_off;
-      const uint32_t cnt = P.child_cnt;
-      constexpr uint32_t CB = sizeof(T) == 4 ? 4 : 2;  // rows in flight (VGPR budget of 8 waves/SIMD)
-      uint32_t c = 0;
-      for (; c + CB <= cnt; c += CB) {
-        T f[CB][kPer];
-#pragma unroll
-        for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, te, f[j]);
-#pragma unroll
-        for (uint32_t j = 0; j < CB; ++j) take(f[j], c + j >= c_max_from);
-      }
-      for (; c < cnt; ++c) {
-        T f[kPer];
-        load4t<T>(row<T>(k.WF, k.ld, ch[c]), b0, te, f);
-        take(f, c >= c_max_from);
-      }
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) m[i] = (uint64_t)cm[i] > m[i] ? (uint64_t)cm[i] : m[i];
-    }
-    uint64_t o[kPer];
-    const uint32_t stm = des_status4(k, v, b0);
-    uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      const uint64_t t = b0 + i;
-      o[i] = 0;
-      if (t < te) {
-        const uint64_t F = leaf ? m[i] : m[i] + P.post;
-        const uint32_t own = (stm >> i) & 1u;
-        const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
-        const uint64_t dur = F - a[i];
-        bad |= !Row<T>::fits(F);
-        o[i] = F | ((uint64_t)st << Row<T>::kTop);
-        if (st && !k.quiet) atomicAdd(k.E + t, 1u);
-        n500 += st;
-        dsum1 += st ? dur : 0;
-        dsum0 += st ? 0 : dur;
-        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
-      }
-    }
-    hist_add4(hist, bin);
-    if (k.changed) {
-      T ot[kPer];
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) ot[i] = (T)o[i];
-      track4<T>(k, fin, b0, te, ot);
-    }
-    store4n<T>(fin, b0, te, o);
+    if (b0 + kPer <= te)
+      up_quad<T, true>(k, P, v, b0, te, mine, fin, par, off, leaf, base_t, c_max_from, hist, lut, dsum0, dsum1, n500, bad);
+    else
+      up_quad<T, false>(k, P, v, b0, te, mine, fin, par, off, leaf, base_t, c_max_from, hist, lut, dsum0, dsum1, n500,
+                        bad);
   }
   flag_overflow(k, bad);
   if (k.quiet) return;
