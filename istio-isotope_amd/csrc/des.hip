@@ -1264,36 +1264,49 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pi
   }
 }
 
-// one thread's 4 consecutive traces of the up pass (FULL: all below te, so
-// every row access is one vector load and the loads issue back to back)
+// One thread's 4 consecutive traces of the up pass (FULL: all below te, so
+// every row access is one vector load).  Every load of the quad is issued
+// before any arithmetic (start, arrival and step-begin rows, the status word,
+// the first kUpCB children's finish rows: one memory round trip, not five);
+// children past kUpCB (hubs) follow in batches.  `ch`: the child positions,
+// staged in LDS by the workgroup when they fit.
+#ifndef ISIM_DES_UP_CB
+#define ISIM_DES_UP_CB 3
+#endif
+#ifndef ISIM_DES_UP_WAVES
+#define ISIM_DES_UP_WAVES 6  // waves per SIMD the up pass is compiled for (80 VGPRs: no spills)
+#endif
+template <typename T>
+constexpr uint32_t kUpCB = sizeof(T) == 4 ? ISIM_DES_UP_CB : 2;  // children rows in flight with the rest
+constexpr uint32_t kUpChildLds = 1024;  // child ids staged in LDS per workgroup
 template <typename T, bool FULL>
 __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t v, uint64_t b0, uint64_t te,
-                                        const T *mine, T *fin, const T *par, uint64_t off, bool leaf, const T *base_t,
-                                        uint32_t c_max_from, uint32_t *hist, const uint8_t *lut, uint64_t &dsum0,
-                                        uint64_t &dsum1, uint64_t &n500, bool &bad) {
+                                        T *fin, const T *arow, uint64_t amask, uint64_t off, bool leaf,
+                                        const T *mrow, uint32_t c_max_from, const uint32_t *ch,
+                                        const uint32_t (&id0)[kUpCB<T>], uint32_t *hist, const uint8_t *lut,
+                                        uint64_t &dsum0, uint64_t &dsum1, uint64_t &n500, bool &bad) {
   __asm__ volatile("" : "+v"(b0));  // opaque to loop strength reduction (down1_chunk)
   const uint64_t n = FULL ? b0 + kPer : te;
-  uint64_t S[kPer], a[kPer], m[kPer];
+  const uint32_t cnt = leaf ? 0u : P.child_cnt;
+  T ar[kPer], mr[kPer];
+  T f0[kUpCB<T>][kPer];
+  // 1. the loads (no branch around the row loads: a branch that merges
+  // loaded values makes the compiler wait for them inside it)
+  load4t<T>(arow, b0, n, ar);
+  load4t<T>(mrow, b0, n, mr);
+  const uint32_t stm = des_status4(k, v, b0);
+#pragma unroll
+  for (uint32_t j = 0; j < kUpCB<T>; ++j)
+    if (j < cnt) load4t<T>(row<T>(k.WF, k.ld, id0[j]), b0, n, f0[j]);
+  // 2. the arithmetic
+  uint64_t a[kPer], m[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    a[i] = ((uint64_t)ar[i] + off) & amask;
+    m[i] = (uint64_t)mr[i] + P.floor;
+  }
   uint32_t sto = 0;  // children's 500s, bit i
-  load4n<T>(mine, b0, n, S);
-  if (par) {
-    load4n<T>(par, b0, n, a);
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] += off;
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] = 0;
-  }
-  if (base_t) load4n<T>(base_t, b0, n, m);
-  else {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) m[i] = S[i];
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) m[i] += P.floor;
-  if (!leaf) {
-    // children's finishes: several rows in flight per step (each child row is a
-    // full memory latency; one at a time left the hubs latency-bound)
+  if (cnt) {
     T cm[kPer] = {0, 0, 0, 0};
     auto take = [&](const T (&f)[kPer], bool in_max) {
 #pragma unroll
@@ -1303,27 +1316,22 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
         sto |= (uint32_t)(f[i] >> Row<T>::kTop) << i;
       }
     };
-    const uint32_t *ch = k.child + P.child_off;
-    const uint32_t cnt = P.child_cnt;
-    constexpr uint32_t CB = sizeof(T) == 4 ? 4 : 2;  // rows in flight (VGPR budget of 8 waves/SIMD)
-    uint32_t c = 0;
-    for (; c + CB <= cnt; c += CB) {
-      T f[CB][kPer];
 #pragma unroll
-      for (uint32_t j = 0; j < CB; ++j) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, n, f[j]);
+    for (uint32_t j = 0; j < kUpCB<T>; ++j)
+      if (j < cnt) take(f0[j], j >= c_max_from);
+    for (uint32_t c = kUpCB<T>; c < cnt; c += kUpCB<T>) {
+      T f[kUpCB<T>][kPer];
 #pragma unroll
-      for (uint32_t j = 0; j < CB; ++j) take(f[j], c + j >= c_max_from);
-    }
-    for (; c < cnt; ++c) {
-      T f[kPer];
-      load4t<T>(row<T>(k.WF, k.ld, ch[c]), b0, n, f);
-      take(f, c >= c_max_from);
+      for (uint32_t j = 0; j < kUpCB<T>; ++j)
+        if (c + j < cnt) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, n, f[j]);
+#pragma unroll
+      for (uint32_t j = 0; j < kUpCB<T>; ++j)
+        if (c + j < cnt) take(f[j], c + j >= c_max_from);
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) m[i] = (uint64_t)cm[i] > m[i] ? (uint64_t)cm[i] : m[i];
   }
   uint64_t o[kPer];
-  const uint32_t stm = des_status4(k, v, b0);
   uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
@@ -1356,7 +1364,7 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
 // ---- up pass: finish times, statuses, per-service durations.
 // (position, trace-range) blocks; 4 consecutive traces per thread.
 template <typename T>
-__global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
+__global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
   __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
@@ -1380,12 +1388,37 @@ __global__ void __launch_bounds__(kDesUpThreads, 8) des_up(DesK k) {
   const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
   bool bad = false;
-  for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
-    if (b0 + kPer <= te)
-      up_quad<T, true>(k, P, v, b0, te, mine, fin, par, off, leaf, base_t, c_max_from, hist, lut, dsum0, dsum1, n500, bad);
-    else
-      up_quad<T, false>(k, P, v, b0, te, mine, fin, par, off, leaf, base_t, c_max_from, hist, lut, dsum0, dsum1, n500,
-                        bad);
+  // rows read unconditionally: the arrival row (the entry: any row, masked
+  // to 0) and the row F's floor starts from (the last step's begin, or S)
+  const T *arow = par ? par : mine;
+  const uint64_t amask = par ? ~0ull : 0ull;
+  const T *mrow = base_t ? base_t : mine;
+  // the child positions: in LDS when they fit (read by every quad; LDS
+  // addressing known to the compiler, not flat), else from global memory
+  __shared__ uint32_t s_ch[kUpChildLds];
+  const uint32_t cnt = leaf ? 0u : P.child_cnt;
+  const uint32_t *gch = k.child + P.child_off;
+  auto run = [&](const uint32_t *ch) {
+    // the first children's positions in (uniform) registers for the whole
+    // range: their row loads issue with the others, no id load in front
+    uint32_t id0[kUpCB<T>];
+#pragma unroll
+    for (uint32_t j = 0; j < kUpCB<T>; ++j) id0[j] = j < cnt ? ch[j] : 0u;
+    for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
+      if (b0 + kPer <= te)
+        up_quad<T, true>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut, dsum0,
+                         dsum1, n500, bad);
+      else
+        up_quad<T, false>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut,
+                          dsum0, dsum1, n500, bad);
+    }
+  };
+  if (cnt <= kUpChildLds) {
+    for (uint32_t i = threadIdx.x; i < cnt; i += kDesUpThreads) s_ch[i] = gch[i];
+    __syncthreads();
+    run(s_ch);
+  } else {
+    run(gch);
   }
   flag_overflow(k, bad);
   if (k.quiet) return;
