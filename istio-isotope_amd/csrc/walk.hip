@@ -438,6 +438,17 @@ __device__ __forceinline__ Node4 load_group(CNode4 *p) {
   return r;
 }
 
+// m = 2 m + (this lane in mask): one v_addc_co_u32 with the lane mask as carry-in
+__device__ __forceinline__ void shift_in(uint32_t &m, uint64_t mask) {
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %0, %0, %2" : "+v"(m), "=s"(co) : "s"(mask));
+}
+// v += (this lane in mask)
+__device__ __forceinline__ void add_lane(uint32_t &v, uint64_t mask) {
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, 0, %0, %2" : "+v"(v), "=s"(co) : "s"(mask));
+}
+
 template <bool LDSC>
 __device__ __forceinline__ void count_t(uint64_t *__restrict__ gstats, uint32_t *cnt, uint32_t idx, uint32_t v,
                                         bool lane0) {
@@ -612,7 +623,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
       uint32_t n = 0;
 #pragma unroll
       for (int u = 0; u < TPL; ++u) {
-        errh[u] += lane_in(own[u]) ? 1u : 0u;
+        add_lane(errh[u], own[u]);
         any |= own[u];
         n += popc(own[u]);
       }
@@ -628,7 +639,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
         uint32_t n = 0;
 #pragma unroll
         for (int u = 0; u < TPL; ++u) {
-          errh[u] += lane_in(own[u]) ? 1u : 0u;
+          add_lane(errh[u], own[u]);
           any |= own[u];
           n += popc(own[u]);
         }
@@ -664,13 +675,13 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
 #pragma unroll
           for (int u = 0; u < TPL; ++u) {
             root_st[u] = st[u];
-            errh[u] += lane_in(st[u]) ? 1u : 0u;
+            add_lane(errh[u], st[u]);
           }
         } else if (any) {
           uint32_t n = 0;
 #pragma unroll
           for (int u = 0; u < TPL; ++u) {
-            errh[u] += lane_in(st[u]) ? 1u : 0u;
+            add_lane(errh[u], st[u]);
             n += popc(st[u]);
             bs_set(u, p - 1, st[u]);  // mode B: a 500 fails the caller
             bs_clear(u, p);
@@ -689,7 +700,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
         uint32_t n = 0;
 #pragma unroll
         for (int u = 0; u < TPL; ++u) {
-          errh[u] += lane_in(own[u]) ? 1u : 0u;
+          add_lane(errh[u], own[u]);
           any |= own[u];
           n += popc(own[u]);
           top[u] |= own[u];
@@ -714,7 +725,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
 #pragma unroll
         for (int u = 0; u < TPL; ++u) {
           st[u] = top[u];
-          errh[u] += lane_in(st[u]) ? 1u : 0u;
+          add_lane(errh[u], st[u]);
           any |= st[u];
           n += popc(st[u]);
         }
@@ -763,7 +774,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
             uint32_t n = 0;
 #pragma unroll
             for (int u = 0; u < TPL; ++u) {
-              errh[u] += lane_in(own[u]) ? 1u : 0u;
+              add_lane(errh[u], own[u]);
               n += popc(own[u]);
             }
             count_t<LDSC>(c.gstats, c.cnt, c.n_slots + (q.n[j].meta & 0xFFFFFFu), n, lane0);
@@ -798,7 +809,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
         for (int u = 0; u < TPL; ++u) {
           const uint64_t own =
               (bufA.n[0].meta & 0x80000000u) ? all[u] : (ballot(xw[u] < bufA.n[0].thr) & all[u]);
-          errh[u] += lane_in(own) ? 1u : 0u;
+          add_lane(errh[u], own);
           root_st[u] = own;
         }
       } else {
@@ -818,17 +829,6 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
   }
 #pragma unroll
   for (int u = 0; u < TPL; ++u) finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st[u], errh[u]);
-}
-
-// m = 2 m + (this lane in mask): one v_addc_co_u32 with the lane mask as carry-in
-__device__ __forceinline__ void shift_in(uint32_t &m, uint64_t mask) {
-  uint64_t co;
-  asm("v_addc_co_u32 %0, %1, %0, %0, %2" : "+v"(m), "=s"(co) : "s"(mask));
-}
-// v += (this lane in mask)
-__device__ __forceinline__ void add_lane(uint32_t &v, uint64_t mask) {
-  uint64_t co;
-  asm("v_addc_co_u32 %0, %1, 0, %0, %2" : "+v"(v), "=s"(co) : "s"(mask));
 }
 
 typedef const __attribute__((address_space(4))) StreamClose CClose;
