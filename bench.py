@@ -418,7 +418,11 @@ def main():
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
     if args.config == "c5":
         if args.batch == 1 << 22:
-            args.batch = 1 << 16  # the DES keeps 8 B per invocation per trace (5.2 GB at 2^16 x 10k)
+            # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
+            # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
+            # the pipelined queue pass's fill and drain (2^16 20.8,
+            # 2^18 22.3, 2^20 23.9 M traces/s)
+            args.batch = 1 << 20
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
     if args.config == "c1" and args.batch == 1 << 22:
         args.batch = 1_000_000  # BASELINE config 1: 1M traces
