@@ -35,6 +35,9 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "des.h"
+#ifndef ISIM_NT_ROWS
+#define ISIM_NT_ROWS 1  // row stores of fused leaves and finishes nontemporal: keep L2 for the A_t re-reads
+#endif
 #include "kernel_abi.h"
 
 namespace isim {
@@ -256,7 +259,12 @@ template <typename T>
 __device__ __forceinline__ void store4t(T *p, uint64_t base, uint64_t n, const T (&x)[kPer]) {
   if (base + kPer <= n) {
     if constexpr (sizeof(T) == 4) {
+#if ISIM_NT_ROWS
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(v4u{x[0], x[1], x[2], x[3]}, reinterpret_cast<v4u *>(p + base));
+#else
       *reinterpret_cast<uint4 *>(p + base) = make_uint4(x[0], x[1], x[2], x[3]);
+#endif
     } else {
       reinterpret_cast<ulonglong2 *>(p + base)[0] = make_ulonglong2(x[0], x[1]);
       reinterpret_cast<ulonglong2 *>(p + base)[1] = make_ulonglong2(x[2], x[3]);
