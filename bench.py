@@ -57,7 +57,9 @@ def parse():
                     help="dynamic walks: skip the per-service duration histograms")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-traces", type=int, default=0, help="cpu_baseline sample size (0 = auto)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    args.des_auto_batch = False  # c5 with the default batch: shrink it to the device's free HBM
+    return args
 
 
 def build_graph(config: str):
@@ -147,6 +149,19 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     d = isim.DesHandler(h, args.mean_interarrival_ns)
     B = args.batch
     wsb = d.workspace_bytes(B)
+    if args.des_auto_batch:
+        # the default batch on a device with less free HBM than the 288 GB of
+        # an MI355X: the largest halving whose workspace takes <= 80 % of it
+        free = torch.cuda.mem_get_info(dev)[0]
+        while B > 4096 and wsb > 0.8 * free:
+            B //= 2
+            wsb = d.workspace_bytes(B)
+        if world > 1:  # one batch length on every rank (shard_begin)
+            t = torch.tensor([B], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            B = int(t.item())
+        wsb = d.workspace_bytes(B)
+        args.batch = B
     ws = torch.empty(wsb // 8 + 1, dtype=torch.int64, device=dev)
     stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
     table = torch.zeros(max(1, d.table_words), dtype=torch.int64, device=dev)
@@ -423,6 +438,7 @@ def main():
             # the pipelined queue pass's fill and drain (2^16 20.8,
             # 2^18 22.3, 2^20 23.9 M traces/s)
             args.batch = 1 << 20
+            args.des_auto_batch = True
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
     if args.config == "c1" and args.batch == 1 << 22:
         args.batch = 1_000_000  # BASELINE config 1: 1M traces
