@@ -556,6 +556,12 @@ __device__ __forceinline__ void hist_add4(uint32_t *hist, const uint32_t (&bin)[
   if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(any)) atomicAdd(&hist[b0], n);
 }
 
+// m = 2 m + (this lane in mask): one v_addc_co_u32 with the mask as carry-in
+__device__ __forceinline__ void des_shift_in(uint32_t &m, uint64_t mask) {
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %0, %0, %2" : "+v"(m), "=s"(co) : "s"(mask));
+}
+
 // own error statuses of traces [base, base+4) of position v (base % 4 == 0),
 // bit i; the status pass zeroes bits past N
 __device__ __forceinline__ uint32_t des_status4(const DesK &k, uint32_t v, uint64_t base) {
@@ -586,7 +592,60 @@ __global__ void __launch_bounds__(256) des_status(DesK k) {
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) bits[j] |= (uint32_t)(always[j] || (thr[j] && c[j] < thr[j])) << b;
   };
-  if (any && w * 32 + 32 <= k.N) {
+  // whole waves of one group and one trace-id high word (the usual case):
+  // counter words 1-3 are wave-uniform, so rounds 1-2 fold into scalar math
+  // (as walk.hip philox_lockstep), and each trace's bit is shifted in from
+  // the compare's lane mask (one v_addc_co_u32)
+  const uint64_t t0 = k.trace_begin + w * 32;
+  const uint32_t gu = __builtin_amdgcn_readfirstlane((uint32_t)g);
+  const uint32_t hiu = __builtin_amdgcn_readfirstlane((uint32_t)(t0 >> 32));
+  const bool lane_ok = any && w * 32 + 32 <= k.N && (uint32_t)g == gu && (uint32_t)(t0 >> 32) == hiu &&
+                       (uint32_t)((t0 + 31) >> 32) == hiu;
+  if (__ballot(!lane_ok) == 0) {
+    uint32_t lim[4], en[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {  // wave-uniform: bit = en && c <= lim
+      const uint32_t a = __builtin_amdgcn_readfirstlane(always[j]), t = __builtin_amdgcn_readfirstlane(thr[j]);
+      en[j] = a | (t != 0u);
+      lim[j] = a ? 0xFFFFFFFFu : t - 1u;
+    }
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    const uint64_t q1 = (uint64_t)M1 * gu;                           // scalar
+    const uint32_t u0 = (uint32_t)(q1 >> 32) ^ hiu ^ k.k0;           // uniform
+    const uint64_t q0 = (uint64_t)M0 * u0;                           // scalar (round 2)
+    uint32_t uk0 = (uint32_t)q1 ^ (k.k0 + W0), uk1 = (uint32_t)(q0 >> 32) ^ (k.k1 + W1);
+    asm volatile("" : "+s"(uk0), "+s"(uk1));
+    uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+    for (int b = 15; b >= 0; --b) {  // traces b and b + 16, shifted in from the top bit down
+      uint32_t c[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t tl = (uint32_t)t0 + (uint32_t)b + 16u * u;
+        const uint64_t p0 = (uint64_t)M0 * tl;
+        const uint64_t p1 = (uint64_t)M1 * ((uint32_t)(p0 >> 32) ^ k.k1);
+        c[u][0] = (uint32_t)(p1 >> 32) ^ uk0;
+        c[u][1] = (uint32_t)p1;
+        c[u][2] = (uint32_t)p0 ^ uk1;
+        c[u][3] = (uint32_t)q0;
+      }
+      uint32_t k0 = k.k0 + 2u * W0, k1 = k.k1 + 2u * W1;
+#pragma unroll
+      for (int r = 2; r < 10; ++r) {
+        asm volatile("" : "+s"(k0), "+s"(k1));
+        des_round(c[0], k0, k1);
+        des_round(c[1], k0, k1);
+        k0 += W0;
+        k1 += W1;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        des_shift_in(lo[j], en[j] ? __ballot(c[0][j] <= lim[j]) : 0ull);
+        des_shift_in(hi[j], en[j] ? __ballot(c[1][j] <= lim[j]) : 0ull);
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) bits[j] = lo[j] | (hi[j] << 16);
+  } else if (any && w * 32 + 32 <= k.N) {
     // two independent Philox chains per step (ILP)
     for (uint32_t b = 0; b < 16; ++b) {
       const uint64_t t0 = k.trace_begin + w * 32 + b, t1 = t0 + 16;
