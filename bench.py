@@ -478,7 +478,9 @@ def main():
             traffic = None
 
     line = {
-        "metric": "simulated request traces/sec (node), 10k-svc topology" if args.config == "c3"
+        # BASELINE.json's metric verbatim (the roofline fraction is the "roofline" object)
+        "metric": "simulated request traces/sec (node) + % HBM roofline, 10k-svc topology, 1/2/4/8 GPU"
+        if args.config == "c3"
         else f"simulated request traces/sec (node), config {args.config}",
         "value": value,
         "unit": "traces/s",
