@@ -152,6 +152,10 @@ __device__ __forceinline__ void des_bucket_lut_init(uint8_t *lut) {
   for (uint32_t i = threadIdx.x; i < kBucketLutWords; i += blockDim.x)
     reinterpret_cast<uint32_t *>(lut)[i] = kDesBucketLut.w[i];
 }
+__device__ __forceinline__ uint32_t des_prom_bucket32(const uint8_t *lut, uint32_t t) {
+  const uint32_t c = t < 500000001u ? t : 500000001u;  // v_min_u32
+  return lut[(c + 999999u) / 1000000u];
+}
 __device__ __forceinline__ uint32_t des_prom_bucket(const uint8_t *lut, uint64_t t) {
   const uint32_t c = (uint32_t)(t < 500000001ull ? t : 500000001ull);  // branch-free: entry 501 is the +Inf bucket
   return lut[(c + 999999u) / 1000000u];
@@ -868,7 +872,9 @@ __device__ __forceinline__ void store_row_sc1(T *p, uint64_t c0, uint64_t base, 
 // waits and durations as queue_finish.
 struct QAcc {
   uint64_t wsum = 0, wmax = 0, dsum = 0, d1 = 0, n5 = 0;  // d0 = dsum - d1
+  uint32_t wmax32 = 0;  // 32-bit rows: the largest wait (< 2^31 unless `bad`), folded into wmax by max_wait()
   bool bad = false;
+  __device__ uint64_t max_wait() const { return wmax > wmax32 ? wmax : wmax32; }
 };
 template <typename T, bool FUSED, bool FULL>
 __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, uint64_t base, uint64_t N, int64_t p,
@@ -880,6 +886,33 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
   for (uint32_t i = 0; i < kPer; ++i) {
     if (FULL || base + i < N) {
       p = max_i64(p, key[i]);
+      if constexpr (sizeof(T) == 4) {
+        // 32-bit rows: a stored value below 2^31 needs a wait below 2^31, so
+        // the wait, the duration and their maxima are 32-bit (a larger wait
+        // marks the batch bad: it is rerun with 64-bit rows)
+        const uint64_t w64 = (uint64_t)(p - key[i]);
+        const uint32_t w = (uint32_t)w64;
+        q.bad |= w64 >= Row<T>::kSt;
+        q.wsum += w;
+        q.wmax32 = w > q.wmax32 ? w : q.wmax32;
+        uint64_t val = (uint64_t)w + (uint64_t)r[i] + off;  // S - A_t (off is 0 for the entry: r = 0)
+        if constexpr (FUSED) {
+          const uint64_t F = val + P.floor;
+          const uint32_t st = (stm >> i) & 1u;
+          const uint32_t dur = w + (uint32_t)P.floor;  // F - a; exact whenever F fits
+          if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
+          q.n5 += st;
+          q.dsum += dur;
+          q.d1 += st ? dur : 0u;
+          bin[i] = st * ISIM_N_PROM + des_prom_bucket32(lut, dur);
+          q.bad |= !Row<T>::fits(F);
+          val = F | ((uint64_t)st << Row<T>::kTop);
+        } else {
+          q.bad |= !Row<T>::fits(val);
+        }
+        out[i] = (T)val;
+        continue;
+      }
       const uint64_t w = (uint64_t)(p - key[i]);
       q.wsum += w;
       q.wmax = w > q.wmax ? w : q.wmax;
@@ -1009,7 +1042,7 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   if (c0 < N) down1_chunk<T, FUSED, false>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q);
   flag_overflow(k, q.bad);
   if (k.quiet) return;
-  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.wmax, N, N * P.hold, red);
+  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.max_wait(), N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
     des_flush_durations<kDownThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
@@ -1220,7 +1253,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   store4t<T>(out, base, N, o);
   flag_overflow(k, q.bad);
   if (k.quiet) return;
-  des_flush_waits<kDesThreads>(k, P.row, q.wsum, q.wmax, chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
+  des_flush_waits<kDesThreads>(k, P.row, q.wsum, q.max_wait(), chunk == 0 ? N : 0, chunk == 0 ? N * P.hold : 0, red);
   if constexpr (FUSED) {
     __syncthreads();
     des_flush_durations<kDesThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
@@ -1311,7 +1344,7 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   }
   flag_overflow(k, q.bad);
   if (k.quiet) return;
-  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.wmax, N, N * P.hold, red);
+  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.max_wait(), N, N * P.hold, red);
   if constexpr (FUSED) {
     __syncthreads();
     des_flush_durations<kDownThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
