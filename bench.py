@@ -110,7 +110,7 @@ def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
     dt = time.perf_counter() - t0
     return {"value": n_traces / dt, "unit": "traces/s", "cores": threads, "kind": "port",
             "sample": f"{n_traces} traces of the same workload (trace ids from {trace_begin}), "
-                      f"C oracle oracle/isim_oracle.c with OpenMP, {dt:.1f} s",
+                      f"C oracle oracle/isim_oracle.c with OpenMP, {dt:.3g} s",
             "hop_visits_per_s": float(st[2]) / dt}
 
 
@@ -514,10 +514,42 @@ def main():
         # 1M-trace workload; other configs on a bounded sample
         n_cpu = args.cpu_traces or (B if args.config == "c1" else 0)
         line["cpu_baseline"] = cpu_baseline(json_text, params, n_cpu, 0)
+    if args.config == "c1":
+        line["error_path"] = c1_error_path(args, json_text, params, rank, world, dev, multi)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def c1_error_path(args, json_text, params, rank, world, dev, multi=None):
+    """SURVEY §8(d) config 1's error-path variant: canonical.yaml with
+    errorRate 1 % on every service (the defaults block), same SimParams and
+    trace range, on the GPU and — rank 0, one GPU — the whole workload on the
+    CPU oracle."""
+    import numpy as np
+    import torch
+
+    import isim
+    doc = json.loads(json_text)
+    doc.setdefault("defaults", {})
+    doc["defaults"] = dict(doc["defaults"] or {}, errorRate="1%")
+    j = json.dumps(doc)
+    h = isim.Handler(isim.ServiceGraph.from_json(j), None, params)
+    B = args.batch
+    stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
+    recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
+    elapsed, kern_ms = time_walk(h, args.steps, args.warmup, B, recs, stats, rank, world, dev, multi)
+    f = h.fold(stats.cpu().numpy().view(np.uint64))
+    total = args.steps * B * world
+    assert f["n_traces"] == total
+    out = {"errorRate": "1% (defaults)", "value": total / elapsed, "unit": "traces/s",
+           "ms_per_step": elapsed * 1e3 / args.steps, "kernel_ms": kern_ms, "n_500_frac": f["n_500"] / total,
+           "err_hops_per_trace": f["sum_err_hops"] / total,
+           "kernel_kind": h.launch_info(torch.cuda.current_device())["kernel_kind"]}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(j, params, args.cpu_traces or B, 0)
+    return out
 
 
 if __name__ == "__main__":
