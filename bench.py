@@ -271,7 +271,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        teardown(multi)
 
 
 def compute_roofline(stream: bool, info, B: int, kern_ms: float):
@@ -310,6 +310,21 @@ def make_multi(rank, world, local):
     except Exception as e:  # reported in the JSON line: the torch RCCL merge is used instead
         print(f"isim_multi_init_rank failed ({e}); merging with torch.distributed", file=sys.stderr)
         return None, f"torch.distributed all_reduce (isim_multi_init_rank failed: {e})"
+
+
+def teardown(multi):
+    """Every rank frees libisim's communicator at the same point (after a
+    barrier, while the process group still lives), then the process group:
+    the communicator is never finalised at interpreter exit, in whatever order
+    the ranks reach it."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    dist.barrier()
+    if multi is not None:
+        multi.close()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def merge(h, multi, stats, sptr):
@@ -519,7 +534,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        teardown(multi)
 
 
 def c1_error_path(args, json_text, params, rank, world, dev, multi=None):
