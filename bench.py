@@ -431,14 +431,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ISIM_BENCH_BACKEND=gloo: a rehearsal of the N-rank flow on fewer GPUs
+    # than ranks (ranks share devices; no RCCL, stats merged by gloo)
+    backend = os.environ.get("ISIM_BENCH_BACKEND", "nccl")
     if world > 1:
+        local = local % torch.cuda.device_count() if backend != "nccl" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    multi, merge_label = make_multi(rank, world, local)
+    if backend == "nccl":
+        multi, merge_label = make_multi(rank, world, local)
+    else:
+        multi, merge_label = None, f"torch.distributed all_reduce ({backend} rehearsal)"
     json_text, desc = build_graph(args.config)
     # every trace is walked unless --fill: a draw-free static walk (config 2)
     # is otherwise walked once and filled, which is not a walk rate
