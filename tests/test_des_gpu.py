@@ -114,6 +114,23 @@ def test_config5_bench_scale(gpu):
     assert int(rows[:, isim.native.DES_SUM_WAIT].sum()) > 0  # the queues are contended
 
 
+def test_config5_bench_batch_prefix(gpu):
+    """The bench's own batch (2^20 traces per step, bench.py --config c5):
+    on the config-5 graph every service has one position fed by one caller,
+    so arrivals stay in trace order and a trace never waits for a later one —
+    the first 20,000 records of the 2^20 batch equal the 20,000-trace batch
+    that test_config5_bench_scale pins to the event-driven oracle."""
+    c = DesCase(config3_topology(), 6_000_000)
+    full, stats, table = c.d.serve(1000, 1 << 20)
+    pre, _, _ = c.d.serve(1000, 20_000)
+    rows = c.d.fold(table)
+    assert np.array_equal(full[:20_000], pre)
+    f = c.h.fold(stats)
+    assert f["n_traces"] == 1 << 20 and f["sum_hops"] == (1 << 20) * 10_000
+    assert int(full["latency_ns"].astype(np.uint64).sum()) == f["sum_latency"]
+    assert int(rows[:, isim.native.DES_SUM_WAIT].sum()) > 0
+
+
 @pytest.mark.parametrize("wide", [False, True])
 def test_device_entry_accumulates(gpu, wide):
     import torch
