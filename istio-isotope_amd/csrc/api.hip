@@ -53,6 +53,7 @@ struct DevState {
   uint32_t *d_close_end = nullptr;        // and its per-chunk ends
   uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
   unsigned long long *d_work = nullptr;  // kWorkSlots sets of batch queues, zero between launches
+  uint32_t *d_stage = nullptr;  // draw stream: kWorkSlots rows of n_slots u32 500 counts, zero between launches
   // draw-free static walks (no error draw anywhere): every trace walks alike
   bool draw_free = false;
   uint64_t *d_const_stats = nullptr;     // the stats of one trace (computed on first use)
@@ -79,7 +80,7 @@ struct DevState {
 
 void free_dev(DevState &d) {
   for (void *q : {(void *)d.d_prog, (void *)d.d_mult, (void *)d.d_closes, (void *)d.d_close_end,
-                  (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_const_stats,
+                  (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_stage, (void *)d.d_const_stats,
                   d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
                   (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
                   (void *)d.d_des_pipe,
@@ -325,6 +326,11 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (is_stream(st.kind)) {
     st.max_mult = 1;
     for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
+    if (st.lds_counters && p.n_slots > 0 && p.n_slots <= isim::kStageMaxSlots) {
+      const size_t bytes = (size_t)isim::kWorkSlots * p.n_slots * sizeof(uint32_t);
+      HIPCHK(hipMalloc(&st.d_stage, bytes));
+      HIPCHK(hipMemset(st.d_stage, 0, bytes));
+    }
   }
   return ISIM_OK;
 }
@@ -543,7 +549,10 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const uint64_t waves = st->threads / 64;
   const uint64_t want = (batches + waves - 1) / waves;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(want, st->max_blocks);
-  kp.work = st->d_work + isim::kWorkWords * (__atomic_fetch_add(&st->work_next, 1u, __ATOMIC_RELAXED) % isim::kWorkSlots);
+  const uint32_t slot = __atomic_fetch_add(&st->work_next, 1u, __ATOMIC_RELAXED) % isim::kWorkSlots;
+  kp.work = st->d_work + isim::kWorkWords * slot;
+  // u32 staging of the 500 counts: the launch split (launch_walk) keeps n x max_mult below 2^32
+  kp.stage = st->d_stage ? st->d_stage + (size_t)slot * h->prog.n_slots : nullptr;
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
@@ -551,7 +560,8 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   if (is_stream(st->kind) && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;
-    void *args2[] = {&mult, &n_slots, &n_traces, &d_stats};
+    uint32_t *stage = kp.stage;
+    void *args2[] = {&mult, &n_slots, &n_traces, &d_stats, &stage};
     HIPCHK(hipLaunchKernel(isim::stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args2, 0,
                            (hipStream_t)hip_stream));
   }

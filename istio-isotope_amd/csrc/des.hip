@@ -2091,7 +2091,8 @@ int des_launch(const DesLaunch &L, void *stream_) {
     uint64_t n = L.n_traces;
     const uint32_t *mult = L.d_mult;
     uint64_t *st = k.stats;
-    void *args[] = {&mult, &n_slots, &n, &st};
+    uint32_t *stage = nullptr;  // the DES counts its 500s itself (no staged walk flush)
+    void *args[] = {&mult, &n_slots, &n, &st, &stage};
     if (hipLaunchKernel(stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args, 0, stream) !=
         hipSuccess)
       return 1;

@@ -126,6 +126,7 @@ struct KParams {
   uint32_t svc_dur;         // dynamic walks: 1 = record per-service durations
   uint32_t root_dur;        // the entry's duration-table word (row | leaf bucket << 24)
   unsigned long long *work; // batch queues (kWorkWords): zero at launch, zeroed again by the last wave
+  uint32_t *stage;          // draw stream: u32 per-site 500 counts of this launch (null: u64 atomics into stats)
   const StreamClose *closes;     // kind 6: close list (+kClosePad zero records of tail padding)
   const uint32_t *close_slot;    // kind 6: per close, the call-site slot of the closing invocation
   const uint32_t *close_end;     // kind 6: per chunk, closes up to and including it
@@ -144,6 +145,11 @@ constexpr uint32_t kWorkQueues = 8;
 constexpr uint32_t kWorkLine = 16;                    // u64 words per 128-B line
 constexpr uint32_t kWorkWords = (kWorkQueues + 1) * kWorkLine;
 constexpr uint32_t kWorkSlots = 256;
+// Draw-stream launches flush their per-site 500 counts as u32 atomics into a
+// staging row of the launch's work slot (launch_walk's split keeps a launch's
+// count at a site below 2^32); isim_stream_calls adds the row to the u64
+// stats and zeroes it.  Graphs with more slots keep the u64 atomics.
+constexpr uint32_t kStageMaxSlots = 1u << 16;
 
 constexpr uint32_t kWgThreads = 1024;                 // max workgroup size (launch bound)
 constexpr uint32_t kLdsAccBytes = 64;                 // WgAcc

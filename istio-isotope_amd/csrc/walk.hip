@@ -1022,9 +1022,17 @@ __global__ void __launch_bounds__(256) isim_fill_const(isim_trace_rec *__restric
 }
 
 __global__ void isim_stream_calls(const uint32_t *__restrict__ mult, uint32_t n_slots, uint64_t n_traces,
-                                  uint64_t *__restrict__ gstats) {
+                                  uint64_t *__restrict__ gstats, uint32_t *__restrict__ stage) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_slots) gstats[ISIM_ST_SITES + i] += (uint64_t)mult[i] * n_traces;
+  if (i >= n_slots) return;
+  gstats[ISIM_ST_SITES + i] += (uint64_t)mult[i] * n_traces;
+  if (stage) {  // the launch's staged 500 counts (u32) into the stats; the row is zero again after
+    const uint32_t v = stage[i];
+    if (v) {
+      gstats[ISIM_ST_SITES + n_slots + i] += v;
+      stage[i] = 0;
+    }
+  }
 }
 
 // KIND: 0 static/u32 time, 1 static/u64, 2 dynamic/u32, 3 dynamic/u64, 4 draw stream,
@@ -1119,8 +1127,13 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
   if constexpr (LDSC) {
-    for (uint32_t i = threadIdx.x; i < 2u * kp.n_slots; i += blockDim.x)
-      if (c.cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)c.cnt[i]);
+    if (kp.stage) {  // draw stream: only the 500 counts are counted here (calls: isim_stream_calls)
+      for (uint32_t i = threadIdx.x; i < kp.n_slots; i += blockDim.x)
+        if (c.cnt[kp.n_slots + i]) atomicAdd(kp.stage + i, c.cnt[kp.n_slots + i]);
+    } else {
+      for (uint32_t i = threadIdx.x; i < 2u * kp.n_slots; i += blockDim.x)
+        if (c.cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)c.cnt[i]);
+    }
   }
   if (threadIdx.x == 0 && c.acc->ntr) {
     atomicAdd(st + ISIM_ST_N_TRACES, c.acc->ntr);
