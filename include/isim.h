@@ -227,7 +227,9 @@ ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32
  * first; ~min word starts at 0).  No host synchronisation, no allocation:
  * graph-capturable after the first call on a device.
  * Concurrency limit: the walk kernels claim batches from per-launch queue
- * sets that rotate over 256 sets per (handler, device); at most 256 launches
+ * sets (and draw-stream kernels stage their per-site 500 counts in per-launch
+ * u32 rows, folded into d_stats by the launch's last kernel) that rotate
+ * over 256 sets per (handler, device); at most 256 launches
  * of one handler may be in flight on one device at once (launches on ONE
  * stream are ordered and never collide; with more than 256 streams in
  * flight, order them with events or use one handler per stream). */
