@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 N_CU = 256
 CLOCK_HZ = 2.4e9
+DEFAULT_BATCH = 1 << 24
 
 
 def parse():
@@ -41,7 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 22, help="traces per rank per step")
+    # 2^24 traces (256 MB of records) per launch: the per-launch flush and
+    # tail amortise (config 3: 2^22 335, 2^23 339, 2^24 340 M traces/s)
+    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="traces per rank per step")
     ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
                     "fill the records (the library default) instead of walking every trace")
@@ -457,7 +460,7 @@ def main():
                             (0 if args.fill else isim.native.FLAG_WALK_ALL))
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
     if args.config == "c5":
-        if args.batch == 1 << 22:
+        if args.batch == DEFAULT_BATCH:
             # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
             # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
             # the pipelined queue pass's fill and drain (2^16 20.8,
@@ -465,7 +468,7 @@ def main():
             args.batch = 1 << 20
             args.des_auto_batch = True
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
-    if args.config == "c1" and args.batch == 1 << 22:
+    if args.config == "c1" and args.batch == DEFAULT_BATCH:
         args.batch = 1_000_000  # BASELINE config 1: 1M traces
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
