@@ -468,6 +468,11 @@ def main():
             args.batch = 1 << 20
             args.des_auto_batch = True
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
+    if args.config == "c4" and args.batch == DEFAULT_BATCH:
+        # the lane tree walk's per-launch cost (the tree copied to every
+        # workgroup's LDS, the flush, the tail) amortises further: 2^24 / 2^25
+        # / 2^26 traces per launch 5.82 / 6.06 / 6.23 G traces/s (1 GB of records)
+        args.batch = 1 << 26
     if args.config == "c1" and args.batch == DEFAULT_BATCH:
         args.batch = 1_000_000  # BASELINE config 1: 1M traces
     info = h.info
