@@ -541,15 +541,6 @@ __device__ __forceinline__ void philox_lockstep(const uint32_t (&t_lo)[TPL], uin
   }
 }
 
-#ifndef ISIM_LOCKSTEP
-#define ISIM_LOCKSTEP 1
-#endif
-#ifndef ISIM_EARLY_WAIT
-#define ISIM_EARLY_WAIT 0
-#endif
-#ifndef ISIM_FAST_A
-#define ISIM_FAST_A 1
-#endif
 
 
 // TPL traces per lane: the wave walks 64*TPL traces through one pass over the
@@ -744,7 +735,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
   };
   auto draws = [&](const Node4 &q, uint32_t g, uint32_t (&x)[TPL][4]) {
     if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0) {
-      if (ISIM_LOCKSTEP && hi_uniform) {
+      if (hi_uniform) {
         philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
       } else {
 #pragma unroll
@@ -757,7 +748,7 @@ __device__ __forceinline__ void walk_stream(const Ctx &c, CNode4 *__restrict__ s
 #pragma unroll
     for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
     draws(q, g, x);
-    if constexpr (!MODEB && ISIM_FAST_A) {
+    if constexpr (!MODEB) {
       // mode A, no errorRate-1 record in the group: per record one compare
       // per trace; counts only on the (rarer) records where some lane errs
       if (((q.n[0].meta | q.n[1].meta | q.n[2].meta | q.n[3].meta) & 0x80000000u) == 0) {
@@ -904,7 +895,7 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
 #pragma unroll
       for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
       if ((cur.n[0].thr | cur.n[1].thr | cur.n[2].thr | cur.n[3].thr) != 0) {
-        if (ISIM_LOCKSTEP && hi_uniform) {
+        if (hi_uniform) {
           philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
         } else {
 #pragma unroll
