@@ -546,8 +546,11 @@ __global__ void __launch_bounds__(kDesThreads) des_add_blocks(DesK k) {
 // equal to its first lane's first bin with ballots and adds them with one LDS
 // atomic; the rest go one atomic each.  Call with the wave converged.
 constexpr uint32_t kNoBin = 0xFFFFFFFFu;
+// FULL: every bin is set (whole quads of traces below N)
+template <bool FULL = false>
 __device__ __forceinline__ void hist_add4(uint32_t *hist, const uint32_t (&bin)[4]) {
-  const uint32_t first = bin[0] != kNoBin ? bin[0] : bin[1] != kNoBin ? bin[1] : bin[2] != kNoBin ? bin[2] : bin[3];
+  const uint32_t first =
+      FULL ? bin[0] : bin[0] != kNoBin ? bin[0] : bin[1] != kNoBin ? bin[1] : bin[2] != kNoBin ? bin[2] : bin[3];
   const uint64_t any = __ballot(first != kNoBin);
   if (!any) return;
   const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)first, (int)__builtin_ctzll(any));
@@ -555,7 +558,7 @@ __device__ __forceinline__ void hist_add4(uint32_t *hist, const uint32_t (&bin)[
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
     n += (uint32_t)__builtin_popcountll(__ballot(bin[i] == b0));
-    if (bin[i] != kNoBin && bin[i] != b0) atomicAdd(&hist[bin[i]], 1u);
+    if ((FULL || bin[i] != kNoBin) && bin[i] != b0) atomicAdd(&hist[bin[i]], 1u);
   }
   if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(any)) atomicAdd(&hist[b0], n);
 }
@@ -938,7 +941,7 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
   }
   if constexpr (FUSED) {
     // per-trace 500 counts: one wave-uniform test, the atomics only where a 500 is
-    hist_add4(hist, bin);
+    hist_add4<FULL>(hist, bin);
   }
 }
 
@@ -1451,7 +1454,7 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
       bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
     }
   }
-  hist_add4(hist, bin);
+  hist_add4<FULL>(hist, bin);
   if (k.changed) {
     T ot[kPer];
 #pragma unroll
