@@ -35,6 +35,22 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 N_CU = 256
 CLOCK_HZ = 2.4e9
 DEFAULT_BATCH = 1 << 24
+# traces per rank per step of each config when --batch is left at its default
+# (the parity suite checks these exact batches: tests/test_fullsize_gpu.py)
+BENCH_BATCH = {
+    "c1": 1_000_000,  # BASELINE config 1: 1M traces
+    "c2": DEFAULT_BATCH,
+    "c3": DEFAULT_BATCH,
+    # the lane tree walk's per-launch cost (the tree copied to every
+    # workgroup's LDS, the flush, the tail) amortises further: 2^24 / 2^25
+    # / 2^26 traces per launch 5.82 / 6.06 / 6.23 G traces/s (1 GB of records)
+    "c4": 1 << 26,
+    # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
+    # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
+    # the pipelined queue pass's fill and drain (2^16 20.8,
+    # 2^18 22.3, 2^20 23.9 M traces/s)
+    "c5": 1 << 20,
+}
 
 
 def parse():
@@ -300,19 +316,49 @@ def compute_roofline(stream: bool, info, B: int, kern_ms: float):
 def make_multi(rank, world, local):
     """libisim's RCCL communicator for the stats merge (isim_multi_init_rank;
     the 128-byte id travels over torch.distributed, as a Go host would send it
-    out of band).  Returns (Multi or None, merge label)."""
+    out of band).  Returns (Multi or None, merge label).
+
+    The choice is collective: every rank first loads RCCL and draws an id
+    locally (isim_multi_get_id), the ranks agree on success (all_reduce MIN)
+    before anyone enters the collective ncclCommInitRank, and agree again
+    after it; on any failure every rank frees what it holds and all merge
+    with torch.distributed together (no rank is left waiting in a collective
+    the others skipped)."""
+    import torch
     import torch.distributed as dist
 
     from isim.dist import Multi
     if world == 1:
         return None, "none (1 rank)"
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    err = ""
+    mid = None
     try:
-        obj = [Multi.get_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        return Multi.init_rank(obj[0], world, rank, local), "isim_stats_allreduce_device (libisim RCCL)"
-    except Exception as e:  # reported in the JSON line: the torch RCCL merge is used instead
-        print(f"isim_multi_init_rank failed ({e}); merging with torch.distributed", file=sys.stderr)
-        return None, f"torch.distributed all_reduce (isim_multi_init_rank failed: {e})"
+        mid = Multi.get_id()  # RCCL loads on this rank (rank 0's id is the one used)
+    except Exception as e:
+        err = f"isim_multi_get_id failed on rank {rank}: {e}"
+    if not agree(mid is not None):
+        print(err or "isim_multi_get_id failed on another rank", file=sys.stderr)
+        return None, "torch.distributed all_reduce (isim_multi_get_id failed)"
+    obj = [mid if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    multi = None
+    try:
+        multi = Multi.init_rank(obj[0], world, rank, local)
+    except Exception as e:
+        err = f"isim_multi_init_rank failed on rank {rank}: {e}"
+    if not agree(multi is not None):
+        if multi is not None:
+            multi.close()
+        print(err or "isim_multi_init_rank failed on another rank", file=sys.stderr)
+        return None, "torch.distributed all_reduce (isim_multi_init_rank failed)"
+    return multi, "isim_stats_allreduce_device (libisim RCCL)"
 
 
 def teardown(multi):
@@ -459,22 +505,11 @@ def main():
                             flags=(isim.native.FLAG_NO_SVC_DUR if args.no_svc_dur else 0) |
                             (0 if args.fill else isim.native.FLAG_WALK_ALL))
     h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, params)
+    if args.batch == DEFAULT_BATCH:
+        args.batch = BENCH_BATCH[args.config]
+        args.des_auto_batch = args.config == "c5"
     if args.config == "c5":
-        if args.batch == DEFAULT_BATCH:
-            # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
-            # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
-            # the pipelined queue pass's fill and drain (2^16 20.8,
-            # 2^18 22.3, 2^20 23.9 M traces/s)
-            args.batch = 1 << 20
-            args.des_auto_batch = True
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
-    if args.config == "c4" and args.batch == DEFAULT_BATCH:
-        # the lane tree walk's per-launch cost (the tree copied to every
-        # workgroup's LDS, the flush, the tail) amortises further: 2^24 / 2^25
-        # / 2^26 traces per launch 5.82 / 6.06 / 6.23 G traces/s (1 GB of records)
-        args.batch = 1 << 26
-    if args.config == "c1" and args.batch == DEFAULT_BATCH:
-        args.batch = 1_000_000  # BASELINE config 1: 1M traces
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())
     B = args.batch

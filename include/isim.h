@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 7
+#define ISIM_ABI_VERSION 8
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -179,6 +179,9 @@ typedef struct {
                                 invocations and LDS tables fit; else 2/3) */
   int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
+  int32_t reserved;          /* 0 */
+  uint64_t max_launch_traces; /* isim_serve_device splits a batch into launches of at most this many traces
+                                 (per-workgroup u32 LDS counters must not wrap) */
 } isim_launch_info;
 
 ISIM_API const char *isim_last_error(void);
@@ -330,6 +333,11 @@ ISIM_API int isim_multi_init_rank(const isim_multi_id *id, int n_ranks, int rank
 /* One process, n_devices local devices = ranks 0..n-1 in the order given (ncclCommInitAll). */
 ISIM_API int isim_multi_init_all(const int *devices, int n_devices, isim_multi **out);
 ISIM_API void isim_multi_free(isim_multi *m);
+/* Aborts the communicator (ncclCommAbort on every local comm): a rank that
+ * fails before a collective calls it so that its peers' pending or next
+ * collectives fail with ISIM_ECOMM instead of waiting forever.  The handle
+ * is then only good for isim_multi_free; collectives on it return ECOMM. */
+ISIM_API int isim_multi_abort(isim_multi *m);
 ISIM_API int isim_multi_info(const isim_multi *m, int *n_ranks, int *n_local, int *first_rank);
 /* In-place all-reduce of the stats buffers of the local devices (d_stats[i]
  * on local device i, enqueued on hip_streams[i]; hip_streams may be NULL =
@@ -342,7 +350,9 @@ ISIM_API int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *
 /* Synchronous sharded batch: every local device walks its rank's shard; the
  * merged stats (identical on every rank) go to h_stats, the local shards'
  * records (n_local * n_per_rank, local device order) to h_records; either may
- * be NULL.  Collective over all ranks. */
+ * be NULL.  Collective over all ranks.  A local HIP failure before the
+ * all-reduce aborts the communicator when it has remote ranks
+ * (isim_multi_abort), so the peers return ECOMM rather than hang. */
 ISIM_API int isim_serve_multi(isim_handler *h, isim_multi *m, uint64_t trace_begin, uint64_t n_per_rank,
                      isim_trace_rec *h_records, uint64_t *h_stats);
 /* Host-side merges (the same rules): dst += src. */

@@ -337,6 +337,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
 
 }  // namespace
 
+static uint64_t max_launch_traces(const DevState *st);
+
 extern "C" {
 
 const char *isim_last_error(void) { return g_err.c_str(); }
@@ -486,6 +488,8 @@ int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out)
   out->max_blocks = (int32_t)st->max_blocks;
   out->kernel_kind = (int32_t)st->kind;
   out->fill = st->draw_free && !(h->params.flags & ISIM_FLAG_WALK_ALL) ? 1 : 0;
+  out->reserved = 0;
+  out->max_launch_traces = max_launch_traces(st);
   return ISIM_OK;
 }
 
@@ -507,10 +511,15 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
 // below 2^31 traces, and below 2^32 / max_mult traces with LDS counters (a
 // DAG whose shared callee is reached 2^22 times per trace: 1,023 traces per
 // launch).  Global counters are u64 atomics and need no split.
+static uint64_t max_launch_traces(const DevState *st) {
+  uint64_t m = 1ull << 31;
+  if (st->lds_counters) m = std::min<uint64_t>(m, std::max<uint64_t>(1, 0xFFFFFFFFull / st->max_mult));
+  return m;
+}
+
 static int launch_walk(isim_handler *h, DevState *st, uint64_t trace_begin, uint64_t n_traces,
                        isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream) {
-  uint64_t kMaxLaunch = 1ull << 31;
-  if (st->lds_counters) kMaxLaunch = std::min<uint64_t>(kMaxLaunch, std::max<uint64_t>(1, 0xFFFFFFFFull / st->max_mult));
+  const uint64_t kMaxLaunch = max_launch_traces(st);
   for (uint64_t done = 0; done < n_traces;) {
     const uint64_t n = std::min(n_traces - done, kMaxLaunch);
     const int rc = launch_walk_one(h, st, trace_begin + done, n, d_records ? d_records + done : nullptr, d_stats,

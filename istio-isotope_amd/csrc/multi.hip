@@ -42,6 +42,7 @@ struct Rccl {
   decltype(&ncclCommInitRank) CommInitRank = nullptr;
   decltype(&ncclCommInitAll) CommInitAll = nullptr;
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;  // optional
   decltype(&ncclAllReduce) AllReduce = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
@@ -70,6 +71,7 @@ const Rccl &rccl() {
            sym(r.AllReduce, "ncclAllReduce") && sym(r.GroupStart, "ncclGroupStart") &&
            sym(r.GroupEnd, "ncclGroupEnd") && sym(r.GetErrorString, "ncclGetErrorString");
     if (!r.ok) r.why = "RCCL library lacks an nccl* entry point";
+    (void)sym(r.CommAbort, "ncclCommAbort");
   });
   return r;
 }
@@ -84,6 +86,19 @@ const Rccl &rccl() {
   do {                                                                                       \
     hipError_t e_ = (expr);                                                                  \
     if (e_ != hipSuccess) return mfail(ISIM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Inside ncclGroupStart..ncclGroupEnd: an error closes the group and restores
+// the caller's device before returning (an open group would swallow the next
+// collective of this thread).
+#define GRPCHK(expr)                                                                         \
+  do {                                                                                       \
+    ncclResult_t e_ = (expr);                                                                \
+    if (e_ != ncclSuccess) {                                                                 \
+      (void)R.GroupEnd();                                                                    \
+      (void)hipSetDevice(prev);                                                              \
+      return mfail(ISIM_ECOMM, std::string(#expr) + ": " + R.GetErrorString(e_));            \
+    }                                                                                        \
   } while (0)
 
 // Gathers / scatters word `w` of each `row_words`-word row (the DES table's
@@ -107,6 +122,7 @@ struct isim_multi {
   std::vector<ncclComm_t> comms;   // one per local device
   std::vector<uint64_t *> scratch; // per local device: MAX-word staging of a DES table (grown on demand)
   std::vector<uint64_t> scratch_words;
+  bool aborted = false;            // isim_multi_abort: comms aborted, handle only freeable
   ~isim_multi() {
     const Rccl &R = rccl();
     for (size_t i = 0; i < comms.size(); ++i) {
@@ -197,6 +213,21 @@ int isim_multi_init_all(const int *devices, int n_devices, isim_multi **out) {
 
 void isim_multi_free(isim_multi *m) { delete m; }
 
+int isim_multi_abort(isim_multi *m) {
+  if (!m) return mfail(ISIM_EINVAL, "null argument");
+  const Rccl &R = rccl();
+  if (!m->aborted && R.ok) {
+    for (size_t i = 0; i < m->comms.size(); ++i) {
+      if (!m->comms[i]) continue;
+      if (R.CommAbort) (void)R.CommAbort(m->comms[i]);
+      else (void)R.CommDestroy(m->comms[i]);
+      m->comms[i] = nullptr;
+    }
+  }
+  m->aborted = true;
+  return ISIM_OK;
+}
+
 int isim_multi_info(const isim_multi *m, int *n_ranks, int *n_local, int *first_rank) {
   if (!m) return mfail(ISIM_EINVAL, "null argument");
   if (n_ranks) *n_ranks = m->n_ranks;
@@ -214,6 +245,7 @@ int isim_stats_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *
   uint32_t rows = 0;
   if (const int rc = stats_words_of(h, words, rows)) return rc;
   const Rccl &R = rccl();
+  if (m->aborted) return mfail(ISIM_ECOMM, "communicator aborted (isim_multi_abort)");
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
   RCCLCHK(R.GroupStart());
@@ -221,11 +253,11 @@ int isim_stats_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *
     uint64_t *s = d_stats[i];
     hipStream_t st = hip_streams ? (hipStream_t)hip_streams[i] : nullptr;
     constexpr uint64_t lo = ISIM_ST_NOT_MIN_LATENCY, hi = ISIM_ST_MAX_LATENCY + 1;
-    RCCLCHK(R.AllReduce(s, s, lo, ncclUint64, ncclSum, m->comms[i], st));
-    RCCLCHK(R.AllReduce(s + lo, s + lo, hi - lo, ncclUint64, ncclMax, m->comms[i], st));
-    RCCLCHK(R.AllReduce(s + hi, s + hi, words - hi, ncclUint64, ncclSum, m->comms[i], st));
+    GRPCHK(R.AllReduce(s, s, lo, ncclUint64, ncclSum, m->comms[i], st));
+    GRPCHK(R.AllReduce(s + lo, s + lo, hi - lo, ncclUint64, ncclMax, m->comms[i], st));
+    GRPCHK(R.AllReduce(s + hi, s + hi, words - hi, ncclUint64, ncclSum, m->comms[i], st));
   }
-  RCCLCHK(R.GroupEnd());
+  GRPCHK(R.GroupEnd());
   (void)hipSetDevice(prev);
   return ISIM_OK;
 }
@@ -239,6 +271,7 @@ int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *m, uint64
   if (rows == 0) return ISIM_OK;
   for (size_t i = 0; i < m->devices.size(); ++i)
     if (!d_tables[i]) return mfail(ISIM_EINVAL, "null device buffer");
+  if (m->aborted) return mfail(ISIM_ECOMM, "communicator aborted (isim_multi_abort)");
   const Rccl &R = rccl();
   int prev = 0;
   HIPCHK(hipGetDevice(&prev));
@@ -260,10 +293,10 @@ int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *m, uint64
   RCCLCHK(R.GroupStart());
   for (size_t i = 0; i < m->devices.size(); ++i) {
     hipStream_t st = hip_streams ? (hipStream_t)hip_streams[i] : nullptr;
-    RCCLCHK(R.AllReduce(d_tables[i], d_tables[i], (size_t)rows * W, ncclUint64, ncclSum, m->comms[i], st));
-    RCCLCHK(R.AllReduce(m->scratch[i], m->scratch[i], rows, ncclUint64, ncclMax, m->comms[i], st));
+    GRPCHK(R.AllReduce(d_tables[i], d_tables[i], (size_t)rows * W, ncclUint64, ncclSum, m->comms[i], st));
+    GRPCHK(R.AllReduce(m->scratch[i], m->scratch[i], rows, ncclUint64, ncclMax, m->comms[i], st));
   }
-  RCCLCHK(R.GroupEnd());
+  GRPCHK(R.GroupEnd());
   for (size_t i = 0; i < m->devices.size(); ++i) {
     HIPCHK(hipSetDevice(m->devices[i]));
     hipStream_t st = hip_streams ? (hipStream_t)hip_streams[i] : nullptr;
@@ -304,6 +337,9 @@ int isim_serve_multi(isim_handler *h, isim_multi *m, uint64_t trace_begin, uint6
     const uint64_t begin = trace_begin + (uint64_t)(m->first_rank + (int)i) * n_per_rank;
     rc = isim_serve_device(h, begin, n_per_rank, d_rec[i], d_stats[i], s);
   }
+  // a local failure before the collective: abort the communicator so the
+  // peer ranks' all-reduce fails (ECOMM) instead of waiting for this rank
+  if (rc != ISIM_OK && m->n_ranks > (int)L) (void)isim_multi_abort(m);
   if (rc == ISIM_OK) rc = isim_stats_allreduce_device(h, m, d_stats.data(), streams.data());
   for (size_t i = 0; i < L && rc == ISIM_OK; ++i) {
     if (hipSetDevice(m->devices[i]) != hipSuccess || hipStreamSynchronize((hipStream_t)streams[i]) != hipSuccess) {

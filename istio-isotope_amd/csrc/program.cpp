@@ -132,6 +132,9 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   out.slot_tbkt.assign(out.n_slots, 0);
   for (int32_t sl = 0; sl < out.n_slots; ++sl) out.slot_tbkt[sl] = slot_word(out.slot_callee[sl]);
   std::vector<uint32_t> through(out.n_slots, 0);
+  // positions whose callee's row has an LDS bucket table: a table word counts
+  // every invocation of that row in a workgroup (u32), like a slot counter
+  std::vector<uint32_t> row_through(out.row_svc.size(), 0);
   // preorder DFS over call sites; frame = (service, next call index, position, open calling invocations)
   struct Frame {
     int32_t svc;
@@ -177,6 +180,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
       nd.slot = (uint16_t)slot;
       through[slot] += 1;
+      if (dyn_off[out.svc_row[c]] != kTreeStaticRow) row_through[out.svc_row[c]] += 1;
       nd.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
       nd.pre = (uint32_t)cs.pre;
       TreeExt x{};
@@ -208,6 +212,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   }
   out.tree_mult = 1;
   for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
+  for (uint32_t m : row_through) out.tree_mult = std::max(out.tree_mult, m);
   out.tree_why.clear();
 }
 

@@ -53,7 +53,8 @@ struct Program {
   std::vector<TreeDynRow> tree_dyn; // rows whose duration bucket varies: their LDS bucket tables
   uint32_t tree_dyn_words = 0;
   uint32_t tree_frames = 0;         // register-stack frames the walk needs (open calling invocations - 1)
-  uint32_t tree_mult = 0;           // most positions through one slot (LDS counter overflow guard)
+  uint32_t tree_mult = 0;           // most positions through one slot or into one bucket-table row (LDS u32
+                                    // counter overflow guard)
   std::string tree_why;
 };
 

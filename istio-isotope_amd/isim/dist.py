@@ -107,6 +107,11 @@ class Multi:
     def __del__(self):
         self.close()
 
+    def abort(self):
+        """isim_multi_abort: peers' collectives on this communicator fail (ECOMM) instead of waiting."""
+        if self._m is not None and self._m.value:
+            native.check(native.load().isim_multi_abort(self._m))
+
     def allreduce_stats(self, handler, d_stats: Sequence[int], streams: Optional[Sequence[int]] = None):
         """In-place merge of the local devices' stats buffers (device pointers)."""
         native.check(native.load().isim_stats_allreduce_device(

@@ -23,7 +23,7 @@ STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "E
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV",
                 10: "ECOMM"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 7  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 8  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
@@ -76,7 +76,7 @@ class HandlerInfo(C.Structure):
 class LaunchInfo(C.Structure):
     _fields_ = [("wg_threads", C.c_int32), ("lds_bytes", C.c_int32), ("lds_counters", C.c_int32),
                 ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32),
-                ("fill", C.c_int32)]
+                ("fill", C.c_int32), ("reserved", C.c_int32), ("max_launch_traces", C.c_uint64)]
 
 
 class DesParams(C.Structure):
@@ -126,6 +126,7 @@ SIGNATURES = {
     "isim_multi_init_rank": (C.c_int, [C.POINTER(MultiId), C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),
     "isim_multi_init_all": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(_VP)]),
     "isim_multi_free": (None, [_VP]),
+    "isim_multi_abort": (C.c_int, [_VP]),
     "isim_multi_info": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "isim_stats_allreduce_device": (C.c_int, [_VP, _VP, C.POINTER(_VP), C.POINTER(_VP)]),
     "isim_des_table_allreduce_device": (C.c_int, [_VP, _VP, C.POINTER(_VP), C.POINTER(_VP)]),

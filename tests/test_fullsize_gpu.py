@@ -1,9 +1,16 @@
 """Full-size GPU runs (BASELINE-scale batches) checked through size-independent
 properties, plus bit-exact windows sampled across the trace range and
-recomputed by the CPU oracle."""
+recomputed by the CPU oracle.  The bench's own batches (bench.BENCH_BATCH:
+config 3 at 2^24 traces per launch in modes A and B, config 4 at 2^26) are
+checked at exactly those sizes, two consecutive launches into one stats
+buffer as bench.time_walk runs them, with oracle windows at the first and
+last traces of each launch and across every internal launch split
+(isim_launch_info.max_launch_traces).  Reference behaviour:
+isotope/service/pkg/srv/executable.go:84-144 (skips, calls, error handling)."""
 import numpy as np
 import pytest
 
+import bench
 import isim
 from isim.generators import config2_topology, config3_topology, mesh_topology, realistic_topology
 from isim.yamljson import obj_to_json
@@ -13,29 +20,56 @@ from parity import Case, assert_records_equal, with_defaults
 pytestmark = pytest.mark.gpu
 
 
-def _device_run(case: Case, begin: int, n: int):
+def _device_run(case: Case, begin: int, n: int, launches: int = 1):
+    """`launches` consecutive isim_serve_device calls of n traces each (trace
+    ids begin + i*n), records into one device buffer, ONE stats buffer
+    accumulated across them (bench.time_walk's pattern)."""
     import torch
     h = case.handler
     dev = torch.device("cuda", 0)
     stats = torch.zeros(h.stats_words, dtype=torch.int64, device=dev)
-    recs = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    recs = torch.empty((n * launches, 2), dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev)
-    h.serve_device(begin, n, recs.data_ptr(), stats.data_ptr(), s.cuda_stream)
+    for i in range(launches):
+        h.serve_device(begin + i * n, n, recs[i * n:].data_ptr(), stats.data_ptr(), s.cuda_stream)
     torch.cuda.synchronize()
     r = recs.cpu().numpy().view(np.uint64)
-    rec = np.zeros(n, isim.REC_DTYPE)
+    del recs
+    rec = np.zeros(n * launches, isim.REC_DTYPE)
     rec["latency_ns"] = r[:, 0]
     rec["hops"] = (r[:, 1] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     rec["status_err"] = (r[:, 1] >> np.uint64(32)).astype(np.uint32)
     return rec, h.fold(stats.cpu().numpy().view(np.uint64))
 
 
+def _check_window(case: Case, rec, begin, s0, width):
+    orec, _ = case.cpu(begin + int(s0), width)
+    assert_records_equal(rec[s0:s0 + width], orec)
+
+
 def _sampled_windows(case: Case, rec, begin, n, windows=8, width=256, seed=0):
     rng = np.random.default_rng(seed)
     starts = sorted(set([0, n - width] + list(rng.integers(0, n - width, windows))))
     for s0 in starts:
-        orec, _ = case.cpu(begin + int(s0), width)
-        assert_records_equal(rec[s0:s0 + width], orec)
+        _check_window(case, rec, begin, s0, width)
+
+
+def _launch_edge_windows(case: Case, rec, begin, n, launches, width=256):
+    """Oracle windows at the first and last `width` traces of every launch and
+    straddling every internal split of a launch (the library splits a batch
+    into launches of at most max_launch_traces traces so that no u32 LDS
+    counter can wrap: api.hip launch_walk, Program::tree_mult)."""
+    m = int(case.handler.launch_info(0)["max_launch_traces"])
+    assert m >= 1
+    edges = set()
+    for i in range(launches):
+        lo = i * n
+        edges.update([lo, lo + n - width])
+        for cut in range(lo + m, lo + n, m):  # internal splits of launch i
+            edges.add(cut - width // 2)
+    for s0 in sorted(edges):
+        _check_window(case, rec, begin, s0, width)
+    return m
 
 
 def _common_properties(f, rec, n):
@@ -54,9 +88,9 @@ def _common_properties(f, rec, n):
     assert int(f["svc_calls"].sum()) == f["sum_hops"]
 
 
-def test_config3_full_batch():
-    """BASELINE config 3 graph, one full bench batch (2^22 traces) at a
-    trace offset beyond 2^32; mode A."""
+def test_config3_full_batch(gpu):
+    """BASELINE config 3 graph, 2^22 traces at a trace offset beyond 2^32;
+    mode A (the bench batch itself: test_config3_bench_batch)."""
     c = Case(obj_to_json(config3_topology()))
     n, begin = 1 << 22, (1 << 32) - (1 << 21)
     rec, f = _device_run(c, begin, n)
@@ -84,7 +118,7 @@ def config3_informative():
 
 
 @pytest.mark.parametrize("informative", [True, False])
-def test_config3_mode_b_full_batch(informative):
+def test_config3_mode_b_full_batch(gpu, informative):
     c = Case(config3_informative() if informative else obj_to_json(config3_topology()), None,
              isim.SimParams(error_mode=isim.MODE_B))
     n = 1 << 21
@@ -103,7 +137,7 @@ def test_config3_mode_b_full_batch(informative):
     _sampled_windows(c, rec, 123, n, windows=8 if informative else 4)
 
 
-def test_config2_full_batch():
+def test_config2_full_batch(gpu):
     """BASELINE config 2 (tree 4x8, sequential) with a 0.1% errorRate."""
     c = Case(with_defaults(obj_to_json(config2_topology()), errorRate=0.001))
     n = 1 << 23
@@ -113,7 +147,7 @@ def test_config2_full_batch():
     _sampled_windows(c, rec, 0, n)
 
 
-def test_config4_mesh_full_batch():
+def test_config4_mesh_full_batch(gpu):
     """BASELINE config 4 graph (100k-service mesh, probability 30): dynamic
     walk; hop counts vary per trace."""
     c = Case(with_defaults(obj_to_json(mesh_topology()), errorRate=0.01))
@@ -126,3 +160,76 @@ def test_config4_mesh_full_batch():
     expected = sum(0.9 ** k for k in range(8))
     assert abs(hops.mean() - expected) < 0.05
     _sampled_windows(c, rec, 7, n)
+
+
+def test_config3_bench_batch(gpu):
+    """config 3 exactly as bench.py times it: bench.build_graph("c3"), the
+    bench's params (mode A, every trace walked), BENCH_BATCH["c3"] = 2^24
+    traces per launch, two consecutive launches into one stats buffer, trace
+    ids from just below 2^32 (the bench's shard_begin ids cross it at step
+    256)."""
+    j, _ = bench.build_graph("c3")
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    n, L = bench.BENCH_BATCH["c3"], 2
+    assert n == 1 << 24
+    begin = (1 << 32) - n - 1000
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    assert np.all(rec["hops"] == 10000)
+    assert np.all(rec["latency_ns"] == c.handler.info.max_latency_ns)
+    assert np.all(f["svc_calls"] == n * L)
+    # executed calls per site = traces (static walk); callee 500s per site sum to the services' 500s
+    assert np.all(f["site_calls"] == n * L)
+    _launch_edge_windows(c, rec, begin, n, L)
+    _sampled_windows(c, rec, begin, n * L, windows=6, seed=3)
+
+
+def test_config3_bench_batch_mode_b(gpu):
+    """config 3's graph in mode B with the informative errorRate
+    (bench.mode_b_legs "mode_b_informative"), the close-list kernel, 2^24
+    traces per launch, two launches into one stats buffer."""
+    c = Case(config3_informative(), None, isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_WALK_ALL))
+    assert c.handler.launch_info(0)["kernel_kind"] == 6
+    n, L = bench.BENCH_BATCH["c3"], 2
+    begin = 5 * n
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    st500 = (rec["status_err"] >> 31).astype(bool)
+    assert np.array_equal(st500, (rec["status_err"] & 0x7FFFFFFF) > 0)
+    assert 0.2 < f["n_500"] / (n * L) < 0.8
+    _launch_edge_windows(c, rec, begin, n, L)
+    _sampled_windows(c, rec, begin, n * L, windows=4, seed=4)
+
+
+def test_config4_bench_batch(gpu):
+    """config 4 exactly as bench.py times it: bench.build_graph("c4") (no
+    errorRate: every draw is a probability skip), per-service duration rows
+    on, BENCH_BATCH["c4"] = 2^26 traces per launch (1 GiB of records), two
+    launches into one stats buffer; oracle windows at every launch edge and
+    internal split; the duration table's counts and sums checked against the
+    records and the slot counters."""
+    j, _ = bench.build_graph("c4")
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7
+    n, L = bench.BENCH_BATCH["c4"], 2
+    assert n == 1 << 26
+    begin = 11
+    rec, f = _device_run(c, begin, n, L)
+    N = n * L
+    _common_properties(f, rec, N)
+    hops = rec["hops"].astype(np.float64)
+    expected = sum(0.9 ** k for k in range(8))
+    assert abs(hops.mean() - expected) < 0.01
+    assert f["n_500"] == 0 and f["sum_err_hops"] == 0
+    # duration table: every row's code-200 bucket counts = the service's invocations
+    dur = np.asarray(f["svc_dur"], np.uint64)
+    assert np.array_equal(dur[:, :isim.native.N_PROM].sum(axis=1), np.asarray(f["svc_calls"], np.uint64))
+    assert int(dur[:, isim.native.N_PROM:2 * isim.native.N_PROM].sum()) == 0
+    entry = c.handler.info.entry
+    assert int(dur[entry, 2 * isim.native.N_PROM]) == f["sum_latency"]
+    m = _launch_edge_windows(c, rec, begin, n, L)
+    _sampled_windows(c, rec, begin, N, windows=8, seed=5)
+    # the full stats of one oracle-sized window through the same kernel (1 launch, svc_dur included)
+    c.compare(begin + 3 * n // 2, 1 << 16)
+    print(f"max_launch_traces={m}")
