@@ -204,6 +204,37 @@ ISIM_API int isim_graph_marshal_json(const isim_graph *g, char *buf, size_t cap,
  * the Graphviz DOT text of `isotope convert graphviz`. */
 ISIM_API int isim_graph_to_dot(const isim_graph *g, char *buf, size_t cap, size_t *len);
 /* extractService: first service with that name (graph.go:97-109); -1 if absent. */
+/* ---- Kubernetes manifests (convert/pkg/kubernetes) ----
+ * Replaces kubernetes.ServiceGraphToKubernetesManifests(serviceGraph,
+ * serviceNodeSelector, serviceImage, serviceMaxIdleConnectionsPerHost,
+ * clientNodeSelector, clientImage, environmentName)
+ * (isotope/convert/pkg/kubernetes/kubernetes.go:56-63): Namespace, ConfigMap
+ * (the graph as yaml.Marshal), per service a Deployment + Service (+ RBAC
+ * rules under ISTIO), the Fortio client Deployment + Service, YAML documents
+ * joined by "---\n" exactly as sigs.k8s.io/yaml v1.2.0 renders k8s.io/api
+ * v0.18.0 objects.  Node selectors are n key/value pairs [k0, v0, k1, v1, ...]
+ * (the CLI's "k=v" flag, cmd/kubernetes.go:96-108).  EXT: the reference stamps
+ * time.Now() and names RBAC rules with uuid.New(); here every
+ * creationTimestamp is creation_timestamp_s (UTC, RFC 3339) and the rule
+ * names are v4 UUIDs from Philox4x32-10 keyed by rbac_seed. */
+typedef struct {
+  const char *service_image;                 /* "" / NULL: omitted, as Go's omitempty */
+  const char *client_image;
+  const char *environment_name;              /* "NONE" or "ISTIO" (strings.EqualFold); NULL = "NONE" */
+  const char *const *service_node_selector;  /* 2 * n_service_node_selector strings */
+  const char *const *client_node_selector;   /* 2 * n_client_node_selector strings */
+  int32_t n_service_node_selector;
+  int32_t n_client_node_selector;
+  int32_t service_max_idle_connections_per_host;
+  int32_t reserved;                          /* 0 */
+  int64_t creation_timestamp_s;              /* unix seconds of every metadata.creationTimestamp */
+  uint64_t rbac_seed;                        /* RBAC rule names (environment ISTIO, numRbacPolicies > 0) */
+} isim_k8s_params;
+/* Writes at most cap bytes (NUL-terminated when it fits); *len = bytes needed. */
+ISIM_API int isim_graph_to_k8s_manifests(const isim_graph *g, const isim_k8s_params *p, char *buf, size_t cap,
+                                         size_t *len);
+/* yaml.Marshal(graph) (sigs.k8s.io/yaml: JSONToYAML of json.Marshal) — the ConfigMap payload. */
+ISIM_API int isim_graph_marshal_yaml(const isim_graph *g, char *buf, size_t cap, size_t *len);
 ISIM_API int isim_graph_service_index(const isim_graph *g, const char *name);
 
 /* ---- units (convert/pkg/graph/size, pct, script/sleep_command.go) ---- */

@@ -15,6 +15,7 @@
 #include "../../include/isim.h"
 #include "gounits.h"
 #include "graph.h"
+#include "k8s.h"
 #include "marshal.h"
 #include "des.h"
 #include "kernel_abi.h"
@@ -391,6 +392,21 @@ int isim_graph_marshal_json(const isim_graph *g, char *buf, size_t cap, size_t *
 int isim_graph_to_dot(const isim_graph *g, char *buf, size_t cap, size_t *len) {
   if (!g) return fail(ISIM_EINVAL, "null graph");
   return emit(isim::to_dot(g->g), buf, cap, len);
+}
+
+int isim_graph_to_k8s_manifests(const isim_graph *g, const isim_k8s_params *p, char *buf, size_t cap, size_t *len) {
+  if (!g || !p) return fail(ISIM_EINVAL, "null argument");
+  std::string out, err;
+  const int rc = isim::k8s_manifests(g->g, *p, out, err);
+  if (rc != ISIM_OK) return fail(rc, err);
+  return emit(out, buf, cap, len);
+}
+
+int isim_graph_marshal_yaml(const isim_graph *g, char *buf, size_t cap, size_t *len) {
+  if (!g) return fail(ISIM_EINVAL, "null graph");
+  const std::string y = isim::graph_yaml(g->g);
+  if (y.empty()) return fail(ISIM_EINVAL, "graph marshal failed");
+  return emit(y, buf, cap, len);
 }
 
 int isim_graph_service_index(const isim_graph *g, const char *name) {

@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 from dataclasses import dataclass, field
-from typing import Any, List, Optional
+from typing import Optional, Any, List, Optional
 
 from . import native
 from .yamljson import yaml_to_json
@@ -126,6 +126,37 @@ class ServiceGraph:
     def to_dot(self) -> str:
         """graphviz.ServiceGraphToDotLanguage (convert/pkg/graphviz/graphviz.go:28-41)."""
         return self._text(native.load().isim_graph_to_dot).decode("utf-8")
+
+    def marshal_yaml(self) -> str:
+        """yaml.Marshal(graph) through sigs.k8s.io/yaml (the ConfigMap payload
+        of convert/pkg/kubernetes/kubernetes.go:159-175)."""
+        return self._text(native.load().isim_graph_marshal_yaml).decode("utf-8")
+
+    def to_k8s_manifests(self, service_node_selector: Optional[dict] = None, service_image: str = "",
+                         service_max_idle_connections_per_host: int = 0,
+                         client_node_selector: Optional[dict] = None, client_image: str = "",
+                         environment_name: str = "NONE", creation_timestamp_s: int = 0,
+                         rbac_seed: int = 0) -> str:
+        """kubernetes.ServiceGraphToKubernetesManifests (kubernetes.go:56-137),
+        same argument order.  EXT: creationTimestamp and RBAC rule names are
+        deterministic (creation_timestamp_s, rbac_seed) where the reference
+        uses time.Now() and uuid.New()."""
+        def kv(d):
+            items = [x for k, v in (d or {}).items() for x in (str(k).encode(), str(v).encode())]
+            arr = (C.c_char_p * max(1, len(items)))(*items)
+            return arr, len(items) // 2
+        sarr, sn = kv(service_node_selector)
+        carr, cn = kv(client_node_selector)
+        p = native.K8sParams(service_image.encode(), client_image.encode(), environment_name.encode(),
+                             C.cast(sarr, C.c_void_p), C.cast(carr, C.c_void_p), sn, cn,
+                             service_max_idle_connections_per_host, 0, creation_timestamp_s,
+                             rbac_seed & ((1 << 64) - 1))
+        lib = native.load()
+        n = C.c_size_t()
+        native.check(lib.isim_graph_to_k8s_manifests(self._h, C.byref(p), None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        native.check(lib.isim_graph_to_k8s_manifests(self._h, C.byref(p), buf, n.value, C.byref(n)))
+        return buf.raw[:n.value - 1].decode("utf-8")
 
     @property
     def services(self) -> List[Service]:

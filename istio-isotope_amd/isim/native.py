@@ -83,6 +83,14 @@ class DesParams(C.Structure):
     _fields_ = [("mean_interarrival_ns", C.c_uint64), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class K8sParams(C.Structure):
+    _fields_ = [("service_image", C.c_char_p), ("client_image", C.c_char_p), ("environment_name", C.c_char_p),
+                ("service_node_selector", C.c_void_p), ("client_node_selector", C.c_void_p),
+                ("n_service_node_selector", C.c_int32), ("n_client_node_selector", C.c_int32),
+                ("service_max_idle_connections_per_host", C.c_int32), ("reserved", C.c_int32),
+                ("creation_timestamp_s", C.c_int64), ("rbac_seed", C.c_uint64)]
+
+
 class MultiId(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
@@ -103,6 +111,8 @@ SIGNATURES = {
     "isim_graph_canonical_json": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "isim_graph_marshal_json": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "isim_graph_to_dot": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "isim_graph_to_k8s_manifests": (C.c_int, [_VP, C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "isim_graph_marshal_yaml": (C.c_int, [_VP, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "isim_graph_service_index": (C.c_int, [_VP, C.c_char_p]),
     "isim_size_from_string": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     "isim_duration_parse": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
