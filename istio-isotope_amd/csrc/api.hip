@@ -218,7 +218,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
       tree = true;
       st.kind = 7;
       st.tree_ext_lds = ext_lds;
-      st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames, ext_lds);
+      st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames, ext_lds,
+                                    (p.tree_flags & isim::kTreeAnyConc) != 0);
       st.threads = isim::kWgThreads;
       st.lds_bytes = need;
       st.lds_counters = 1;
@@ -569,6 +570,7 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.n_rows = (uint32_t)h->prog.row_svc.size();
   kp.n_dyn = (uint32_t)h->prog.tree_dyn.size();
   kp.dyn_words = h->prog.tree_dyn_words;
+  kp.tree_flags = h->prog.tree_flags;
   const uint64_t per_wave = is_stream(st->kind) ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;

@@ -81,7 +81,14 @@ enum TreeFlag : uint8_t {
   TF_LEAF = 4,        // the callee makes no calls
   TF_ERR_ALWAYS = 8,  // callee errorRate 1
   TF_ERR_DRAW = 16,   // 0 < callee errorRate < 1: draw against thr
+  TF_PROBK0 = 32,     // the callee's script has a probabilistic call among its first 4 calls (its skip
+                      // residues, Philox block (t, hop, 1, 0), are drawn when it opens)
 };
+// Program.tree_flags / KParams.tree_flags: what the walk contains
+constexpr uint32_t kTreeAnyProb = 1;  // some position is a probabilistic call
+constexpr uint32_t kTreeAnyDraw = 2;  // some position draws its error against a threshold
+constexpr uint32_t kTreeAnyConc = 4;  // some call step is concurrent
+constexpr uint32_t kTreeMaxCalls = 4 * 2047;  // calls per script: the skip-block index fits 11 flag bits
 struct TreeNode {
   uint16_t size;   // positions in the subtree (itself included): a skipped call jumps over them
   uint16_t k;      // index of the call command in the caller's script (skip-draw block and word)
@@ -136,6 +143,7 @@ struct KParams {
   uint32_t n_rows;               // kind 7: duration-table rows (LDS sums)
   uint32_t n_dyn;                // kind 7: entries of tree_dyn
   uint32_t dyn_words;            // kind 7: LDS words of the bucket tables
+  uint32_t tree_flags;           // kind 7: kTreeAny*
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to
@@ -160,7 +168,7 @@ constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 // 5 draw stream + mode-B bit stack, 6 draw stream + mode-B close list,
 // 7 lane tree walk (dynamic walks, tree.hip; `frames` = register stack depth).
 void *walk_kernel(int kind, bool modeb, bool lds_counters);
-void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds);
+void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds, bool conc);
 // LDS layout of the kind-7 kernel: accumulators, histograms, per-slot
 // counters (u32 calls, u32 500s), per-row u64 duration sums (code 200), the
 // bucket tables of the varying rows, the nodes, and (ext_lds) the TreeExt

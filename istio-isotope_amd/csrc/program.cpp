@@ -129,6 +129,18 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     if (thr[s] >= (1ull << 32)) return TF_ERR_ALWAYS;
     return thr[s] > 0 ? (uint8_t)TF_ERR_DRAW : (uint8_t)0;
   };
+  // per service: a probabilistic call among its first 4 call commands (TF_PROBK0); script length bound
+  std::vector<char> probk0(n, 0);
+  for (int32_t s = 0; s < n; ++s)
+    for (int32_t si : svc_sites[s]) {
+      const Site &st = sites[si];
+      if (st.k < 4 && st.prob >= 1 && st.prob <= 99) probk0[s] = 1;
+      if (st.k >= kTreeMaxCalls) {
+        out.tree_why = "a script with more than 8188 calls";
+        return;
+      }
+    }
+  out.tree_flags = 0;
   out.slot_tbkt.assign(out.n_slots, 0);
   for (int32_t sl = 0; sl < out.n_slots; ++sl) out.slot_tbkt[sl] = slot_word(out.slot_callee[sl]);
   std::vector<uint32_t> through(out.n_slots, 0);
@@ -144,7 +156,8 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   std::vector<Frame> stack;
   const int32_t e = out.entry;
   TreeNode root{};
-  root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e));
+  root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e) | (probk0[e] ? TF_PROBK0 : 0));
+  if (root.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
   root.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
   TreeExt rx{};
   rx.tc = (uint32_t)shape_of(e).tail;
@@ -176,7 +189,10 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       }
       nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
       nd.flags = (uint8_t)((cs.step_first ? TF_STEP : 0) | (cs.conc ? TF_CONC : 0) | (leaf[c] ? TF_LEAF : 0) |
-                           err_flags(c));
+                           err_flags(c) | (probk0[c] ? TF_PROBK0 : 0));
+      if (nd.prob) out.tree_flags |= kTreeAnyProb;
+      if (nd.flags & TF_CONC) out.tree_flags |= kTreeAnyConc;
+      if (nd.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
       const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
       nd.slot = (uint16_t)slot;
       through[slot] += 1;

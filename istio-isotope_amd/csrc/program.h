@@ -55,6 +55,7 @@ struct Program {
   uint32_t tree_frames = 0;         // register-stack frames the walk needs (open calling invocations - 1)
   uint32_t tree_mult = 0;           // most positions through one slot or into one bucket-table row (LDS u32
                                     // counter overflow guard)
+  uint32_t tree_flags = 0;          // kTreeAnyProb | kTreeAnyDraw
   std::string tree_why;
 };
 

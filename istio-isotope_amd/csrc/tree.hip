@@ -110,7 +110,7 @@ struct TreeSink {
   }
 };
 
-template <bool MODEB, int FRAMES, bool EXTL>
+template <bool MODEB, int FRAMES, bool EXTL, bool CONC>
 __global__ void __launch_bounds__(kWgThreads, 1)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(kWgThreads, 1)
   bool dry = b >= n_batches;
   uint64_t nxt = dry ? 0 : b * 64, lim = dry ? 0 : (b * 64 + 64 < n ? b * 64 + 64 : n);
   const uint64_t lt = ((uint64_t)1 << lane_id()) - 1;  // lanes below this one
-  tw::Lane<FRAMES, MODEB> L;
+  tw::Lane<FRAMES, MODEB, CONC> L;
   bool active = false;  // the lane holds a trace whose record is not yet written
   uint64_t idx = 0;
   uint64_t a_lat = 0, a_hops = 0, a_err = 0, a_lat500 = 0, a_max = 0, a_notmin = 0;
@@ -319,17 +319,19 @@ __global__ void __launch_bounds__(kWgThreads, 1)
 }  // namespace dev
 
 // Register-stack depths compiled: the smallest that holds the graph's frames;
-// TreeExt in LDS when it fits (ext_lds), else read from HBM.
-template <bool EXTL>
+// TreeExt in LDS when it fits (ext_lds), else read from HBM; walks without
+// concurrent steps keep no step maxima (CONC = false).
+template <bool EXTL, bool CONC>
 static void *tree_pick(bool modeb, uint32_t frames) {
   using namespace dev;
-  if (frames <= 4) return modeb ? (void *)&isim_tree<true, 4, EXTL> : (void *)&isim_tree<false, 4, EXTL>;
-  if (frames <= 8) return modeb ? (void *)&isim_tree<true, 8, EXTL> : (void *)&isim_tree<false, 8, EXTL>;
-  return modeb ? (void *)&isim_tree<true, 16, EXTL> : (void *)&isim_tree<false, 16, EXTL>;
+  if (frames <= 4) return modeb ? (void *)&isim_tree<true, 4, EXTL, CONC> : (void *)&isim_tree<false, 4, EXTL, CONC>;
+  if (frames <= 8) return modeb ? (void *)&isim_tree<true, 8, EXTL, CONC> : (void *)&isim_tree<false, 8, EXTL, CONC>;
+  return modeb ? (void *)&isim_tree<true, 16, EXTL, CONC> : (void *)&isim_tree<false, 16, EXTL, CONC>;
 }
 
-void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds) {
-  return ext_lds ? tree_pick<true>(modeb, frames) : tree_pick<false>(modeb, frames);
+void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds, bool conc) {
+  if (conc) return ext_lds ? tree_pick<true, true>(modeb, frames) : tree_pick<false, true>(modeb, frames);
+  return ext_lds ? tree_pick<true, false>(modeb, frames) : tree_pick<false, false>(modeb, frames);
 }
 
 }  // namespace isim

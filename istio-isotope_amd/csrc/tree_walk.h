@@ -19,7 +19,9 @@
 //   * an invocation closes when the walk passes its subtree: the time after
 //     its last call step is added (unless it failed), its status is its own
 //     error draw (or its failure in mode B), and H + T folds into the caller
-//     (sum for a sequential call, max inside a concurrent step).
+//     (sum for a sequential call, max inside a concurrent step);
+//   * a call's skip draw comes from its caller's block of four residues,
+//     drawn when the caller opens (Lane::step).
 #pragma once
 #include <stdint.h>
 
@@ -77,22 +79,41 @@ ISIM_TW uint32_t word4(uint32_t w, uint32_t a, uint32_t b, uint32_t c, uint32_t 
   return (w & 2u) ? hi : lo;
 }
 
+constexpr uint32_t KB_SHIFT = 5;  // f_fl bits 5-15: the call block whose skip residues f_res holds
+constexpr uint32_t KB_NONE = 0x7FFu;
+constexpr int kScan = 3;          // skipped calls a step may pass after its action (tree.hip: uniform trips)
+
+// The four skip draws of a Philox block reduced to what shouldSkipRequest
+// compares (word % 100, 7 bits each): skip call k iff residue(k & 3) < 100 - p.
+ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return (a % 100u) | (b % 100u) << 7 | (c % 100u) << 14 | (d % 100u) << 21;
+}
+
 // Sink: call(slot) per executed call; resp(slot, row word, T, status) per
 // response of a called invocation (the entry's is the trace result).
-template <int FRAMES, bool MODEB>
+//
+// One step() is a MACRO step: close the current invocation if the walk has
+// passed its subtree, then process position p (a call: skip it, run a leaf
+// callee, or open a calling callee), then pass up to kScan further calls whose
+// skip draw says skip.  A wave runs its 64 lanes' steps in lock step, so
+// fewer, fuller steps per trace are what count (config 4: 25.9 -> 11.1
+// wave iterations per 64 traces).  The skip residues of an invocation are
+// drawn once, when it opens, and kept in its frame (f_res), so returning from
+// a callee never recomputes the caller's block and the scans need no draw.
+// CONC: the walk has concurrent steps (without them no frame keeps a step max).
+template <int FRAMES, bool MODEB, bool CONC = true>
 struct Lane {
   uint32_t t_lo = 0, t_hi = 0;
   uint32_t p = 0, d = 0, end = 0, hopn = 0, errh = 0;
   bool done = true;
   uint32_t lat = 0;
   bool root500 = false;
-  // current invocation
-  uint32_t f_pos = 0, f_acc = 0, f_cmax = 0, f_hop = 0, f_fl = 0;
-  // calling invocations below it
-  uint32_t s_pos[FRAMES > 0 ? FRAMES : 1], s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[FRAMES > 0 ? FRAMES : 1],
-      s_hop[FRAMES > 0 ? FRAMES : 1];
-  // cached Philox blocks: skip draws (key: caller hop, block) and error draws (key: hop >> 2)
-  uint32_t sk_hop = 0xFFFFFFFFu, sk_blk = 0, sk0 = 0, sk1 = 0, sk2 = 0, sk3 = 0;
+  // current invocation (f_fl: FL_* | call block of f_res << KB_SHIFT)
+  uint32_t f_pos = 0, f_acc = 0, f_cmax = 0, f_hop = 0, f_fl = 0, f_res = 0;
+  // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time
+  uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1],
+      s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
+  // cached error block: words of Philox (t, ek_blk, 0, 0)
   uint32_t ek_blk = 0xFFFFFFFFu, e0 = 0, e1 = 0, e2 = 0, e3 = 0;
 
   // k0, k1: the Philox key (wave-uniform: passed in, never stored per lane)
@@ -112,6 +133,13 @@ struct Lane {
     return word4(hop & 3u, e0, e1, e2, e3) < thr;
   }
 
+  // skip residues of call block kb of the invocation with hop id `hop`
+  ISIM_TW uint32_t residues(uint32_t hop, uint32_t kb, uint32_t k0, uint32_t k1) const {
+    uint32_t a = t_lo, b = t_hi, c = hop, dd = 1u + kb;
+    philox10(a, b, c, dd, k0, k1);
+    return pack_res(a, b, c, dd);
+  }
+
   // Enters the entry invocation (hop 0).  A leaf entry responds at once.
   ISIM_TW void start(uint64_t trace, uint32_t key0, uint32_t key1, const TreeNode *nodes, const TreeExt *ext) {
     t_lo = (uint32_t)trace;
@@ -120,8 +148,7 @@ struct Lane {
     hopn = 1;
     errh = 0;
     d = 0;
-    sk_hop = 0xFFFFFFFFu;  // the Philox caches belong to the previous trace of the lane
-    ek_blk = 0xFFFFFFFFu;
+    ek_blk = 0xFFFFFFFFu;  // the error block belongs to the previous trace of the lane
     const TreeNode n = nodes[0];
     const bool own = own_error(0, n.flags, n.thr, key0, key1);
     if (n.flags & TF_LEAF) {
@@ -135,13 +162,15 @@ struct Lane {
     f_acc = 0;
     f_cmax = 0;
     f_hop = 0;
-    f_fl = own ? FL_OWN : 0u;
+    const bool pk = (n.flags & TF_PROBK0) != 0;
+    f_res = pk ? residues(0, 0, key0, key1) : 0u;
+    f_fl = (own ? FL_OWN : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
     end = n.size;
     p = 1;
   }
 
   ISIM_TW void fold(uint32_t c, bool st, bool conc) {
-    if (conc) {
+    if (CONC && conc) {
       f_cmax = c > f_cmax ? c : f_cmax;
       if (MODEB && st) f_fl |= FL_CERR;
     } else {
@@ -154,97 +183,103 @@ struct Lane {
 #pragma unroll
     for (int i = 0; i < FRAMES; ++i) {
       const bool m = d == (uint32_t)i;
-      s_pos[i] = m ? (f_pos | (f_fl << 16)) : s_pos[i];
+      s_pe[i] = m ? (f_pos | (end << 16)) : s_pe[i];
+      s_hf[i] = m ? (f_hop | (f_fl << 16)) : s_hf[i];
+      s_res[i] = m ? f_res : s_res[i];
       s_acc[i] = m ? f_acc : s_acc[i];
-      s_cmax[i] = m ? f_cmax : s_cmax[i];
-      s_hop[i] = m ? f_hop : s_hop[i];
+      if (CONC) s_cmax[i] = m ? f_cmax : s_cmax[i];
     }
     ++d;
   }
 
   ISIM_TW void pop() {
     --d;
-    uint32_t a = 0, b = 0, c = 0, h = 0;
+    uint32_t pe = 0, hf = 0, r = 0, a = 0, c = 0;
 #pragma unroll
     for (int i = 0; i < FRAMES; ++i) {
       const bool m = d == (uint32_t)i;
-      a = m ? s_pos[i] : a;
-      b = m ? s_acc[i] : b;
-      c = m ? s_cmax[i] : c;
-      h = m ? s_hop[i] : h;
+      pe = m ? s_pe[i] : pe;
+      hf = m ? s_hf[i] : hf;
+      r = m ? s_res[i] : r;
+      a = m ? s_acc[i] : a;
+      if (CONC) c = m ? s_cmax[i] : c;
     }
-    f_pos = a & 0xFFFFu;
-    f_fl = a >> 16;
-    f_acc = b;
+    f_pos = pe & 0xFFFFu;
+    end = pe >> 16;
+    f_hop = hf & 0xFFFFu;
+    f_fl = hf >> 16;
+    f_res = r;
+    f_acc = a;
     f_cmax = c;
-    f_hop = h;
   }
 
-  // One action: close the current invocation, or process position p.
+  // The step begin of call position p (TF_STEP: the previous concurrent step
+  // ends, the non-call time since the previous call step is added, a
+  // concurrent step starts) on copies of the frame's time and flags; returns
+  // false when the script has failed (mode B: it runs no further step).
+  ISIM_TW bool step_begin(const TreeNode &n, const TreeExt *ext, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
+    if (!(n.flags & TF_STEP)) return true;
+    if (CONC && (fl & FL_INCONC)) {
+      acc += cm;
+      if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
+      fl &= ~(FL_INCONC | FL_CERR);
+    }
+    if (MODEB && (fl & FL_FAILED)) return false;
+    acc += n.pre;
+    if (CONC && (n.flags & TF_CONC)) {
+      fl |= FL_INCONC;
+      cm = ext[p].cmax0;
+    }
+    return true;
+  }
+
+  // the skip draw of call n (its block's residues are in f_res)
+  ISIM_TW bool skipped(const TreeNode &n) const {
+    return ((f_res >> (7u * (n.k & 3u))) & 0x7Fu) < 100u - n.prob;
+  }
+
+  // close f_pos: its response folds into its caller (false: the entry responded)
   template <class Sink>
-  ISIM_TW void step(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
-#ifdef ISIM_TREE_DEBUG
-    if (sink.bad(p, f_pos, d, FRAMES)) {
+  ISIM_TW bool close(const TreeNode *nodes, const TreeExt *ext, Sink &sink) {
+    uint32_t T = f_acc, fl = f_fl;
+    if (CONC && (fl & FL_INCONC)) {
+      T += f_cmax;
+      if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
+    }
+    const TreeExt x = ext[f_pos];
+    const bool failed = MODEB && (fl & FL_FAILED);
+    if (!failed) T += x.tc;
+    const bool st = failed || (fl & FL_OWN);
+    errh += st ? 1u : 0u;
+    if (f_pos == 0) {
       done = true;
-      return;
+      lat = T;
+      root500 = st;
+      return false;
     }
-#endif
-    if (p >= end) {  // ---- close f_pos
-      uint32_t T = f_acc, fl = f_fl;
-      if (fl & FL_INCONC) {
-        T += f_cmax;
-        if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
-      }
-      const TreeExt x = ext[f_pos];
-      const bool failed = MODEB && (fl & FL_FAILED);
-      if (!failed) T += x.tc;
-      const bool st = failed || (fl & FL_OWN);
-      errh += st ? 1u : 0u;
-      if (f_pos == 0) {
-        done = true;
-        lat = T;
-        root500 = st;
-        return;
-      }
-      sink.resp(nodes[f_pos].slot, x.row, T, st);
-      const uint32_t c = x.H + T;
-      const bool cc = (fl & FL_CONC_CHILD) != 0;
-      pop();
-      end = f_pos + nodes[f_pos].size;
-      fold(c, st, cc);
-      return;
-    }
-    // ---- process the call at position p (a call command of f_pos's script)
+    sink.resp(nodes[f_pos].slot, x.row, T, st);
+    const uint32_t c = x.H + T;
+    const bool cc = (fl & FL_CONC_CHILD) != 0;
+    pop();
+    fold(c, st, cc);
+    return true;
+  }
+
+  // process call position p (p < end)
+  template <class Sink>
+  ISIM_TW void process(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
     const TreeNode n = nodes[p];
-    if (n.flags & TF_STEP) {
-      if (f_fl & FL_INCONC) {
-        f_acc += f_cmax;
-        if (MODEB && (f_fl & FL_CERR)) f_fl |= FL_FAILED;
-        f_fl &= ~(FL_INCONC | FL_CERR);
-      }
-      if (MODEB && (f_fl & FL_FAILED)) {  // the script stops: close at the subtree's end
-        p = end;
-        return;
-      }
-      f_acc += n.pre;
-      if (n.flags & TF_CONC) {
-        f_fl |= FL_INCONC;
-        f_cmax = ext[p].cmax0;
-      }
+    if (!step_begin(n, ext, f_acc, f_fl, f_cmax)) {  // mode B: the script stops, close at the subtree's end
+      p = end;
+      return;
     }
     if (n.prob) {  // shouldSkipRequest: word (k & 3) of Philox((t, caller hop, 1 + k/4, 0)) % 100 < 100 - p
-      const uint32_t blk = 1u + (n.k >> 2);
-      if (sk_hop != f_hop || sk_blk != blk) {
-        uint32_t a = t_lo, b = t_hi, c = f_hop, dd = blk;
-        philox10(a, b, c, dd, k0, k1);
-        sk0 = a;
-        sk1 = b;
-        sk2 = c;
-        sk3 = dd;
-        sk_hop = f_hop;
-        sk_blk = blk;
+      const uint32_t kb = (uint32_t)n.k >> 2;
+      if (((f_fl >> KB_SHIFT) & KB_NONE) != kb) {  // a call block past the first four calls
+        f_res = residues(f_hop, kb, k0, k1);
+        f_fl = (f_fl & ~(KB_NONE << KB_SHIFT)) | (kb << KB_SHIFT);
       }
-      if (word4(n.k & 3u, sk0, sk1, sk2, sk3) % 100u < 100u - n.prob) {
+      if (skipped(n)) {
         p += n.size;
         return;
       }
@@ -265,9 +300,42 @@ struct Lane {
     f_acc = 0;
     f_cmax = 0;
     f_hop = hop;
-    f_fl = (own ? FL_OWN : 0u) | ((n.flags & TF_CONC) ? FL_CONC_CHILD : 0u);
+    const bool pk = (n.flags & TF_PROBK0) != 0;
+    f_res = pk ? residues(hop, 0, k0, k1) : 0u;
+    f_fl = (own ? FL_OWN : 0u) | ((n.flags & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
     end = p + n.size;
     p += 1;
+  }
+
+  // pass call position p if its skip draw (already in f_res) says skip
+  ISIM_TW bool scan(const TreeNode *nodes, const TreeExt *ext) {
+    const TreeNode n = nodes[p];
+    if (!n.prob || (((f_fl >> KB_SHIFT) & KB_NONE) != ((uint32_t)n.k >> 2)) || !skipped(n)) return false;
+    uint32_t acc = f_acc, fl = f_fl, cm = f_cmax;
+    if (!step_begin(n, ext, acc, fl, cm)) return false;
+    f_acc = acc;
+    f_fl = fl;
+    f_cmax = cm;
+    p += n.size;
+    return true;
+  }
+
+  // One macro step (see above).
+  template <class Sink>
+  ISIM_TW void step(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
+#ifdef ISIM_TREE_DEBUG
+    if (sink.bad(p, f_pos, d, FRAMES)) {
+      done = true;
+      return;
+    }
+#endif
+    if (p >= end && !close(nodes, ext, sink)) return;
+    if (p < end) process(nodes, ext, sink, k0, k1);
+    bool go = true;
+#pragma unroll
+    for (int i = 0; i < kScan; ++i) {
+      go = go && p < end && scan(nodes, ext);
+    }
   }
 };
 
