@@ -903,7 +903,9 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
           const uint64_t F = val + P.floor;
           const uint32_t st = (stm >> i) & 1u;
           const uint32_t dur = w + (uint32_t)P.floor;  // F - a; exact whenever F fits
+#ifndef DES_HOIST_500
           if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
+#endif
           q.n5 += st;
           q.dsum += dur;
           q.d1 += st ? dur : 0u;
@@ -925,8 +927,11 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
         const uint32_t st = (stm >> i) & 1u;
         const uint64_t dur = w + P.floor;  // F - a
         // (per trace: hoisting these atomics under one wave-uniform test gave
-        // wrong batches with ROCm 7.2, cause not found)
+        // wrong batches with ROCm 7.2, cause not found; DES_HOIST_500 builds
+        // that variant)
+#ifndef DES_HOIST_500
         if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
+#endif
         q.n5 += st;
         q.dsum += dur;
         q.d1 += st ? dur : 0;  // a select, not a branch
@@ -940,7 +945,14 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
     }
   }
   if constexpr (FUSED) {
+#ifdef DES_HOIST_500
     // per-trace 500 counts: one wave-uniform test, the atomics only where a 500 is
+    if (!k.quiet && __ballot(stm != 0u)) {
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i)
+        if ((stm >> i) & 1u) atomicAdd(k.E + base + i, 1u);
+    }
+#endif
     hist_add4<FULL>(hist, bin);
   }
 }

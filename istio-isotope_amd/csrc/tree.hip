@@ -209,9 +209,13 @@ __global__ void __launch_bounds__(kWgThreads, 1)
         active = false;
       }
 #ifndef TREE_NO_HIST
-      hist_add(c.hist, (is500 ? ISIM_N_PROM : 0u) + prom_bucket(lat), fin);
-      const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
-      hist_add(c.hist + 2 * ISIM_N_PROM, (is500 ? ISIM_N_LOG2 : 0u) + l2, fin);
+      // the latency histograms: one LDS atomic per responding lane (their
+      // buckets mostly differ, so a wave-aggregated add would loop per bucket)
+      if (mine) {
+        lds_add(c.hist + (is500 ? ISIM_N_PROM : 0u) + prom_bucket(lat), 1u);
+        const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
+        lds_add(c.hist + 2 * ISIM_N_PROM + (is500 ? ISIM_N_LOG2 : 0u) + l2, 1u);
+      }
 #endif
     }
     // idle lanes take the next trace ids of the wave's batch, claiming batches as it runs dry
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(kWgThreads, 1)
       if (take) {
         idx = nxt + rank;
         active = true;
-        L.start(kp.trace_begin + idx, kp.seed_lo, kp.seed_hi, nodes, ext);
+        L.start(kp.trace_begin + idx);
       }
       const uint64_t took = ballot(take);
       nxt += popc(took);

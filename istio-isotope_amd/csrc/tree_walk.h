@@ -29,8 +29,10 @@
 
 #if defined(__HIPCC__)
 #define ISIM_TW __host__ __device__ __forceinline__
+#define TW_PRAGMA_UNROLL _Pragma("unroll")
 #else
 #define ISIM_TW inline
+#define TW_PRAGMA_UNROLL
 #endif
 
 namespace isim {
@@ -57,9 +59,12 @@ ISIM_TW void philox10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, ui
   asm volatile("" : "+s"(k0), "+s"(k1));  // keep the key schedule in two SGPRs
 #endif
 #if defined(TW_UNROLL)
-#pragma unroll
+TW_PRAGMA_UNROLL
 #endif
-  for (int r = 0; r < 10; ++r) {
+#ifndef TW_ROUNDS
+#define TW_ROUNDS 10  // timing experiments only: Philox4x32-10 is the semantics
+#endif
+  for (int r = 0; r < TW_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
@@ -81,7 +86,10 @@ ISIM_TW uint32_t word4(uint32_t w, uint32_t a, uint32_t b, uint32_t c, uint32_t 
 
 constexpr uint32_t KB_SHIFT = 5;  // f_fl bits 5-15: the call block whose skip residues f_res holds
 constexpr uint32_t KB_NONE = 0x7FFu;
-constexpr int kScan = 3;          // skipped calls a step may pass after its action (tree.hip: uniform trips)
+#ifndef TW_SCAN
+#define TW_SCAN 3
+#endif
+constexpr int kScan = TW_SCAN;    // skipped calls a step may pass after its action (tree.hip: uniform trips)
 
 // The four skip draws of a Philox block reduced to what shouldSkipRequest
 // compares (word % 100, 7 bits each): skip call k iff residue(k & 3) < 100 - p.
@@ -140,33 +148,21 @@ struct Lane {
     return pack_res(a, b, c, dd);
   }
 
-  // Enters the entry invocation (hop 0).  A leaf entry responds at once.
-  ISIM_TW void start(uint64_t trace, uint32_t key0, uint32_t key1, const TreeNode *nodes, const TreeExt *ext) {
+  // Starts a trace: the entry invocation (position 0, hop 0) opens in the
+  // first step, through the same code as every other open (one Philox site
+  // for skip residues per step, shared by the lanes that open and the lanes
+  // that start).
+  ISIM_TW void start(uint64_t trace) {
     t_lo = (uint32_t)trace;
     t_hi = (uint32_t)(trace >> 32);
     done = false;
-    hopn = 1;
+    hopn = 0;
     errh = 0;
     d = 0;
     ek_blk = 0xFFFFFFFFu;  // the error block belongs to the previous trace of the lane
-    const TreeNode n = nodes[0];
-    const bool own = own_error(0, n.flags, n.thr, key0, key1);
-    if (n.flags & TF_LEAF) {
-      done = true;
-      lat = ext[0].tc;
-      root500 = own;
-      errh = own ? 1u : 0u;
-      return;
-    }
-    f_pos = 0;
-    f_acc = 0;
-    f_cmax = 0;
-    f_hop = 0;
-    const bool pk = (n.flags & TF_PROBK0) != 0;
-    f_res = pk ? residues(0, 0, key0, key1) : 0u;
-    f_fl = (own ? FL_OWN : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
-    end = n.size;
-    p = 1;
+    p = 0;
+    end = 1;
+    f_fl = 0;
   }
 
   ISIM_TW void fold(uint32_t c, bool st, bool conc) {
@@ -180,7 +176,7 @@ struct Lane {
   }
 
   ISIM_TW void push() {
-#pragma unroll
+TW_PRAGMA_UNROLL
     for (int i = 0; i < FRAMES; ++i) {
       const bool m = d == (uint32_t)i;
       s_pe[i] = m ? (f_pos | (end << 16)) : s_pe[i];
@@ -195,7 +191,7 @@ struct Lane {
   ISIM_TW void pop() {
     --d;
     uint32_t pe = 0, hf = 0, r = 0, a = 0, c = 0;
-#pragma unroll
+TW_PRAGMA_UNROLL
     for (int i = 0; i < FRAMES; ++i) {
       const bool m = d == (uint32_t)i;
       pe = m ? s_pe[i] : pe;
@@ -286,16 +282,23 @@ struct Lane {
     }
     const uint32_t hop = hopn++;
     const bool own = own_error(hop, n.flags, n.thr, k0, k1);
-    sink.call(n.slot);
+    const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
+    if (!entry) sink.call(n.slot);
     if (n.flags & TF_LEAF) {
       const TreeExt x = ext[p];
       errh += own ? 1u : 0u;
+      if (entry) {
+        done = true;
+        lat = x.tc;
+        root500 = own;
+        return;
+      }
       sink.resp(n.slot, x.row, x.tc, own);
       fold(x.H + x.tc, own, (n.flags & TF_CONC) != 0);
       p += 1;
       return;
     }
-    push();
+    if (!entry) push();
     f_pos = p;
     f_acc = 0;
     f_cmax = 0;
@@ -331,8 +334,8 @@ struct Lane {
 #endif
     if (p >= end && !close(nodes, ext, sink)) return;
     if (p < end) process(nodes, ext, sink, k0, k1);
-    bool go = true;
-#pragma unroll
+    bool go = !done;
+TW_PRAGMA_UNROLL
     for (int i = 0; i < kScan; ++i) {
       go = go && p < end && scan(nodes, ext);
     }

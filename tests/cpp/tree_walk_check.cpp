@@ -101,7 +101,7 @@ int main(int argc, char **argv) {
     uint32_t lat = 0, hops = 0, errh = 0;
     bool r500 = false;
     auto run = [&](auto &L) {
-      L.start(begin + i, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), prog.tree_nodes.data(), prog.tree_ext.data());
+      L.start(begin + i);
       while (!L.done) L.step(prog.tree_nodes.data(), prog.tree_ext.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
       lat = L.lat;
       hops = L.hopn;
