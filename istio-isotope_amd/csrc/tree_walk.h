@@ -78,6 +78,39 @@ TW_PRAGMA_UNROLL
   }
 }
 
+// A TreeNode / TreeExt as ONE 16-byte load (the kernel's copies live in LDS:
+// one ds_read_b128 instead of a narrow read per field), fields unpacked by
+// shifts.  Layout: kernel_abi.h.
+struct NodeW {
+  uint32_t w0, w1, w2, w3;  // size | k << 16, prob | flags << 8 | slot << 16, thr, pre
+  ISIM_TW uint32_t size() const { return w0 & 0xFFFFu; }
+  ISIM_TW uint32_t k() const { return w0 >> 16; }
+  ISIM_TW uint32_t prob() const { return w1 & 0xFFu; }
+  ISIM_TW uint32_t flags() const { return (w1 >> 8) & 0xFFu; }
+  ISIM_TW uint32_t slot() const { return w1 >> 16; }
+  ISIM_TW uint32_t thr() const { return w2; }
+  ISIM_TW uint32_t pre() const { return w3; }
+};
+static_assert(sizeof(TreeNode) == sizeof(NodeW), "TreeNode is four words");
+ISIM_TW NodeW load_node(const TreeNode *nodes, uint32_t p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4 v = reinterpret_cast<const uint4 *>(nodes)[p];
+  return NodeW{v.x, v.y, v.z, v.w};
+#else
+  NodeW n;
+  __builtin_memcpy(&n, nodes + p, sizeof n);
+  return n;
+#endif
+}
+ISIM_TW TreeExt load_ext(const TreeExt *ext, uint32_t p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4 v = reinterpret_cast<const uint4 *>(ext)[p];
+  return TreeExt{v.x, v.y, v.z, v.w};
+#else
+  return ext[p];
+#endif
+}
+
 ISIM_TW uint32_t word4(uint32_t w, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const uint32_t lo = (w & 1u) ? b : a;
   const uint32_t hi = (w & 1u) ? d : c;
@@ -213,25 +246,25 @@ TW_PRAGMA_UNROLL
   // ends, the non-call time since the previous call step is added, a
   // concurrent step starts) on copies of the frame's time and flags; returns
   // false when the script has failed (mode B: it runs no further step).
-  ISIM_TW bool step_begin(const TreeNode &n, const TreeExt *ext, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
-    if (!(n.flags & TF_STEP)) return true;
+  ISIM_TW bool step_begin(const NodeW &n, const TreeExt *ext, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
+    if (!(n.flags() & TF_STEP)) return true;
     if (CONC && (fl & FL_INCONC)) {
       acc += cm;
       if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
       fl &= ~(FL_INCONC | FL_CERR);
     }
     if (MODEB && (fl & FL_FAILED)) return false;
-    acc += n.pre;
-    if (CONC && (n.flags & TF_CONC)) {
+    acc += n.pre();
+    if (CONC && (n.flags() & TF_CONC)) {
       fl |= FL_INCONC;
-      cm = ext[p].cmax0;
+      cm = load_ext(ext, p).cmax0;
     }
     return true;
   }
 
   // the skip draw of call n (its block's residues are in f_res)
-  ISIM_TW bool skipped(const TreeNode &n) const {
-    return ((f_res >> (7u * (n.k & 3u))) & 0x7Fu) < 100u - n.prob;
+  ISIM_TW bool skipped(const NodeW &n) const {
+    return ((f_res >> (7u * (n.k() & 3u))) & 0x7Fu) < 100u - n.prob();
   }
 
   // close f_pos: its response folds into its caller (false: the entry responded)
@@ -242,7 +275,7 @@ TW_PRAGMA_UNROLL
       T += f_cmax;
       if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
     }
-    const TreeExt x = ext[f_pos];
+    const TreeExt x = load_ext(ext, f_pos);
     const bool failed = MODEB && (fl & FL_FAILED);
     if (!failed) T += x.tc;
     const bool st = failed || (fl & FL_OWN);
@@ -253,7 +286,7 @@ TW_PRAGMA_UNROLL
       root500 = st;
       return false;
     }
-    sink.resp(nodes[f_pos].slot, x.row, T, st);
+    sink.resp(load_node(nodes, f_pos).slot(), x.row, T, st);
     const uint32_t c = x.H + T;
     const bool cc = (fl & FL_CONC_CHILD) != 0;
     pop();
@@ -264,28 +297,28 @@ TW_PRAGMA_UNROLL
   // process call position p (p < end)
   template <class Sink>
   ISIM_TW void process(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
-    const TreeNode n = nodes[p];
+    const NodeW n = load_node(nodes, p);
     if (!step_begin(n, ext, f_acc, f_fl, f_cmax)) {  // mode B: the script stops, close at the subtree's end
       p = end;
       return;
     }
-    if (n.prob) {  // shouldSkipRequest: word (k & 3) of Philox((t, caller hop, 1 + k/4, 0)) % 100 < 100 - p
-      const uint32_t kb = (uint32_t)n.k >> 2;
+    if (n.prob()) {  // shouldSkipRequest: word (k & 3) of Philox((t, caller hop, 1 + k/4, 0)) % 100 < 100 - p
+      const uint32_t kb = (uint32_t)n.k() >> 2;
       if (((f_fl >> KB_SHIFT) & KB_NONE) != kb) {  // a call block past the first four calls
         f_res = residues(f_hop, kb, k0, k1);
         f_fl = (f_fl & ~(KB_NONE << KB_SHIFT)) | (kb << KB_SHIFT);
       }
       if (skipped(n)) {
-        p += n.size;
+        p += n.size();
         return;
       }
     }
     const uint32_t hop = hopn++;
-    const bool own = own_error(hop, n.flags, n.thr, k0, k1);
+    const bool own = own_error(hop, n.flags(), n.thr(), k0, k1);
     const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
-    if (!entry) sink.call(n.slot);
-    if (n.flags & TF_LEAF) {
-      const TreeExt x = ext[p];
+    if (!entry) sink.call(n.slot());
+    if (n.flags() & TF_LEAF) {
+      const TreeExt x = load_ext(ext, p);
       errh += own ? 1u : 0u;
       if (entry) {
         done = true;
@@ -293,8 +326,8 @@ TW_PRAGMA_UNROLL
         root500 = own;
         return;
       }
-      sink.resp(n.slot, x.row, x.tc, own);
-      fold(x.H + x.tc, own, (n.flags & TF_CONC) != 0);
+      sink.resp(n.slot(), x.row, x.tc, own);
+      fold(x.H + x.tc, own, (n.flags() & TF_CONC) != 0);
       p += 1;
       return;
     }
@@ -303,23 +336,23 @@ TW_PRAGMA_UNROLL
     f_acc = 0;
     f_cmax = 0;
     f_hop = hop;
-    const bool pk = (n.flags & TF_PROBK0) != 0;
+    const bool pk = (n.flags() & TF_PROBK0) != 0;
     f_res = pk ? residues(hop, 0, k0, k1) : 0u;
-    f_fl = (own ? FL_OWN : 0u) | ((n.flags & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
-    end = p + n.size;
+    f_fl = (own ? FL_OWN : 0u) | ((n.flags() & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
+    end = p + n.size();
     p += 1;
   }
 
   // pass call position p if its skip draw (already in f_res) says skip
   ISIM_TW bool scan(const TreeNode *nodes, const TreeExt *ext) {
-    const TreeNode n = nodes[p];
-    if (!n.prob || (((f_fl >> KB_SHIFT) & KB_NONE) != ((uint32_t)n.k >> 2)) || !skipped(n)) return false;
+    const NodeW n = load_node(nodes, p);
+    if (!n.prob() || (((f_fl >> KB_SHIFT) & KB_NONE) != ((uint32_t)n.k() >> 2)) || !skipped(n)) return false;
     uint32_t acc = f_acc, fl = f_fl, cm = f_cmax;
     if (!step_begin(n, ext, acc, fl, cm)) return false;
     f_acc = acc;
     f_fl = fl;
     f_cmax = cm;
-    p += n.size;
+    p += n.size();
     return true;
   }
 
