@@ -37,8 +37,9 @@ def checker(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("twc") / "tree_walk_check")
     srcs = [os.path.join(ROOT, "tests", "cpp", "tree_walk_check.cpp")] + \
         [os.path.join(CSRC, f) for f in ("json.cpp", "gounits.cpp", "graph.cpp", "program.cpp")]
-    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs,
-                    "-o", out], check=True)
+    # ISIM_TW_CFLAGS: compile-time variants of tree_walk.h checked the same way (e.g. -DTW_SCAN=2)
+    subprocess.run(["g++", "-std=c++17", "-O2", *os.environ.get("ISIM_TW_CFLAGS", "").split(), "-I",
+                    os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", out], check=True)
     return out
 
 

@@ -2,13 +2,17 @@
 // on the CPU: 64 lanes stepping tree_walk.h's Lane in lock step with the
 // kernel's refill, counting wave iterations and Philox executions (the open
 // site runs when any lane of the wave opens a calling invocation) per 64
-// traces.  Build (g++, from the repo root):
+// traces, and which Philox sites (a call block past the fourth call, an error
+// block, the skip residues of an open) the wave runs per iteration.  Build
+// (g++, from the repo root; -DTW_... selects tree_walk.h variants):
 //   C=istio-isotope_amd/csrc; g++ -O2 -std=c++17 -I$C tools/tree_wave_sim.cpp \
 //     $C/json.cpp $C/gounits.cpp $C/graph.cpp $C/program.cpp $C/marshal.cpp -o /tmp/tree_wave_sim
 //   /tmp/tree_wave_sim graph.json [waves]
-// ("Round 3 — macro steps": config 4 at 11.1-12.5 iterations per
-// 64 traces against 25.9 for round 2's one-position steps.)
+// ("Round 3 — macro steps": config 4 at 10.4 iterations per 64
+// traces, 12.5 without the end-of-step close, 25.9 for round 2's one-position
+// steps.)
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -55,7 +59,7 @@ int main(int argc, char **argv) {
   const TreeExt *ext = prog.tree_ext.data();
   NullSink sk;
   const int waves = argc > 2 ? atoi(argv[2]) : 100, per_wave = 1024;
-  uint64_t next = 0, it = 0, execs = 0, lanes = 0, hops = 0;
+  uint64_t next = 0, it = 0, execs = 0, lanes = 0, hops = 0, siteA = 0, siteB = 0, merged = 0;
   for (int w = 0; w < waves; ++w) {
     std::vector<tw::Lane<16, true, true>> L(64);
     std::vector<bool> act(64, false);
@@ -75,18 +79,27 @@ int main(int argc, char **argv) {
       bool any = false;
       for (int l = 0; l < 64; ++l) any = any || act[l];
       if (!any) break;
-      uint32_t opening = 0;
+      uint32_t opening = 0, nA = 0, nB = 0, maxBC = 0;
       for (int l = 0; l < 64; ++l) {
         if (!act[l] || L[l].done) continue;
-        const uint32_t d0 = L[l].d;
+        const uint32_t d0 = L[l].d, eb = L[l].ek_blk, fp = L[l].f_pos, kb = L[l].f_fl >> tw::KB_SHIFT & tw::KB_NONE;
         const bool entry_step = L[l].p == 0;
         L[l].step(nodes, ext, sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-        if (L[l].d > d0 || (entry_step && !L[l].done)) ++opening;  // drew its skip residues
+        const bool C = L[l].d > d0 || (entry_step && !L[l].done);  // drew its skip residues at an open
+        const bool B = L[l].ek_blk != eb;                          // drew an error block
+        const bool A = !C && L[l].d == d0 && L[l].f_pos == fp && (L[l].f_fl >> tw::KB_SHIFT & tw::KB_NONE) != kb;
+        opening += C;
+        nA += A;
+        nB += B;
+        maxBC = std::max<uint32_t>(maxBC, (uint32_t)B + (uint32_t)C);
       }
       if (opening) {
         ++execs;
         lanes += opening;
       }
+      siteA += nA > 0;
+      siteB += nB > 0;
+      merged += maxBC;
       ++it;
     }
   }
@@ -94,5 +107,7 @@ int main(int argc, char **argv) {
   std::printf("wave iterations per 64 traces %.2f; Philox open-site executions per 64 traces %.2f (%.1f lanes each); "
               "hops per trace %.3f\n", it / n64, execs / n64, execs ? (double)lanes / execs : 0.0,
               hops / (n64 * 64));
+  std::printf("per 64 traces: block-residue site %.2f, error site %.2f, open site %.2f; error + open sites merged %.2f\n",
+              siteA / n64, siteB / n64, execs / n64, merged / n64);
   return 0;
 }
