@@ -134,22 +134,39 @@ def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
 
 
 def cpu_baseline_des(json_text: str, params, mean_ns: int, n_traces: int):
-    """The DES oracle (oracle/des_oracle.c: sequential event-driven, one core)."""
+    """The DES oracle (oracle/des_oracle.c: sequential event-driven) on every
+    host core: one DES of one arrival stream is sequential, so each thread runs
+    an independent replica of n traces with its own trace ids (the same split
+    as bench's N > 1 DES ranks, main_des); value = all threads' traces / wall
+    time.  ctypes drops the GIL for the C call."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import des as od
     from oracle import graph_ref as gr
+    from oracle.executor import OracleGraph
     from oracle.executor_py import SimGraph
     from oracle.executor_py import SimParams as OParams
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     sg = SimGraph(gr.unmarshal_service_graph(json_text))
     op = OParams(params.seed, params.hop_base_ns, params.req_ps_per_byte, params.resp_ps_per_byte,
                  params.error_mode)
+    og = OracleGraph(sg, op)
+    od.ln_table()  # the oracle's lazily built log table, built once before the threads start
     n = n_traces or 2048
+
+    def one(r):
+        return od.run(sg, op, sg.entry(), r * n, n, mean_ns, records=False, og=og)[1]
+
     t0 = time.perf_counter()
-    _, st, _ = od.run(sg, op, sg.entry(), 0, n, mean_ns, records=False)
+    with ThreadPoolExecutor(threads) as ex:
+        sts = list(ex.map(one, range(threads)))
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "traces/s", "cores": 1, "kind": "port",
-            "sample": f"{n} traces of the same DES workload (trace ids from 0, arrivals from time 0), "
-                      f"event-driven C oracle oracle/des_oracle.c (binary heap, sequential), {dt:.1f} s",
-            "hop_visits_per_s": float(st[2]) / dt}
+    hops = sum(float(st[2]) for st in sts)
+    return {"value": threads * n / dt, "unit": "traces/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} independent replicas (one per thread) x {n} traces of the same DES workload "
+                      f"(replica r: trace ids from r*{n}, arrivals from time 0), event-driven C oracle "
+                      f"oracle/des_oracle.c (binary heap, sequential per replica), {dt:.1f} s",
+            "hop_visits_per_s": hops / dt}
 
 
 def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, merge_label=""):
@@ -385,6 +402,19 @@ def merge(h, multi, stats, sptr):
         merge_stats(stats)
 
 
+def pmc_summary(name: str, batch: int, kernel: str):
+    """profiles/pmc_summary_<name>.json if it profiled this very workload:
+    the same configuration name, batch and kernel (name and template)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_summary_{name}.json")
+    try:
+        pmc = json.load(open(path))
+    except Exception:
+        return None
+    if pmc.get("config") == name and pmc.get("batch") == batch and kernel in str(pmc.get("kernel", "")):
+        return pmc
+    return None
+
+
 def kernel_name(launch) -> str:
     """The dominant kernel of a walk launch: the lane tree walk (kind 7) or
     the walk kernels (kinds 0-6)."""
@@ -462,10 +492,15 @@ def mode_b_legs(args, json_text, rank, world, dev, multi=None):
         f = h.fold(stats.cpu().numpy().view(np.uint64))
         total = steps * B * world
         assert f["n_traces"] == total
+        launch = h.launch_info(torch.cuda.current_device())
         out[key] = {"value": total / elapsed, "unit": "traces/s", "ms_per_step": elapsed * 1e3 / steps,
                     "kernel_ms": kern_ms, "steps": steps, "n_500_frac": f["n_500"] / total,
-                    "kernel_kind": h.launch_info(torch.cuda.current_device())["kernel_kind"],
+                    "kernel_kind": launch["kernel_kind"],
                     "errorRate": "U[0,1%]" if key == "mode_b" else "U[0,1e-4]"}
+        if key == "mode_b":  # the mode-B profile (tools/profile_cfg.sh c3B "--config c3 --mode B --no-mode-b")
+            pmc = pmc_summary("c3B", B, kernel_name(launch))
+            out[key]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
+            out[key]["occupancy_measured"] = pmc.get("occupancy") if pmc else None
     return out
 
 
@@ -533,17 +568,12 @@ def main():
     traffic = None
     occupancy = {"launched_waves_per_cu": launch["blocks_per_cu"] * launch["wg_threads"] // 64,
                  "peak_waves_per_cu": 32, "measured": None}
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_summary_{args.config}.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            # only a profile of the same kernel (name and template) describes this run
-            if pmc.get("config") == args.config and pmc.get("batch") == B and \
-                    kernel_name(launch) in str(pmc.get("kernel", "")):
-                traffic = pmc.get("hbm_bytes_per_launch")
-                occupancy["measured"] = pmc.get("occupancy")
-        except Exception:
-            traffic = None
+    # the PMC summary of this line's own configuration (profiles/pmc_summary_<name>.json,
+    # tools/profile_cfg.sh + tools/pmc_summary.py; c3 in mode B: "c3B")
+    pmc = pmc_summary(f"{args.config}B" if args.mode == "B" else args.config, B, kernel_name(launch))
+    if pmc:
+        traffic = pmc.get("hbm_bytes_per_launch")
+        occupancy["measured"] = pmc.get("occupancy")
 
     line = {
         # BASELINE.json's metric verbatim (the roofline fraction is the "roofline" object)
