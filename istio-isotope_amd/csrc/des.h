@@ -24,14 +24,6 @@ constexpr uint32_t kDesMaxRounds = 65536; // schedule length limit (each round i
 constexpr uint32_t kDesFlagAlways = 1u;   // errorRate 1
 constexpr uint32_t kDesFlagLeaf = 2u;     // no call step
 constexpr uint32_t kDesFlagFused = 4u;    // fast-path leaf: finished by its queue pass (no up pass)
-// Treelets (round 3): a fused leaf whose caller is a
-// non-fused position of the same pipelined segment is queued by the caller's
-// workgroup; it has no workgroup and no rows of its own.
-constexpr uint32_t kDesFlagAbsorbed = 8u;     // queued and finished by its caller's pipelined workgroup
-constexpr uint32_t kDesFlagTreelet = 16u;     // every callee absorbed: finished in its queue pass (no up pass)
-constexpr uint32_t kDesFlagHasAbsorbed = 32u; // some callees absorbed: its finish row holds their max F | status
-                                              // when the up pass starts (read, then overwritten)
-constexpr uint32_t kDesMaxAbsorb = 8;         // absorbed callees per caller
 
 // One invocation position of the unrolled tree (64 bytes, device layout).
 struct DesPos {
@@ -65,7 +57,7 @@ struct DesPosExt {
   uint32_t bk_in;      // BK row whose value + off is the arrival (kDesNone: start(parent) + off)
   uint32_t bk_last;    // BK row of the position's own last call step (kDesNone: one call step or none)
   uint32_t last_child; // index in its children list where the last call step's children start
-  uint32_t absorbed;   // absorbed callees: the LAST `absorbed` entries of its children list
+  uint32_t pad;
 };
 
 // The begin time of call step k of a position, BK[id][t]:
@@ -116,7 +108,6 @@ struct DesPlan {
   std::vector<PipeSeg> pipe;
   std::vector<uint32_t> pipe_pos;    // round order, within a round non-fused first
   std::vector<uint32_t> pipe_dep;    // per pipe_pos: the position whose start row it waits on (kDesNone: none)
-  uint32_t n_absorbed = 0, n_treelet = 0;  // treelets (kDesFlagAbsorbed / kDesFlagTreelet positions)
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 

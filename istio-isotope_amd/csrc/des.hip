@@ -464,20 +464,6 @@ __device__ __forceinline__ int64_t read_lane(int64_t v, uint32_t l) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)l);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-// wave totals by DPP (lane 63 holds them; readlane 63): row shifts then row
-// broadcasts, as wave_max_scan, for sums of non-negative values and maxima
-__device__ __forceinline__ uint64_t wave_total_add(uint64_t v) {
-  v += (uint64_t)dpp0_i64<0x111>((int64_t)v);
-  v += (uint64_t)dpp0_i64<0x112>((int64_t)v);
-  v += (uint64_t)dpp0_i64<0x114>((int64_t)v);
-  v += (uint64_t)dpp0_i64<0x118>((int64_t)v);
-  v += (uint64_t)dpp_i64<0x142, 0xA>(0, (int64_t)v);
-  v += (uint64_t)dpp_i64<0x143, 0xC>(0, (int64_t)v);
-  return (uint64_t)read_lane((int64_t)v, 63);
-}
-__device__ __forceinline__ uint64_t wave_total_max(uint64_t v) {  // v < 2^63
-  return (uint64_t)read_lane(wave_max_scan((int64_t)v), 63);
-}
 // the block's wave totals (LDS, NW <= 16): pre = max(carry, totals of the
 // waves before `wave`), carry = max(carry, all totals); both wave-uniform
 template <uint32_t NW>
@@ -1385,287 +1371,11 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   }
 }
 
-// ---- treelets: the pipelined workgroup of a caller u also
-// queues its absorbed fused-leaf callees.  Per chunk, after u's own queue:
-// u's absolute start S_u is in registers, so callee c's arrivals are
-// S_u + off_c (no A_t or start-row loads), its queue is one more running-max
-// scan (one block barrier), and its finish F_c = S_c + floor_c, status,
-// duration and waits are accumulated without writing a row: u keeps the max
-// F_c (and the OR of the statuses) per trace.  A treelet root (every callee
-// absorbed) then finishes here, F_u = max(S_u + floor_u, max F_c) + post_u;
-// otherwise that max goes to u's finish row for u's up pass.
-struct TreeAcc {  // per absorbed callee: LDS accumulators of the workgroup
-  unsigned long long wsum, wmax, d0, d1, n5;
-};
-template <typename T, bool FULL, bool HAND_IN, bool HAND_OUT, bool TREELET>
-__device__ __forceinline__ void tree_chunk(const DesK &k, const DesPos &P, uint32_t v, const T *par, uint64_t off,
-                                           T *out, T *fout, uint64_t c0, int64_t (*wtot)[2][kDownThreads / 64],
-                                           uint32_t buf, int64_t &carry, int64_t (*ccar)[kDesMaxAbsorb],
-                                           const uint32_t *ach, uint32_t acnt, uint32_t *hist, TreeAcc *acc,
-                                           const uint8_t *lut, QAcc &q, uint32_t chunk) {
-  constexpr uint32_t NW = kDownThreads / 64;
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint64_t N = k.N;
-  uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
-  __asm__ volatile("" : "+v"(base));  // opaque to loop strength reduction (down1_chunk)
-  uint64_t a[kPer];
-  T ar[kPer];
-  if constexpr (HAND_IN) {
-    load4n<uint64_t>(k.A, base, FULL ? base + kPer : N, a);
-    load_row_sc1<T, FULL>(par, c0, base, N, ar);
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)ar[i] + off;
-  } else {
-    load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
-  }
-  // ---- u's own queue (as down1_chunk, not fused)
-  int64_t key[kPer];
-  {
-    const int64_t inc = wave_max_scan(queue_keys<FULL>(a, base, N, P.hold, key));
-    const int64_t exc = wave_shr1(inc);
-    if (lane == 63) wtot[0][buf][wave] = inc;
-    if constexpr (HAND_OUT) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous chunk's stores
-    __syncthreads();
-    if constexpr (HAND_OUT)
-      if (threadIdx.x == 0 && chunk > 0) st_flag(k.prog + v, chunk);
-    int64_t pre;
-    fold_totals<NW>(wtot[0][buf], wave, carry, pre);
-    int64_t p = max_i64(pre, exc);
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      if (FULL || base + i < N) {
-        p = max_i64(p, key[i]);
-        const uint64_t w = (uint64_t)(p - key[i]);
-        q.wsum += w;
-        q.wmax = w > q.wmax ? w : q.wmax;
-        key[i] = (int64_t)(a[i] + w);  // from here on: u's absolute start S_u
-      }
-    }
-  }
-  // u's start rows (relative to A_t): a[i] - (ar + off) is A_t
-  T so[kPer];
-#pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) {
-    const uint64_t srel = (uint64_t)key[i] - (a[i] - ((uint64_t)ar[i] + off));
-    q.bad |= (FULL || base + i < N) && !Row<T>::fits(srel);
-    so[i] = (T)srel;
-  }
-  if constexpr (!TREELET) {
-    if constexpr (HAND_OUT) store_row_sc1<T, FULL>(out, c0, base, N, so);
-    else store4t<T>(out, base, FULL ? base + kPer : N, so);
-  }
-  // ---- the absorbed callees (keys recomputed per pass instead of kept: registers)
-  T mf[kPer] = {0, 0, 0, 0};
-  uint32_t stor = 0;
-#pragma unroll 1
-  for (uint32_t j = 0; j < acnt; ++j) {
-    const uint32_t c = __builtin_amdgcn_readfirstlane(ach[j]);  // wave-uniform: scalar loads of its DesPos
-    const DesPos Pc = k.pos[c];
-    int64_t kt = kKeyMin;
-    {
-      uint64_t th = base * Pc.hold;
-#pragma unroll
-      for (uint32_t i = 0; i < kPer; ++i) {
-        if (FULL || base + i < N) kt = max_i64(kt, (int64_t)((uint64_t)key[i] + Pc.off - th));
-        th += Pc.hold;
-      }
-    }
-    const int64_t inc = wave_max_scan(kt);
-    const int64_t exc = wave_shr1(inc);
-    if (lane == 63) wtot[1 + j][buf][wave] = inc;
-    __syncthreads();
-    // the callee's carry across chunks: LDS, double-buffered (read ccar[buf], written to ccar[buf ^ 1])
-    int64_t pre, cj = ccar[buf][j];
-    fold_totals<NW>(wtot[1 + j][buf], wave, cj, pre);
-    if (threadIdx.x == 0) ccar[buf ^ 1u][j] = cj;
-    int64_t p = max_i64(pre, exc);
-    const uint32_t stm = des_status4(k, c, base);
-    uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
-    uint64_t ws = 0, dsum = 0, d1 = 0, wm = 0;
-    uint32_t n5 = 0;
-    uint64_t th = base * Pc.hold;
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      if (FULL || base + i < N) {
-        const int64_t kc = (int64_t)((uint64_t)key[i] + Pc.off - th);
-        p = max_i64(p, kc);
-        const uint64_t w = (uint64_t)(p - kc);
-        const uint64_t dur = w + Pc.floor;                 // F_c - a_c
-        const uint64_t F = (uint64_t)so[i] + Pc.off + dur; // relative to A_t
-        const uint32_t st = (stm >> i) & 1u;
-        q.bad |= !Row<T>::fits(F);
-        if (st) atomicAdd(k.E + base + i, 1u);  // treelets: never in quiet (fixed-point) passes
-        ws += w;
-        wm = w > wm ? w : wm;
-        n5 += st;
-        dsum += dur;
-        d1 += st ? dur : 0;
-        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
-        mf[i] = (T)F > mf[i] ? (T)F : mf[i];
-        stor |= st << i;
-      }
-      th += Pc.hold;
-    }
-    hist_add4<FULL>(hist + (1 + j) * 2 * ISIM_N_PROM, bin);
-    ws = wave_total_add(ws);
-    dsum = wave_total_add(dsum);
-    d1 = wave_total_add(d1);
-    const uint64_t n5t = wave_total_add(n5);
-    wm = wave_total_max(wm);
-    if (lane == 0) {
-      atomicAdd(&acc[j].wsum, (unsigned long long)ws);
-      atomicMax(&acc[j].wmax, (unsigned long long)wm);
-      atomicAdd(&acc[j].d0, (unsigned long long)(dsum - d1));
-      atomicAdd(&acc[j].d1, (unsigned long long)d1);
-      atomicAdd(&acc[j].n5, (unsigned long long)n5t);
-    }
-  }
-  // ---- u's finish (treelet root) or the callees' max for u's up pass
-  T fo[kPer];
-  if constexpr (TREELET) {
-    const uint32_t stm = des_status4(k, v, base);
-    uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      fo[i] = 0;
-      if (FULL || base + i < N) {
-        const uint64_t s_fl = (uint64_t)so[i] + P.floor;
-        const uint64_t F = ((uint64_t)mf[i] > s_fl ? (uint64_t)mf[i] : s_fl) + P.post;
-        const uint32_t st = ((stm >> i) & 1u) | (k.modeb ? (stor >> i) & 1u : 0u);
-        const uint64_t dur = F - ((uint64_t)ar[i] + off);  // F - a
-        q.bad |= !Row<T>::fits(F);
-        if (st) atomicAdd(k.E + base + i, 1u);  // treelets: never in quiet (fixed-point) passes
-        q.n5 += st;
-        q.dsum += dur;
-        q.d1 += st ? dur : 0;
-        bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
-        fo[i] = (T)(F | ((uint64_t)st << Row<T>::kTop));
-      }
-    }
-    hist_add4<FULL>(hist, bin);
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) fo[i] = (T)((uint64_t)mf[i] | ((uint64_t)((stor >> i) & 1u) << Row<T>::kTop));
-  }
-  store4t<T>(fout, base, FULL ? base + kPer : N, fo);
-}
-
-template <typename T, bool HAND_IN, bool TREELET>
-__device__ __forceinline__ void tree_body(const DesK &k, uint32_t v, uint32_t dep) {
-  constexpr uint32_t NW = kDownThreads / 64;
-  constexpr bool HAND_OUT = !TREELET;  // callees not absorbed may read u's start row in this launch
-  __shared__ int64_t wtot[1 + kDesMaxAbsorb][2][NW];
-  __shared__ uint64_t red[3 * NW];
-  __shared__ uint32_t hist[(1 + kDesMaxAbsorb) * 2 * ISIM_N_PROM];
-  __shared__ TreeAcc acc[kDesMaxAbsorb];
-  __shared__ uint32_t ach[kDesMaxAbsorb];
-  __shared__ int64_t ccar[2][kDesMaxAbsorb];
-  __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
-  __shared__ uint32_t s_known;
-  const DesPos P = k.pos[v];
-  const uint32_t acnt = k.ext[v].absorbed;
-  for (uint32_t i = threadIdx.x; i < (1 + kDesMaxAbsorb) * 2 * ISIM_N_PROM; i += kDownThreads) hist[i] = 0;
-  if (threadIdx.x < kDesMaxAbsorb) {
-    acc[threadIdx.x] = TreeAcc{0, 0, 0, 0, 0};
-    ccar[0][threadIdx.x] = 0;  // callee queues start idle
-    ach[threadIdx.x] = threadIdx.x < acnt ? k.child[P.child_off + P.child_cnt - acnt + threadIdx.x] : 0u;
-  }
-  des_bucket_lut_init(lut);
-  __syncthreads();
-  const uint64_t N = k.N;
-  const T *par = arrival_row<T>(k, v, P);
-  const uint64_t off = par ? P.off : 0;
-  T *out = row<T>(k.W, k.ld, v);
-  T *fout = row<T>(k.WF, k.ld, v);
-  QAcc q;
-  int64_t carry = 0;
-  uint32_t buf = 0, known = 0, chunk = 0;
-  auto wait = [&]() {  // as pipe_body
-    if constexpr (HAND_IN) {
-      if (known <= chunk) {
-        if (threadIdx.x == 0) {
-          uint32_t pv, spins = 0;
-          while ((pv = ld_flag(k.prog + dep)) <= chunk) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {
-              atomicOr(k.ovf, 4u);
-              pv = 0xFFFFFFFFu;
-              break;
-            }
-          }
-          s_known = pv;
-        }
-        __syncthreads();
-        known = s_known;
-      }
-    }
-  };
-  constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
-  uint64_t c0 = 0;
-#pragma unroll 1
-  for (; c0 + CH <= N; c0 += CH, ++chunk) {
-    wait();
-    tree_chunk<T, true, HAND_IN, HAND_OUT, TREELET>(k, P, v, par, off, out, fout, c0, wtot, buf, carry, ccar, ach,
-                                                     acnt, hist, acc, lut, q, chunk);
-    buf ^= 1u;
-  }
-  if (c0 < N) {
-    wait();
-    tree_chunk<T, false, HAND_IN, HAND_OUT, TREELET>(k, P, v, par, off, out, fout, c0, wtot, buf, carry, ccar, ach,
-                                                      acnt, hist, acc, lut, q, chunk);
-    ++chunk;
-  }
-  if constexpr (HAND_OUT) {
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's last stores
-    __syncthreads();
-    if (threadIdx.x == 0) st_flag(k.prog + v, chunk);
-  }
-  flag_overflow(k, q.bad);
-  if (k.quiet) return;
-  __syncthreads();  // the callees' LDS accumulators are complete
-  des_flush_waits<kDownThreads>(k, P.row, q.wsum, q.max_wait(), N, N * P.hold, red);
-  if constexpr (TREELET) {
-    __syncthreads();
-    des_flush_durations<kDownThreads>(k, P, hist, q.dsum - q.d1, q.d1, q.n5, red);
-  }
-  // the absorbed callees' statistics (already reduced in LDS): one thread per
-  // (callee, histogram word), then one thread per callee for the sums
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < acnt * 2 * ISIM_N_PROM; i += kDownThreads) {
-    const uint32_t j = i / (2 * ISIM_N_PROM), w = i - j * 2 * ISIM_N_PROM;
-    const uint32_t h = hist[(1 + j) * 2 * ISIM_N_PROM + w];
-    if (h) atomicAdd((unsigned long long *)(k.table + (uint64_t)k.pos[ach[j]].row * ISIM_DES_ROW_WORDS + w),
-                     (unsigned long long)h);
-  }
-  if (threadIdx.x < acnt) {
-    const DesPos Pc = k.pos[ach[threadIdx.x]];
-    const TreeAcc a = acc[threadIdx.x];
-    unsigned long long *trow = (unsigned long long *)(k.table + (uint64_t)Pc.row * ISIM_DES_ROW_WORDS);
-    atomicAdd(trow + ISIM_DES_COUNT, (unsigned long long)N);
-    if (Pc.hold) atomicAdd(trow + ISIM_DES_SUM_HOLD, (unsigned long long)(N * Pc.hold));
-    if (a.wsum) atomicAdd(trow + ISIM_DES_SUM_WAIT, a.wsum);
-    if (a.wmax) atomicMax(trow + ISIM_DES_MAX_WAIT, a.wmax);
-    if (a.d0) atomicAdd(trow + 2 * ISIM_N_PROM, a.d0);
-    if (a.d1) atomicAdd(trow + 2 * ISIM_N_PROM + 1, a.d1);
-    if (a.n5 && Pc.slot != kSlotRoot)
-      atomicAdd((unsigned long long *)(k.stats + ISIM_ST_SITES + k.n_slots + Pc.slot), a.n5);
-  }
-}
-
 template <typename T>
 __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pipe(DesK k) {
   const uint32_t t = chain_ticket(k);
   const uint32_t v = k.level_pos[k.level_begin + t], dep = k.pipe_dep[k.level_begin + t];
-  const uint32_t fl = k.pos[v].flags;
-  if (fl & (kDesFlagTreelet | kDesFlagHasAbsorbed)) {
-    if (fl & kDesFlagTreelet) {
-      if (dep != kDesNone) tree_body<T, true, true>(k, v, dep);
-      else tree_body<T, false, true>(k, v, dep);
-    } else {
-      if (dep != kDesNone) tree_body<T, true, false>(k, v, dep);
-      else tree_body<T, false, false>(k, v, dep);
-    }
-  } else if (fl & kDesFlagFused) {
+  if (k.pos[v].flags & kDesFlagFused) {
     if (dep != kDesNone) pipe_body<T, true, true>(k, v, dep);
     else pipe_body<T, true, false>(k, v, dep);
   } else {
@@ -1694,18 +1404,16 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
                                         T *fin, const T *arow, uint64_t amask, uint64_t off, bool leaf,
                                         const T *mrow, uint32_t c_max_from, const uint32_t *ch,
                                         const uint32_t (&id0)[kUpCB<T>], uint32_t *hist, const uint8_t *lut,
-                                        uint64_t &dsum0, uint64_t &dsum1, uint64_t &n500, bool &bad,
-                                        uint32_t cnt, bool hasab) {
+                                        uint64_t &dsum0, uint64_t &dsum1, uint64_t &n500, bool &bad) {
   __asm__ volatile("" : "+v"(b0));  // opaque to loop strength reduction (down1_chunk)
   const uint64_t n = FULL ? b0 + kPer : te;
-  T ar[kPer], mr[kPer], ab[kPer];
+  const uint32_t cnt = leaf ? 0u : P.child_cnt;
+  T ar[kPer], mr[kPer];
   T f0[kUpCB<T>][kPer];
   // 1. the loads (no branch around the row loads: a branch that merges
   // loaded values makes the compiler wait for them inside it)
   load4t<T>(arow, b0, n, ar);
   load4t<T>(mrow, b0, n, mr);
-  // treelets: the absorbed callees' max F | status, left in this finish row by the queue pass
-  load4t<T>(hasab ? (const T *)fin : mrow, b0, n, ab);
   const uint32_t stm = des_status4(k, v, b0);
 #pragma unroll
   for (uint32_t j = 0; j < kUpCB<T>; ++j)
@@ -1742,14 +1450,6 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) m[i] = (uint64_t)cm[i] > m[i] ? (uint64_t)cm[i] : m[i];
-  }
-  if (hasab) {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      const uint64_t f = (uint64_t)(ab[i] & (T)Row<T>::kMask);
-      m[i] = f > m[i] ? f : m[i];
-      sto |= (uint32_t)(ab[i] >> Row<T>::kTop) << i;
-    }
   }
   uint64_t o[kPer];
   uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
@@ -1803,7 +1503,6 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
   const bool leaf = P.flags & kDesFlagLeaf;
-  const bool hasab = (P.flags & kDesFlagHasAbsorbed) != 0;
   // several call steps: F = max(BK_last + floor, max F(last step's callees)) + post
   const T *base_t = X.bk_last == kDesNone ? nullptr : row<T>(k.BK, k.ld, X.bk_last);
   const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
@@ -1817,7 +1516,7 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
   // the child positions: in LDS when they fit (read by every quad; LDS
   // addressing known to the compiler, not flat), else from global memory
   __shared__ uint32_t s_ch[kUpChildLds];
-  const uint32_t cnt = leaf ? 0u : P.child_cnt - X.absorbed;  // absorbed callees are last (des_plan.cpp)
+  const uint32_t cnt = leaf ? 0u : P.child_cnt;
   const uint32_t *gch = k.child + P.child_off;
   auto run = [&](const uint32_t *ch) {
     // the first children's positions in (uniform) registers for the whole
@@ -1828,10 +1527,10 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
     for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
       if (b0 + kPer <= te)
         up_quad<T, true>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut, dsum0,
-                         dsum1, n500, bad, cnt, hasab);
+                         dsum1, n500, bad);
       else
         up_quad<T, false>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut,
-                          dsum0, dsum1, n500, bad, cnt, hasab);
+                          dsum0, dsum1, n500, bad);
     }
   };
   if (cnt <= kUpChildLds) {

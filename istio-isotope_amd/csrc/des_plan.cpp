@@ -20,7 +20,6 @@
 #include "des.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace isim {
 namespace {
@@ -71,97 +70,6 @@ ScriptShape shape_of(const Service &s) {
 }
 
 }  // namespace
-
-// ISIM_DES_TREELET=1 (every absorbable callee) or 2 (only callers whose
-// callees are all absorbable) turns treelets on: off by default until they
-// pay (measured slower so far)
-static bool des_treelets_enabled() {
-  const char *e = std::getenv("ISIM_DES_TREELET");
-  return e && (e[0] == '1' || e[0] == '2');
-}
-// ISIM_DES_TREELET=2: only callers whose callees are all absorbed (A/B timing)
-static bool des_treelets_only() {
-  const char *e = std::getenv("ISIM_DES_TREELET");
-  return e && e[0] == '2';
-}
-// ISIM_DES_ABSORB=k (1..kDesMaxAbsorb): at most k absorbed callees per caller (A/B timing)
-static uint32_t des_absorb_cap() {
-  const char *e = std::getenv("ISIM_DES_ABSORB");
-  const long v = e ? std::strtol(e, nullptr, 10) : (long)kDesMaxAbsorb;
-  return v < 1 ? 1u : v > (long)kDesMaxAbsorb ? kDesMaxAbsorb : (uint32_t)v;
-}
-
-// Treelets: a fused leaf of a pipelined segment whose
-// caller is a non-fused position of the same segment (its arrival is the
-// caller's start row) is queued by the caller's workgroup (up to
-// kDesMaxAbsorb per caller): it leaves the segment, its caller's children list
-// ends with it, and a caller whose children are all absorbed finishes in its
-// queue pass (no up pass).  Only plans with one call step per script.
-static void absorb_treelets(DesPlan &out, const std::vector<uint32_t> &seg_of) {
-  const uint32_t np = (uint32_t)out.pos.size();
-  std::vector<uint32_t> cnt(np, 0);
-  std::vector<char> absorbed(np, 0);
-  const uint32_t cap = des_absorb_cap();
-  for (uint32_t v : out.pipe_pos) {
-    const DesPos &P = out.pos[v];
-    if (!(P.flags & kDesFlagFused) || P.parent == kDesNoParent || out.ext[v].bk_in != kDesNone) continue;
-    const uint32_t u = P.parent;
-    if ((out.pos[u].flags & (kDesFlagFused | kDesFlagLeaf)) || seg_of[u] != seg_of[v] || seg_of[u] == kDesNone ||
-        cnt[u] >= cap)
-      continue;
-    absorbed[v] = 1;
-    cnt[u] += 1;
-  }
-  if (des_treelets_only())  // callers whose callees are NOT all absorbed keep them
-    for (uint32_t v = 0; v < np; ++v)
-      if (absorbed[v] && cnt[out.pos[v].parent] != out.pos[out.pos[v].parent].child_cnt) absorbed[v] = 0;
-  if (des_treelets_only())
-    for (uint32_t u = 0; u < np; ++u)
-      if (cnt[u] != out.pos[u].child_cnt) cnt[u] = 0;
-  for (uint32_t u = 0; u < np; ++u) {
-    if (!cnt[u]) continue;
-    DesPos &P = out.pos[u];
-    // the absorbed callees last in the children list (the up pass reads the first child_cnt - absorbed)
-    std::stable_partition(out.child.begin() + P.child_off, out.child.begin() + P.child_off + P.child_cnt,
-                          [&](uint32_t c) { return !absorbed[c]; });
-    out.ext[u].absorbed = cnt[u];
-    P.flags |= cnt[u] == P.child_cnt ? kDesFlagTreelet : kDesFlagHasAbsorbed;
-    out.n_treelet += cnt[u] == P.child_cnt ? 1u : 0u;
-  }
-  for (uint32_t v = 0; v < np; ++v)
-    if (absorbed[v]) {
-      out.pos[v].flags |= kDesFlagAbsorbed;
-      out.n_absorbed += 1;
-    }
-  // the segments without the absorbed positions
-  std::vector<uint32_t> pp, pd;
-  for (DesPlan::PipeSeg &sg : out.pipe) {
-    const uint32_t off = (uint32_t)pp.size();
-    for (uint32_t i = sg.off; i < sg.off + sg.cnt; ++i)
-      if (!absorbed[out.pipe_pos[i]]) {
-        pp.push_back(out.pipe_pos[i]);
-        pd.push_back(out.pipe_dep[i]);
-      }
-    sg.off = off;
-    sg.cnt = (uint32_t)pp.size() - off;
-  }
-  out.pipe_pos.swap(pp);
-  out.pipe_dep.swap(pd);
-  // the finish groups without the treelet roots (empty groups dropped)
-  std::vector<uint32_t> fp, fo(1, 0), fro(out.fin_round_off.size(), 0);
-  for (size_t r = 0; r + 1 < out.fin_round_off.size(); ++r) {
-    for (uint32_t gi = out.fin_round_off[r]; gi < out.fin_round_off[r + 1]; ++gi) {
-      const size_t before = fp.size();
-      for (uint32_t i = out.fin_off[gi]; i < out.fin_off[gi + 1]; ++i)
-        if (!(out.pos[out.fin_pos[i]].flags & kDesFlagTreelet)) fp.push_back(out.fin_pos[i]);
-      if (fp.size() != before) fo.push_back((uint32_t)fp.size());
-    }
-    fro[r + 1] = (uint32_t)fo.size() - 1;
-  }
-  out.fin_pos.swap(fp);
-  out.fin_off.swap(fo);
-  out.fin_round_off.swap(fro);
-}
 
 int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err) {
   out = DesPlan();
@@ -551,7 +459,6 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     }
     r = e;
   }
-  if (des_treelets_enabled() && !out.general && !out.cyclic) absorb_treelets(out, seg_of);
   out.slot_mult = p.stream_mult;
   return ISIM_OK;
 }

@@ -411,18 +411,3 @@ def test_cyclic_mode_b_and_wide(gpu):
     r2, s2, t2 = c.d.serve(7, 3000, wide=True)
     assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(t1, t2)
 
-
-@pytest.mark.parametrize("treelet", ["1", "2"])
-def test_treelets(gpu, monkeypatch, treelet):
-    """Treelets (off by default: ISIM_DES_TREELET, read when
-    the plan is built): callers queue their fused-leaf callees themselves —
-    the same records, stats and DES table as the oracle, on a concurrent
-    realistic graph (contended queues, both modes), a ragged batch and the
-    config-5 graph."""
-    monkeypatch.setenv("ISIM_DES_TREELET", treelet)
-    for mode in (isim.MODE_A, isim.MODE_B):
-        c = DesCase(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.05)), 300_000,
-                    error_mode=mode)
-        c.compare(3, 5000)
-    DesCase(_sleepy_tree(3, 4), 700_000).compare(1 << 33, 8193)
-    DesCase(config3_topology(), 6_000_000).compare(0, 2048)

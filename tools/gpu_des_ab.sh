@@ -1,15 +1,15 @@
 #!/bin/bash
-# DES treelets: DES parity suite (TESTS=0 skips it), then
-# config-5 timing of "label:library:ENV=value,..." runs, REPS times:
-#   RUNS="prev:libisim_prev.so: on:libisim.so:ISIM_DES_TREELET=1 off:libisim.so:ISIM_DES_TREELET=0" \
-#     bash tools/gpu_des_tree.sh
+# DES variants: DES parity suite (TESTS=0 skips it), then config-5 timing of
+# "label:library:ENV=value,..." runs, REPS times (the round-3 treelet A/B,
+# DESIGN.md §10.7, ran as RUNS="prev:libisim_prev.so: on:libisim.so:ISIM_DES_TREELET=1 ..."):
+#   RUNS="prev:libisim_prev.so: new:libisim.so:" bash tools/gpu_des_ab.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/dest
 O=gpurun_out/dest
 if [ "${TESTS:-1}" = 1 ]; then
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_des_gpu.py tests/test_golden_records_gpu.py -m gpu > $O/tests.log 2>&1 && echo "DES tests: $(tail -1 $O/tests.log)" || { echo "DES TESTS FAIL"; grep -E "FAILED|Error|assert" $O/tests.log | head -20; tail -5 $O/tests.log; exit 9; }
 fi
-RUNS=${RUNS:-"prev:libisim_prev.so: on:libisim.so:ISIM_DES_TREELET=1 off:libisim.so:ISIM_DES_TREELET=0"}
+RUNS=${RUNS:-"prev:libisim_prev.so: new:libisim.so:"}
 for rep in $(seq ${REPS:-2}); do
 for r in $RUNS; do
   IFS=: read label lib envs <<< "$r"
