@@ -347,7 +347,8 @@ def make_multi(rank, world, local):
     from isim.dist import Multi
     if world == 1:
         return None, "none (1 rank)"
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # the agreement all-reduces run on the process group's own device kind
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
 
     def agree(ok: bool) -> bool:
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)

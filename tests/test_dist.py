@@ -121,3 +121,64 @@ def test_shard_ranges_partition():
     ids = sorted(i for s in range(steps) for r in range(world)
                  for i in range(shard_begin(r, world, s, batch), shard_begin(r, world, s, batch) + batch))
     assert ids == list(range(world * steps * batch))
+
+
+def _make_multi_worker(rank, world, port, scenario, q):
+    """bench.make_multi's collective choice with a stand-in for isim.dist.Multi
+    (no RCCL on a CPU): every rank must come out with the same decision."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "istio-isotope_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import isim.dist
+
+    class FakeMulti:
+        closed = False
+
+        @staticmethod
+        def get_id():
+            if scenario == "id_fails_on_1" and rank == 1:
+                raise RuntimeError("no RCCL here")
+            return bytes(128)
+
+        @staticmethod
+        def init_rank(mid, w, r, local):
+            if scenario == "init_fails_on_0" and r == 0:
+                raise RuntimeError("ncclCommInitRank")
+            return FakeMulti()
+
+        def close(self):
+            FakeMulti.closed = True
+
+    isim.dist.Multi = FakeMulti
+    multi, label = bench.make_multi(rank, world, rank)
+    q.put((rank, multi is not None, label, FakeMulti.closed))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scenario", ["ok", "id_fails_on_1", "init_fails_on_0"])
+def test_make_multi_is_collective(scenario):
+    """a local failure on one rank (loading RCCL / drawing the
+    id, or creating the communicator) sends EVERY rank to the torch.distributed
+    merge, and a rank that did create a communicator frees it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_make_multi_worker, args=(r, world, port, scenario, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    uses = {g[1] for g in got}
+    assert len(uses) == 1, got  # one decision for all ranks
+    if scenario == "ok":
+        assert uses == {True} and all("libisim RCCL" in g[2] for g in got)
+    else:
+        assert uses == {False} and all(g[2].startswith("torch.distributed") for g in got)
+    if scenario == "init_fails_on_0":
+        assert got[1][3]  # rank 1 had a communicator: closed
