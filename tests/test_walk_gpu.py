@@ -294,3 +294,26 @@ def test_site_counter_beyond_u32(gpu):
     assert int(f["svc_calls"][depth]) == n * leaf and int(f["svc_errs"][depth]) == n * leaf
     assert n * leaf > 1 << 32
     assert int(f["svc_errs"][:depth].sum()) == 0 and int(f["svc_calls"][0]) == n
+
+
+def test_tree_row_counter_split(gpu):
+    """ADVICE round 2 (kind 7): a service whose per-service duration row keeps
+    an LDS bucket table (its duration varies: it calls a 10 ms service with
+    probability 50) is reached from 1,600 positions through four callers (one
+    concurrent step of 400 calls each, probability 99), so
+    one workgroup's u32 bucket counter of that row can take 1,600 counts per
+    trace, more than any one call site (400).  The launch split must follow
+    the row (Program::tree_mult takes the row's positions):
+    max_launch_traces = (2^32 - 1) // 1600.  A batch is then bit-exact
+    against the oracle."""
+    svcs = [{"name": "e", "isEntrypoint": True, "script": [{"call": f"m{i}"} for i in range(4)]}]
+    for i in range(4):
+        # one concurrent step of 400 calls (the latency bound stays below 2^32 ns: kind 7)
+        svcs.append({"name": f"m{i}", "script": [[{"call": {"service": "x", "probability": 99}}] * 400]})
+    svcs.append({"name": "x", "script": [{"call": {"service": "y", "probability": 50}}]})
+    svcs.append({"name": "y", "script": [{"sleep": "10ms"}]})
+    c = Case(json.dumps({"services": svcs}), None, isim.SimParams())
+    info = c.handler.launch_info(0)
+    assert info["kernel_kind"] == 7 and info["lds_counters"] == 1
+    assert info["max_launch_traces"] == 0xFFFFFFFF // 1600
+    c.compare(5, 300)
