@@ -24,6 +24,19 @@ constexpr uint32_t kDesMaxRounds = 65536; // schedule length limit (each round i
 constexpr uint32_t kDesFlagAlways = 1u;   // errorRate 1
 constexpr uint32_t kDesFlagLeaf = 2u;     // no call step
 constexpr uint32_t kDesFlagFused = 4u;    // fast-path leaf: finished by its queue pass (no up pass)
+// non-fused position whose invocation durations its caller's up block records
+// (round 3, des.hip des_up: the caller holds S(caller) + off, the arrival, so
+// this position's block reads no arrival row); its index among the caller's
+// such children in bits kDesDurShift.. of the flags
+constexpr uint32_t kDesFlagParentDur = 8u;
+constexpr uint32_t kDesDurShift = 8;
+constexpr uint32_t kDesDurKids = 8;       // per caller
+constexpr uint32_t kDesUpChildLds = 1024; // callers with more children record none (their ids are not staged in LDS)
+// non-fused position whose finish needs no start row: one call step, no step
+// begins, and every callee's hop cost at least the step's longest sleep, so
+// F(c) >= a(c) = S + pre + H(c) >= S + floor for each callee c and
+// F = max_c F(c) + post (des_up reads S only for callee durations)
+constexpr uint32_t kDesFlagNoStart = 16u;
 
 // One invocation position of the unrolled tree (64 bytes, device layout).
 struct DesPos {
@@ -108,6 +121,9 @@ struct DesPlan {
   std::vector<PipeSeg> pipe;
   std::vector<uint32_t> pipe_pos;    // round order, within a round non-fused first
   std::vector<uint32_t> pipe_dep;    // per pipe_pos: the position whose start row it waits on (kDesNone: none)
+  // every pipelined position's holds and offsets fit the 32-bit queue keys
+  // (des.hip down1_chunk_n32: hold < 2^25, off and a leaf's floor < 2^30)
+  bool pipe_n32 = false;
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 

@@ -18,20 +18,25 @@
 //   finalize   latency F(entry), records and the stats header.
 //
 // Rows W[position][trace] (and the step-begin rows BK) hold times RELATIVE to
-// the trace's arrival A_t: every value of trace t lies in [0, latency_t].
-// Narrow rows are u32 (status in bit 31), so a batch whose latencies stay
-// below 2^31 ns (2.1 s) moves 4 B per value; a value that does not fit sets
+// the arrival of the trace's GROUP, G_t = A[t & ~63] (64 consecutive traces,
+// round 3): every value of trace t lies in [A_t - G_t, A_t - G_t + latency_t].
+// A queue scan then needs no per-trace arrival time (its keys are G + row +
+// off - t hold, the wave's groups' bases are 4 scalars), and within one wave
+// the keys relative to the wave's first key fit 32 bits (down1_chunk_n32).
+// Narrow rows are u32 (status in bit 31), so a batch whose latencies plus 63
+// inter-arrival gaps stay below 2^31 ns (2.1 s) moves 4 B per value; a value that does not fit sets
 // the overflow flag, the batch's statistics (staged in the workspace) are
 // then dropped and ISIM_ST_DES_RETRY counts it, to be rerun with u64 rows
 // (ISIM_DES_FLAG_WIDE; isim_serve_des does that itself).  Bytes per
-// (position, trace), narrow: queue pass 4 R + 4 W (+ A_t from L2), up pass
-// 4 R (S) + 4 R (arrival row) + 4 R per child + 4 W.
+// (position, trace), narrow: queue pass 4 R + 4 W, up pass 4 R (S) + 4 R
+// (arrival row) + 4 R per child + 4 W.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "des.h"
@@ -338,10 +343,14 @@ __device__ __forceinline__ void flag_overflow(const DesK &k, bool bad) {
   if (bad) atomicOr(k.ovf, 1u);
 }
 
+// the time every row value of trace t is relative to: its group's first arrival
+constexpr uint64_t kDesGrp = 64;
+__device__ __forceinline__ uint64_t des_gbase(const DesK &k, uint64_t t) { return k.A[t & ~(kDesGrp - 1)]; }
+
 // relative arrival of position v (pp = pos[v]) for trace t
 template <typename T>
 __device__ __forceinline__ uint64_t des_arrival(const DesK &k, uint32_t v, const DesPos &pp, uint64_t t) {
-  if (pp.parent == kDesNoParent) return 0;
+  if (pp.parent == kDesNoParent) return k.A[t] - des_gbase(k, t);
   const uint32_t b = k.ext[v].bk_in;
   const T *r = b == kDesNone ? row<T>(k.W, k.ld, pp.parent) : row<T>(k.BK, k.ld, b);
   return (uint64_t)r[t] + pp.off;
@@ -962,21 +971,30 @@ __device__ __forceinline__ void queue_finish1(const DesK &k, const DesPos &P, ui
   }
 }
 
-// this thread's 4 traces: absolute arrivals a = A_t + relative arrival, and
-// the relative arrivals' row values r (S relative = wait + r + off)
+// this thread's 4 traces (one group: base % 4 == 0): absolute arrivals a =
+// G + relative arrival, and the relative arrivals' row values r (S relative
+// = wait + r + off); the entry's relative arrival is A_t - G.  Returns true
+// when an entry value does not fit the row type (the batch is redone wide).
 template <typename T, bool FULL = false>
-__device__ __forceinline__ void load_arrivals(const DesK &k, const T *par, uint64_t off, uint64_t base,
+__device__ __forceinline__ bool load_arrivals(const DesK &k, const T *par, uint64_t off, uint64_t base,
                                               uint64_t N, uint64_t (&a)[kPer], T (&r)[kPer]) {
   const uint64_t n = FULL ? base + kPer : N;  // whole: one vector access each
-  load4n<uint64_t>(k.A, base, n, a);
+  const uint64_t g = FULL || base < N ? des_gbase(k, base) : 0;
   if (par) {
     load4t<T>(par, base, n, r);
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)r[i] + off;
-  } else {
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) r[i] = 0;
+    for (uint32_t i = 0; i < kPer; ++i) a[i] = g + (uint64_t)r[i] + off;
+    return false;
   }
+  load4n<uint64_t>(k.A, base, n, a);
+  bool bad = false;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint64_t d = FULL || base + i < N ? a[i] - g : 0;
+    r[i] = (T)d;
+    bad |= !Row<T>::fits(d);
+  }
+  return bad;
 }
 
 // ---- queue pass, one workgroup per position (wide groups; replicated
@@ -1003,12 +1021,12 @@ __device__ __forceinline__ void down1_chunk(const DesK &k, const DesPos &P, uint
   uint64_t a[kPer];
   T ar[kPer];
   if constexpr (HAND_IN) {
-    load4n<uint64_t>(k.A, base, FULL ? base + kPer : N, a);
+    const uint64_t g = FULL || base < N ? des_gbase(k, base) : 0;
     load_row_sc1<T, FULL>(par, c0, base, N, ar);
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) a[i] += (uint64_t)ar[i] + off;
+    for (uint32_t i = 0; i < kPer; ++i) a[i] = g + (uint64_t)ar[i] + off;
   } else {
-    load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
+    q.bad |= load_arrivals<T, FULL>(k, par, off, base, N, a, ar);
   }
   const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
   int64_t key[kPer];
@@ -1030,6 +1048,152 @@ __device__ __forceinline__ void down1_chunk(const DesK &k, const DesPos &P, uint
   } else {
     store4t<T>(out, base, FULL ? base + kPer : N, o);
   }
+}
+
+// ---- 32-bit queue keys (round 3; narrow rows, whole chunks, every position
+// but the entry).  A wave's 256 traces are 4 groups of 64, one DPP row (16
+// lanes x 4 traces) each.  With x_t = row + off the group-relative arrival
+// and the group's base kb = G - t_g h (G its first arrival, t_g its first
+// trace), the keys relative to kb,
+//   key_t - kb = x_t - (t - t_g) h,
+// lie in (-64 h, x_t]: 32-bit whenever x_t < 2^31 (a larger one overflows
+// the start row anyway: the batch is redone wide) and 64 h < 2^31 (the
+// caller's check).  A row scan by DPP gives each trace its prefix within the
+// group; the group totals (64-bit absolute) combine across the wave's rows
+// by two row broadcasts, across the waves through LDS (fold_totals) and
+// across chunks in the carry.  A prefix below every key is clamped to
+// INT32_MIN (exact: keys exceed -2^31); one at or above 2^31 puts the
+// group's first start at or above 2^31 (a row overflow: the batch is redone).
+__device__ __forceinline__ int32_t max_i32(int32_t a, int32_t b) { return a > b ? a : b; }
+template <int CTRL>
+__device__ __forceinline__ int32_t dpp_max32(int32_t v) {
+  return max_i32(v, __builtin_amdgcn_update_dpp((int)INT32_MIN, v, CTRL, 0xF, 0xF, false));
+}
+// inclusive max-scan within each DPP row (INT32_MIN where a source lane does not exist)
+__device__ __forceinline__ int32_t row_max_scan32(int32_t v) {
+  v = dpp_max32<0x111>(v);  // row_shr:1
+  v = dpp_max32<0x112>(v);  // row_shr:2
+  v = dpp_max32<0x114>(v);  // row_shr:4
+  v = dpp_max32<0x118>(v);  // row_shr:8
+  return v;
+}
+
+// the finish of one thread's 4 traces with 32-bit keys from the prefix p
+// (FULL: all below N; else the traces past N are left out)
+template <bool FUSED, bool FULL = true>
+__device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, int32_t p, const int32_t (&key)[kPer],
+                                                 const uint32_t (&x)[kPer], uint32_t floor32, uint32_t stm,
+                                                 uint32_t (&out)[kPer], uint32_t *hist, const uint8_t *lut, QAcc &q) {
+  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin}, big = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    out[i] = 0;
+    if (!FULL && base + i >= k.N) continue;
+    p = max_i32(p, key[i]);
+    const uint32_t w = (uint32_t)p - (uint32_t)key[i];  // the wait S - a (< 2^32: exact)
+    q.wsum += w;
+    q.wmax32 = w > q.wmax32 ? w : q.wmax32;
+    uint32_t val = w + x[i];  // S - G (no wrap unless the batch is redone)
+    big |= w | val;           // a wait or start at or above 2^31: redone with 64-bit rows
+    if constexpr (FUSED) {
+      const uint32_t F = val + floor32;
+      const uint32_t st = (stm >> i) & 1u;
+      const uint32_t dur = w + floor32;  // F - a
+      if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
+      q.n5 += st;
+      q.dsum += dur;
+      q.d1 += st ? dur : 0u;
+      bin[i] = st * ISIM_N_PROM + des_prom_bucket32(lut, dur);
+      big |= F;
+      val = F | (st << 31);
+    }
+    out[i] = val;
+  }
+  q.bad |= (big >> 31) != 0u;
+  if constexpr (FUSED) hist_add4<FULL>(hist, bin);
+}
+
+// down1_chunk for narrow rows (FULL: a whole chunk; ENTRY: the entry, whose
+// group-relative arrival is A_t - G; else the caller's row `par`); `jh0` =
+// (t - t_g) h of the thread's first trace (the caller's per-position
+// constant).  The same results as down1_chunk<uint32_t, FUSED, FULL, ...>.
+template <bool FUSED, bool HAND_IN, bool HAND_OUT, bool FULL = true, bool ENTRY = false>
+__device__ __forceinline__ void down1_chunk_n32(const DesK &k, const DesPos &P, uint32_t v, const uint32_t *par,
+                                                uint32_t *out, uint64_t c0, int64_t *wtot, int64_t &carry,
+                                                uint32_t *hist, const uint8_t *lut, QAcc &q, uint32_t chunk,
+                                                uint32_t jh0) {
+  constexpr uint32_t NW = kDownThreads / 64;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t N = k.N;
+  uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+  __asm__ volatile("" : "+v"(base));  // (down1_chunk)
+  const uint64_t n = FULL ? base + kPer : N;
+  const uint64_t tg = base & ~(kDesGrp - 1);
+  const uint64_t g = FULL || tg < N ? k.A[tg] : 0;  // every lane of a group with a trace below N
+  uint32_t x[kPer], xo = 0;
+  if constexpr (ENTRY) {
+    uint64_t at[kPer];
+    load4n<uint64_t>(k.A, base, n, at);
+    uint64_t d = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      const uint64_t r = FULL || base + i < N ? at[i] - g : 0;
+      d |= r;
+      x[i] = (uint32_t)r;
+    }
+    q.bad |= (d >> 31) != 0;
+  } else {
+    uint32_t ar[kPer];
+    if constexpr (HAND_IN) load_row_sc1<uint32_t, FULL>(par, c0, base, N, ar);
+    else load4t<uint32_t>(par, base, n, ar);
+    const uint32_t off32 = (uint32_t)P.off;
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) x[i] = ar[i] + off32;
+  }
+  const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
+  const uint32_t hold32 = (uint32_t)P.hold;
+  int32_t key[kPer], kt = INT32_MIN;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    xo |= x[i];
+    key[i] = FULL || base + i < N ? (int32_t)(x[i] - (jh0 + i * hold32)) : INT32_MIN;
+    kt = max_i32(kt, key[i]);
+  }
+  q.bad |= (xo >> 31) != 0u;  // an arrival at or above 2^31: its start row overflows
+  const int32_t inc = row_max_scan32(kt);
+  const int32_t exc = __builtin_amdgcn_update_dpp((int)INT32_MIN, inc, 0x111, 0xF, 0xF, false);  // row_shr:1
+  // the group totals, absolute, at lane 15 of each row; their inclusive prefix
+  // over the wave's rows at lanes 15/31/47/63, and each row's exclusive one
+  // (a group past N: kb = -t_g h, its total INT32_MIN relative — below any key)
+  const int64_t kb = (int64_t)(g - tg * P.hold);
+  int64_t s = kb + (int64_t)inc;
+  s = max_i64(s, dpp_i64<0x142, 0xA>(s, s));  // row_bcast:15 into rows 1, 3
+  s = max_i64(s, dpp_i64<0x143, 0xC>(s, s));  // row_bcast:31 into rows 2, 3
+  int64_t e = dpp_i64<0x142, 0xA>(kKeyMin, s);  // rows 1, 3: lane 15 / 47
+  e = dpp_i64<0x143, 0x4>(e, s);                // row 2: lane 31
+  if (lane == 63) wtot[wave] = max_i64(0, s);
+  if constexpr (HAND_OUT) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous chunk's stores
+  __syncthreads();
+  if constexpr (HAND_OUT)
+    if (threadIdx.x == 0 && chunk > 0) st_flag(k.prog + v, chunk);
+  int64_t pre;
+  fold_totals<NW>(wtot, wave, carry, pre);
+  const int64_t pr = max_i64(pre, e) - kb;  // the group's prefix, relative
+  q.bad |= (FULL || base < N) && pr > (int64_t)INT32_MAX;
+  const int32_t p0 = pr < (int64_t)INT32_MIN ? INT32_MIN : pr > (int64_t)INT32_MAX ? INT32_MAX : (int32_t)pr;
+  uint32_t o[kPer];
+  queue_finish_n32<FUSED, FULL>(k, base, max_i32(p0, exc), key, x, (uint32_t)P.floor, stm, o, hist, lut, q);
+  if constexpr (FUSED) track4<uint32_t>(k, out, base, N, o);  // a fused leaf's row is final (F)
+  if constexpr (HAND_OUT) store_row_sc1<uint32_t, FULL>(out, c0, base, N, o);
+  else store4t<uint32_t>(out, base, n, o);
+}
+
+// whether a position's whole chunks take the 32-bit keys, and the thread's (t - t_g) h
+template <typename T, bool FUSED>
+__device__ __forceinline__ bool n32_ok(const DesPos &P, const void *par, uint32_t &jh0) {
+  jh0 = (threadIdx.x & 15u) * kPer * (uint32_t)P.hold;
+  return sizeof(T) == 4 && par != nullptr && P.hold < (1ull << 25) && P.off < (1ull << 30) &&
+         (!FUSED || P.floor < (1ull << 30));
 }
 
 template <typename T, bool FUSED>
@@ -1054,6 +1218,16 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   uint32_t buf = 0;
   constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
   uint64_t c0 = 0;
+  uint32_t jh0;
+  if (n32_ok<T, FUSED>(P, par, jh0)) {
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll 1
+      for (; c0 + CH <= N; c0 += CH) {
+        down1_chunk_n32<FUSED, false, false>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q, 0, jh0);
+        buf ^= 1u;
+      }
+    }
+  }
 #pragma unroll 1
   for (; c0 + CH <= N; c0 += CH) {
     down1_chunk<T, FUSED, true>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q);
@@ -1097,7 +1271,7 @@ __device__ __forceinline__ void downr_body(const DesK &k, uint32_t v) {
     uint64_t a[kPer];
     T o[kPer] = {0, 0, 0, 0};
     T ar[kPer];
-    load_arrivals<T>(k, par, off, base, N, a, ar);
+    bad |= load_arrivals<T>(k, par, off, base, N, a, ar);
     uint32_t rr[kPer];
     const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;  // fused leaves: own error statuses, bit i
 #pragma unroll
@@ -1208,7 +1382,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   const uint64_t base = (uint64_t)chunk * kDownChunk + (uint64_t)threadIdx.x * kPer;
   uint64_t a[kPer];
   T ar[kPer];
-  load_arrivals<T>(k, par, off, base, N, a, ar);
+  const bool in_bad = load_arrivals<T>(k, par, off, base, N, a, ar);
   const uint32_t stm = FUSED && base < N ? des_status4(k, v, base) : 0u;
   int64_t key[kPer];
   const int64_t inc = wave_max_scan(queue_keys<false>(a, base, N, P.hold, key));
@@ -1268,6 +1442,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
   fold_totals<NW>(wtot, wave, cin, pre);
   T o[kPer] = {0, 0, 0, 0};
   QAcc q;
+  q.bad = in_bad;
   queue_finish1<T, FUSED, false>(k, P, base, N, max_i64(pre, exc), key, ar, off, stm, o, hist, lut, q);
   if constexpr (FUSED) track4<T>(k, out, base, N, o);  // a fused leaf's row is final (F)
   store4t<T>(out, base, N, o);
@@ -1300,7 +1475,10 @@ __global__ void __launch_bounds__(kDesThreads, 8) des_down_chain_mix(DesK k) {
 // waits chunk by chunk for the caller to publish them (the caller's ticket is
 // earlier, so it is resident and progressing): no level boundaries, no tail
 // of one level in front of the next.
-template <typename T, bool FUSED, bool HAND_IN>
+// N32: every chunk takes the 32-bit keys (narrow rows; the host checked the
+// segment's holds and offsets, DesPlan::pipe_n32): the launch holds no 64-bit
+// key code, so it runs at more waves per SIMD
+template <typename T, bool FUSED, bool HAND_IN, bool N32 = false>
 __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t dep) {
   constexpr uint32_t NW = kDownThreads / 64;
   constexpr bool HAND_OUT = !FUSED;  // non-leaves: their callees may read the start row in this launch
@@ -1346,16 +1524,49 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   };
   constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
   uint64_t c0 = 0;
+  if constexpr (N32 && sizeof(T) == 4) {
+    const uint32_t jh0 = (threadIdx.x & 15u) * kPer * (uint32_t)P.hold;
+    auto chunks = [&](auto entry_t) {
+      constexpr bool ENTRY = decltype(entry_t)::value;
 #pragma unroll 1
-  for (; c0 + CH <= N; c0 += CH, ++chunk) {
-    wait();
-    down1_chunk<T, FUSED, true, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
-    buf ^= 1u;
-  }
-  if (c0 < N) {
-    wait();
-    down1_chunk<T, FUSED, false, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
-    ++chunk;
+      for (; c0 + CH <= N; c0 += CH, ++chunk) {
+        wait();
+        down1_chunk_n32<FUSED, HAND_IN, HAND_OUT, true, ENTRY>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q,
+                                                               chunk, jh0);
+        buf ^= 1u;
+      }
+      if (c0 < N) {
+        wait();
+        down1_chunk_n32<FUSED, HAND_IN, HAND_OUT, false, ENTRY>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q,
+                                                                chunk, jh0);
+        ++chunk;
+      }
+    };
+    if (par) chunks(std::false_type{});
+    else chunks(std::true_type{});
+  } else {
+    uint32_t jh0;
+    if (n32_ok<T, FUSED>(P, par, jh0)) {
+      if constexpr (sizeof(T) == 4) {
+#pragma unroll 1
+        for (; c0 + CH <= N; c0 += CH, ++chunk) {
+          wait();
+          down1_chunk_n32<FUSED, HAND_IN, HAND_OUT>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q, chunk, jh0);
+          buf ^= 1u;
+        }
+      }
+    }
+#pragma unroll 1
+    for (; c0 + CH <= N; c0 += CH, ++chunk) {
+      wait();
+      down1_chunk<T, FUSED, true, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
+      buf ^= 1u;
+    }
+    if (c0 < N) {
+      wait();
+      down1_chunk<T, FUSED, false, HAND_IN, HAND_OUT>(k, P, v, par, off, out, c0, wtot[buf], carry, hist, lut, q, chunk);
+      ++chunk;
+    }
   }
   if constexpr (HAND_OUT) {
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's last stores
@@ -1371,16 +1582,20 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pipe(DesK k) {
+#ifndef ISIM_DES_PIPE32_WAVES
+#define ISIM_DES_PIPE32_WAVES 6  // waves per SIMD of the 32-bit-key pipelined pass
+#endif
+template <typename T, bool N32>
+__global__ void __launch_bounds__(kDownThreads, N32 ? ISIM_DES_PIPE32_WAVES : ISIM_DES_DOWN_WAVES)
+    des_down_pipe(DesK k) {
   const uint32_t t = chain_ticket(k);
   const uint32_t v = k.level_pos[k.level_begin + t], dep = k.pipe_dep[k.level_begin + t];
   if (k.pos[v].flags & kDesFlagFused) {
-    if (dep != kDesNone) pipe_body<T, true, true>(k, v, dep);
-    else pipe_body<T, true, false>(k, v, dep);
+    if (dep != kDesNone) pipe_body<T, true, true, N32>(k, v, dep);
+    else pipe_body<T, true, false, N32>(k, v, dep);
   } else {
-    if (dep != kDesNone) pipe_body<T, false, true>(k, v, dep);
-    else pipe_body<T, false, false>(k, v, dep);
+    if (dep != kDesNone) pipe_body<T, false, true, N32>(k, v, dep);
+    else pipe_body<T, false, false, N32>(k, v, dep);
   }
 }
 
@@ -1398,12 +1613,31 @@ __global__ void __launch_bounds__(kDownThreads, ISIM_DES_DOWN_WAVES) des_down_pi
 #endif
 template <typename T>
 constexpr uint32_t kUpCB = sizeof(T) == 4 ? ISIM_DES_UP_CB : 2;  // children rows in flight with the rest
-constexpr uint32_t kUpChildLds = 1024;  // child ids staged in LDS per workgroup
-template <typename T, bool FULL>
+constexpr uint32_t kUpChildLds = kDesUpChildLds;  // child ids staged in LDS per workgroup
+// Per-block state of the durations a caller records for its flagged callees
+// (kDesFlagParentDur): per callee (index j < kDesDurKids) the histogram, the
+// start sum S(caller) over the traces where the callee responded 500 and
+// their count; the callee's own block adds its finish sums by status, the
+// caller's subtracts the arrivals S(caller) + off (Σ over all its traces: ss).
+struct UpKids {
+  uint32_t nd;                // flagged callees
+  const uint32_t *dch;        // [j]: the callee's position
+  const uint64_t *doff;       // [j]: the callee's off
+  uint32_t *dhist;            // [j][2 * ISIM_N_PROM]
+  unsigned long long *ds5;    // [j]
+  uint32_t *dn5;              // [j]
+};
+
+// OWN: the block records its position's durations (its arrival row is read);
+// else they are 0 (the entry: des_finalize) or its caller's (PDUR sums: the
+// finishes by status).  DK: the block records its flagged callees' durations.
+// NS: the finish needs no start row (kDesFlagNoStart, no callee durations here)
+template <typename T, bool FULL, bool OWN, bool DK, bool NS = false>
 __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t v, uint64_t b0, uint64_t te,
-                                        T *fin, const T *arow, uint64_t amask, uint64_t off, bool leaf,
+                                        T *fin, const T *arow, uint64_t off, bool leaf, bool pdur,
                                         const T *mrow, uint32_t c_max_from, const uint32_t *ch,
                                         const uint32_t (&id0)[kUpCB<T>], uint32_t *hist, const uint8_t *lut,
+                                        const UpKids &dk, uint64_t &ss,
                                         uint64_t &dsum0, uint64_t &dsum1, uint64_t &n500, bool &bad) {
   __asm__ volatile("" : "+v"(b0));  // opaque to loop strength reduction (down1_chunk)
   const uint64_t n = FULL ? b0 + kPer : te;
@@ -1412,8 +1646,13 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
   T f0[kUpCB<T>][kPer];
   // 1. the loads (no branch around the row loads: a branch that merges
   // loaded values makes the compiler wait for them inside it)
-  load4t<T>(arow, b0, n, ar);
-  load4t<T>(mrow, b0, n, mr);
+  if constexpr (OWN) load4t<T>(arow, b0, n, ar);
+  if constexpr (NS) {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) mr[i] = 0;
+  } else {
+    load4t<T>(mrow, b0, n, mr);
+  }
   const uint32_t stm = des_status4(k, v, b0);
 #pragma unroll
   for (uint32_t j = 0; j < kUpCB<T>; ++j)
@@ -1422,8 +1661,9 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
   uint64_t a[kPer], m[kPer];
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
-    a[i] = ((uint64_t)ar[i] + off) & amask;
-    m[i] = (uint64_t)mr[i] + P.floor;
+    a[i] = OWN ? (uint64_t)ar[i] + off : 0;
+    m[i] = NS ? 0 : (uint64_t)mr[i] + P.floor;  // NS: max_c F(c) >= S + floor
+    if constexpr (DK) ss += FULL || b0 + i < te ? (uint64_t)mr[i] : 0;  // S(caller): no step begins (plan)
   }
   uint32_t sto = 0;  // children's 500s, bit i
   if (cnt) {
@@ -1461,17 +1701,19 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
       const uint64_t F = leaf ? m[i] : m[i] + P.post;
       const uint32_t own = (stm >> i) & 1u;
       const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
-      const uint64_t dur = F - a[i];
+      // OWN: the duration; a caller-recorded position: its finish (the
+      // caller subtracts the arrival); the entry: 0 (des_finalize)
+      const uint64_t dur = OWN ? F - a[i] : pdur ? F : 0;
       bad |= !Row<T>::fits(F);
       o[i] = F | ((uint64_t)st << Row<T>::kTop);
       if (st && !k.quiet) atomicAdd(k.E + t, 1u);
       n500 += st;
       dsum1 += st ? dur : 0;
       dsum0 += st ? 0 : dur;
-      bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
+      if constexpr (OWN) bin[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
     }
   }
-  hist_add4<FULL>(hist, bin);
+  if constexpr (OWN) hist_add4<FULL>(hist, bin);
   if (k.changed) {
     T ot[kPer];
 #pragma unroll
@@ -1479,6 +1721,30 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
     track4<T>(k, fin, b0, n, ot);
   }
   store4n<T>(fin, b0, n, o);
+  if constexpr (DK) {
+    // the flagged callees' durations F(c) - (S + off(c)): their finish rows
+    // again (just read above: cache hits), after the quad's own work so the
+    // children loop keeps its registers
+    for (uint32_t j = 0; j < dk.nd; ++j) {
+      T f[kPer];
+      load4t<T>(row<T>(k.WF, k.ld, dk.dch[j]), b0, n, f);
+      const uint64_t offc = dk.doff[j];
+      uint32_t cb[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) {
+        if (FULL || b0 + i < te) {
+          const uint64_t dur = (uint64_t)(f[i] & (T)Row<T>::kMask) - ((uint64_t)mr[i] + offc);
+          const uint32_t st = (uint32_t)(f[i] >> Row<T>::kTop);
+          cb[i] = st * ISIM_N_PROM + des_prom_bucket(lut, dur);
+          if (st) {
+            atomicAdd(dk.ds5 + j, (unsigned long long)mr[i]);
+            atomicAdd(dk.dn5 + j, 1u);
+          }
+        }
+      }
+      hist_add4<FULL>(dk.dhist + j * 2 * ISIM_N_PROM, cb);
+    }
+  }
 }
 
 // ---- up pass: finish times, statuses, per-service durations.
@@ -1488,9 +1754,14 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
   __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
+  __shared__ uint64_t s_doff[kDesDurKids];
+  __shared__ uint32_t s_dch[kDesDurKids], s_nd;
+  __shared__ uint32_t dhist[kDesDurKids * 2 * ISIM_N_PROM];
+  __shared__ unsigned long long ds5[kDesDurKids];
+  __shared__ uint32_t dn5[kDesDurKids];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hist[i] = 0;
   des_bucket_lut_init(lut);
-  __syncthreads();
+  if (threadIdx.x == 0) s_nd = 0;
   const uint32_t v = k.level_pos[k.level_begin + blockIdx.y];
   const DesPos P = k.pos[v];
   const uint64_t N = k.N;
@@ -1503,22 +1774,28 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
   const T *par = arrival_row<T>(k, v, P);
   const uint64_t off = par ? P.off : 0;
   const bool leaf = P.flags & kDesFlagLeaf;
+  const bool pdur = (P.flags & kDesFlagParentDur) != 0;
+  const bool own = par && !pdur;  // the block records the position's durations
   // several call steps: F = max(BK_last + floor, max F(last step's callees)) + post
   const T *base_t = X.bk_last == kDesNone ? nullptr : row<T>(k.BK, k.ld, X.bk_last);
   const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
-  uint64_t dsum0 = 0, dsum1 = 0, n500 = 0;
+  uint64_t dsum0 = 0, dsum1 = 0, n500 = 0, ss = 0;
   bool bad = false;
-  // rows read unconditionally: the arrival row (the entry: any row, masked
-  // to 0) and the row F's floor starts from (the last step's begin, or S)
-  const T *arow = par ? par : mine;
-  const uint64_t amask = par ? ~0ull : 0ull;
+  // rows read: the arrival row when the block records the durations, and the
+  // row F's floor starts from (the last step's begin, or S)
+  const T *arow = par;
   const T *mrow = base_t ? base_t : mine;
   // the child positions: in LDS when they fit (read by every quad; LDS
-  // addressing known to the compiler, not flat), else from global memory
+  // addressing known to the compiler, not flat), else from global memory;
+  // with them, which are flagged callees (the plan flags only callees of
+  // callers with at most kUpChildLds children)
   __shared__ uint32_t s_ch[kUpChildLds];
   const uint32_t cnt = leaf ? 0u : P.child_cnt;
   const uint32_t *gch = k.child + P.child_off;
-  auto run = [&](const uint32_t *ch) {
+  __syncthreads();  // s_nd
+  UpKids dk{0, s_dch, s_doff, dhist, ds5, dn5};
+  auto run = [&](const uint32_t *ch, auto own_t, auto dk_t, auto ns_t) {
+    constexpr bool OWN = decltype(own_t)::value, DK = decltype(dk_t)::value, NS = decltype(ns_t)::value;
     // the first children's positions in (uniform) registers for the whole
     // range: their row loads issue with the others, no id load in front
     uint32_t id0[kUpCB<T>];
@@ -1526,22 +1803,81 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
     for (uint32_t j = 0; j < kUpCB<T>; ++j) id0[j] = j < cnt ? ch[j] : 0u;
     for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
       if (b0 + kPer <= te)
-        up_quad<T, true>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut, dsum0,
-                         dsum1, n500, bad);
+        up_quad<T, true, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
+                                      lut, dk, ss, dsum0, dsum1, n500, bad);
       else
-        up_quad<T, false>(k, P, v, b0, te, fin, arow, amask, off, leaf, mrow, c_max_from, ch, id0, hist, lut,
-                          dsum0, dsum1, n500, bad);
+        up_quad<T, false, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
+                                       lut, dk, ss, dsum0, dsum1, n500, bad);
     }
   };
+  using tt = std::true_type;
+  using ff = std::false_type;
+  uint32_t nd = 0;
   if (cnt <= kUpChildLds) {
-    for (uint32_t i = threadIdx.x; i < cnt; i += kDesUpThreads) s_ch[i] = gch[i];
+    for (uint32_t i = threadIdx.x; i < cnt; i += kDesUpThreads) {
+      const uint32_t c = gch[i];
+      s_ch[i] = c;
+      const uint32_t f = k.pos[c].flags;
+      if (f & kDesFlagParentDur) {
+        const uint32_t j = (f >> kDesDurShift) & 0xFFu;
+        s_doff[j] = k.pos[c].off;
+        s_dch[j] = c;
+        atomicMax(&s_nd, j + 1);
+      }
+    }
     __syncthreads();
-    run(s_ch);
+    nd = s_nd;
+    dk.nd = nd;
+    for (uint32_t i = threadIdx.x; i < nd * 2 * ISIM_N_PROM; i += kDesUpThreads) dhist[i] = 0;
+    if (threadIdx.x < nd) {
+      ds5[threadIdx.x] = 0;
+      dn5[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const bool ns = (P.flags & kDesFlagNoStart) != 0;
+    if (nd) {
+      if (own) run(s_ch, tt{}, tt{}, ff{});
+      else run(s_ch, ff{}, tt{}, ff{});
+    } else if (ns) {
+      if (own) run(s_ch, tt{}, ff{}, tt{});
+      else run(s_ch, ff{}, ff{}, tt{});
+    } else {
+      if (own) run(s_ch, tt{}, ff{}, ff{});
+      else run(s_ch, ff{}, ff{}, ff{});
+    }
   } else {
-    run(gch);
+    if (own) run(gch, tt{}, ff{}, ff{});
+    else run(gch, ff{}, ff{}, ff{});
   }
   flag_overflow(k, bad);
   if (k.quiet) return;
+  if (nd) {
+    // the flagged callees' histograms, and their duration sums less the
+    // arrivals: Σ (S + off) over this block's traces, by the callee's status
+#pragma unroll
+    for (uint32_t d = 32; d > 0; d >>= 1) ss += __shfl_xor(ss, d, 64);
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    uint64_t sall = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kDesUpThreads / 64; ++w) sall += red[w];
+    for (uint32_t i = threadIdx.x; i < nd * 2 * ISIM_N_PROM; i += kDesUpThreads) {
+      const uint32_t j = i / (2 * ISIM_N_PROM), b = i - j * (2 * ISIM_N_PROM);
+      if (dhist[i])
+        atomicAdd((unsigned long long *)(k.table + (uint64_t)k.pos[s_dch[j]].row * ISIM_DES_ROW_WORDS + b),
+                  (unsigned long long)dhist[i]);
+    }
+    if (threadIdx.x < nd) {
+      const uint32_t j = threadIdx.x;
+      const uint64_t s5 = ds5[j], n5 = dn5[j], offc = s_doff[j];
+      const uint64_t a1 = s5 + n5 * offc, a0 = (sall - s5) + ((te - tb) - n5) * offc;
+      unsigned long long *trow =
+          (unsigned long long *)(k.table + (uint64_t)k.pos[s_dch[j]].row * ISIM_DES_ROW_WORDS);
+      if (a0) atomicAdd(trow + 2 * ISIM_N_PROM, (unsigned long long)(0 - a0));
+      if (a1) atomicAdd(trow + 2 * ISIM_N_PROM + 1, (unsigned long long)(0 - a1));
+    }
+    __syncthreads();  // red is reused below
+  }
   des_flush_durations<kDesUpThreads>(k, P, hist, dsum0, dsum1, n500, red);
 }
 
@@ -1549,7 +1885,7 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
 template <typename T>
 __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
-  __shared__ uint64_t red[5 * kDesUpThreads / 64];
+  __shared__ uint64_t red[6 * kDesUpThreads / 64];
   __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads) hp[i] = 0;
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads) hl[i] = 0;
@@ -1559,12 +1895,12 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
   // an overflowed narrow batch is dropped (des_commit): records untouched
   const bool keep = *k.ovf == 0;
   const T *F0 = row<T>(k.WF, k.ld, 0);  // position 0: the entry
-  uint64_t sl = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
+  uint64_t sl = 0, s5 = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * kDesUpThreads + threadIdx.x; t < N;
        t += (uint64_t)gridDim.x * kDesUpThreads) {
     const uint64_t F = F0[t];
     const uint32_t st = (uint32_t)(F >> Row<T>::kTop);
-    const uint64_t L = F & Row<T>::kMask;  // relative to the trace's arrival: the latency
+    const uint64_t L = (F & Row<T>::kMask) - (k.A[t] - des_gbase(k, t));  // the latency
     const uint32_t e = k.E[t];
     if (k.records && keep) {
       isim_trace_rec r;
@@ -1574,6 +1910,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
       k.records[t] = r;
     }
     sl += L;
+    s5 += st ? L : 0;
     se += e;
     n5 += st;
     mn = L < mn ? L : mn;
@@ -1584,6 +1921,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
 #pragma unroll
   for (uint32_t d = 32; d > 0; d >>= 1) {
     sl += __shfl_xor(sl, d, 64);
+    s5 += __shfl_xor(s5, d, 64);
     se += __shfl_xor(se, d, 64);
     n5 += __shfl_xor(n5, d, 64);
     const uint64_t a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
@@ -1598,11 +1936,19 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
     red[2 * W + w] = n5;
     red[3 * W + w] = mn;
     red[4 * W + w] = mx;
+    red[5 * W + w] = s5;
   }
   __syncthreads();
   unsigned long long *st = (unsigned long long *)k.stats;
+  // the entry's invocation durations (RecordResponseSent) are the latencies;
+  // des_up leaves them here unless the entry finished in its queue pass
+  const bool entry_dur = !(k.pos[0].flags & kDesFlagFused);
+  unsigned long long *trow = (unsigned long long *)(k.table + (uint64_t)k.pos[0].row * ISIM_DES_ROW_WORDS);
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kDesUpThreads)
-    if (hp[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)hp[i]);
+    if (hp[i]) {
+      atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)hp[i]);
+      if (entry_dur) atomicAdd(trow + i, (unsigned long long)hp[i]);
+    }
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kDesUpThreads)
     if (hl[i]) atomicAdd(st + ISIM_ST_LOG2 + i, (unsigned long long)hl[i]);
   if (threadIdx.x == 0) {
@@ -1612,6 +1958,11 @@ __global__ void __launch_bounds__(kDesUpThreads) des_finalize(DesK k) {
       red[2 * W] += red[2 * W + i];
       red[3 * W] = red[3 * W + i] < red[3 * W] ? red[3 * W + i] : red[3 * W];
       red[4 * W] = red[4 * W + i] > red[4 * W] ? red[4 * W + i] : red[4 * W];
+      red[5 * W] += red[5 * W + i];
+    }
+    if (entry_dur) {
+      if (red[0] - red[5 * W]) atomicAdd(trow + 2 * ISIM_N_PROM, (unsigned long long)(red[0] - red[5 * W]));
+      if (red[5 * W]) atomicAdd(trow + 2 * ISIM_N_PROM + 1, (unsigned long long)red[5 * W]);
     }
     if (blockIdx.x == 0) {
       atomicAdd(st + ISIM_ST_N_TRACES, (unsigned long long)N);
@@ -1637,7 +1988,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_sort_keys(DesK k) {
        i += (uint64_t)gridDim.x * kDesUpThreads) {
     const uint64_t t = i / P;
     const uint32_t v = k.sort_pos[k.svc.pos_off + (uint32_t)(i - t * P)];
-    const uint64_t a = k.A[t] + des_arrival<T>(k, v, k.pos[v], t);
+    const uint64_t a = des_gbase(k, t) + des_arrival<T>(k, v, k.pos[v], t);
     const uint32_t rb = rep_bits(k.svc.reps);
     uint64_t key = a;
     if (rb) {
@@ -1742,7 +2093,7 @@ __global__ void __launch_bounds__(kDesThreads) des_down_sorted(DesK k) {
       if (base + i < M) {
         if (st[i]) x = 0;  // the replica's worker is idle before its first invocation
         const uint64_t S = x > a[i] ? x : a[i];
-        const uint64_t rel = S - k.A[tt[i]];
+        const uint64_t rel = S - des_gbase(k, tt[i]);
         bad |= !Row<T>::fits(rel);
         row<T>(k.W, k.ld, vv[i])[tt[i]] = (T)rel;
         const uint64_t w = S - a[i];
@@ -1801,7 +2152,7 @@ __global__ void __launch_bounds__(kDesUpThreads) des_zero(DesK k) {
   T *out = row<T>(k.W, k.ld, v);
   bool bad = false;
   for (uint64_t t = tb + threadIdx.x; t < te; t += kDesUpThreads) {
-    const uint64_t a = par ? (uint64_t)par[t] + off : 0;
+    const uint64_t a = par ? (uint64_t)par[t] + off : k.A[t] - des_gbase(k, t);
     bad |= !Row<T>::fits(a);
     out[t] = (T)a;
   }
@@ -1933,7 +2284,12 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       kp.pipe_dep = L.d_pipe + pl.pipe_pos.size();
       kp.level_begin = sg.off;
       kp.chain_ticket = tickets + 4 * r + 2;
-      hipLaunchKernelGGL(des_down_pipe<T>, dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
+      bool n32 = false;
+      if constexpr (sizeof(T) == 4) {
+        n32 = pl.pipe_n32 && !std::getenv("ISIM_DES_NO_PIPE32");
+        if (n32) hipLaunchKernelGGL((des_down_pipe<T, true>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
+      }
+      if (!n32) hipLaunchKernelGGL((des_down_pipe<T, false>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
       piped_to = sg.r1 + 1;
     }
     if (r < piped_to) goto finishes;

@@ -20,6 +20,7 @@
 #include "des.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace isim {
 namespace {
@@ -458,6 +459,38 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       out.pipe.push_back(sg);
     }
     r = e;
+  }
+  out.pipe_n32 = !out.pipe.empty();
+  for (uint32_t v : out.pipe_pos) {
+    const DesPos &ps = out.pos[v];
+    out.pipe_n32 = out.pipe_n32 && ps.hold < (1ull << 25) && ps.off < (1ull << 30) &&
+                   (!(ps.flags & kDesFlagFused) || ps.floor < (1ull << 30));
+  }
+  // finishes without the start row (kDesFlagNoStart; ISIM_DES_NO_NOSTART
+  // set: off, for A/B measurements)
+  if (!out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_NOSTART")) {
+    for (uint32_t v = 0; v < np; ++v) {
+      if ((out.pos[v].flags & kDesFlagFused) || kids[v].empty()) continue;
+      const ScriptShape &sh = shape[pos_svc[v]];
+      const uint64_t smax = sh.smax.empty() ? 0 : sh.smax[0];
+      bool ok = true;
+      for (uint32_t c : kids[v]) ok = ok && out.pos[c].off >= sh.pre + smax;  // off = pre + H
+      if (ok) out.pos[v].flags |= kDesFlagNoStart;
+    }
+  }
+  // durations recorded by the caller (des.hip des_up): one call step per
+  // script (every arrival is start(caller) + off), no fixed-point passes, the
+  // caller's first kDesDurKids non-fused callees (ISIM_DES_NO_PARENT_DUR set:
+  // every position records its own, for A/B measurements)
+  if (!out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_PARENT_DUR")) {
+    for (uint32_t v = 0; v < np; ++v) {
+      if (kids[v].size() > kDesUpChildLds) continue;
+      uint32_t j = 0;
+      for (uint32_t c : kids[v]) {
+        if ((out.pos[c].flags & kDesFlagFused) || j >= kDesDurKids) continue;
+        out.pos[c].flags |= kDesFlagParentDur | (j++ << kDesDurShift);
+      }
+    }
   }
   out.slot_mult = p.stream_mult;
   return ISIM_OK;

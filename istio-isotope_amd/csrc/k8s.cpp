@@ -186,8 +186,24 @@ static std::vector<uint32_t> runes(const std::string &s) {
   }
   return r;
 }
-static bool is_letter(uint32_t r) {  // unicode.IsLetter for the ASCII/Latin range the keys use
-  return (r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z') || (r >= 0xC0 && r != 0xD7 && r != 0xF7);
+#include "unicode_tables.inc"
+static bool in_ranges(const uint32_t (*t)[2], size_t n, uint32_t r) {
+  size_t lo = 0, hi = n;  // first range whose end >= r
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (t[mid][1] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && t[lo][0] <= r;
+}
+// unicode.IsLetter / unicode.IsDigit (Go), as sorter.go uses them
+static bool is_letter(uint32_t r) {
+  if (r < 0x80) return (r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z');
+  return in_ranges(kUniLetter, sizeof(kUniLetter) / sizeof(kUniLetter[0]), r);
+}
+static bool is_udigit(uint32_t r) {
+  if (r < 0x80) return r >= '0' && r <= '9';
+  return in_ranges(kUniDigit, sizeof(kUniDigit) / sizeof(kUniDigit[0]), r);
 }
 static bool is_digit(uint32_t r) { return r >= '0' && r <= '9'; }
 static bool key_less(const std::string &as, const std::string &bs) {
@@ -197,19 +213,20 @@ static bool key_less(const std::string &as, const std::string &bs) {
     const bool al = is_letter(a[i]), bl = is_letter(b[i]);
     if (al && bl) return a[i] < b[i];
     if (al || bl) return bl;
-    long long an = 0, bn = 0;
+    // Go int64 arithmetic on rune - '0' (wrapping; any Nd digit counts)
+    uint64_t an = 0, bn = 0;
     size_t ai, bi;
     if (a[i] == '0' || b[i] == '0') {
-      for (long j = (long)i - 1; j >= 0 && is_digit(a[j]); --j)
+      for (long j = (long)i - 1; j >= 0 && is_udigit(a[j]); --j)
         if (a[j] != '0') {
           an = 1;
           bn = 1;
           break;
         }
     }
-    for (ai = i; ai < a.size() && is_digit(a[ai]); ++ai) an = an * 10 + (a[ai] - '0');
-    for (bi = i; bi < b.size() && is_digit(b[bi]); ++bi) bn = bn * 10 + (b[bi] - '0');
-    if (an != bn) return an < bn;
+    for (ai = i; ai < a.size() && is_udigit(a[ai]); ++ai) an = an * 10 + (uint64_t)((int64_t)a[ai] - '0');
+    for (bi = i; bi < b.size() && is_udigit(b[bi]); ++bi) bn = bn * 10 + (uint64_t)((int64_t)b[bi] - '0');
+    if (an != bn) return (int64_t)an < (int64_t)bn;
     if (ai != bi) return ai < bi;
     return a[i] < b[i];
   }

@@ -34,6 +34,7 @@ import datetime
 import functools
 import json
 import re
+import unicodedata
 from typing import Any, Dict, List, Optional
 
 import yaml
@@ -47,11 +48,23 @@ NAMESPACE = "service-graph"
 
 # ------------------------------------------------------ yaml.v2 choices -----
 def _is_letter(ch: str) -> bool:
-    return ch.isalpha()
+    """Go unicode.IsLetter: categories Lu, Ll, Lt, Lm, Lo."""
+    return unicodedata.category(ch) in ("Lu", "Ll", "Lt", "Lm", "Lo")
+
+
+def _is_digit(ch: str) -> bool:
+    """Go unicode.IsDigit: category Nd (str.isdigit would also take superscripts)."""
+    return unicodedata.category(ch) == "Nd"
+
+
+def _wrap64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >> 63 else x
 
 
 def keylist_less(a: str, b: str) -> bool:
-    """gopkg.in/yaml.v2 sorter.go keyList.Less for two string keys."""
+    """gopkg.in/yaml.v2 sorter.go keyList.Less for two string keys (Go int64
+    arithmetic on rune - '0', so a non-ASCII digit counts by its code point)."""
     ar, br = list(a), list(b)
     for i in range(min(len(ar), len(br))):
         if ar[i] == br[i]:
@@ -64,18 +77,18 @@ def keylist_less(a: str, b: str) -> bool:
         an = bn = 0
         if ar[i] == "0" or br[i] == "0":
             j = i - 1
-            while j >= 0 and ar[j].isdigit():
+            while j >= 0 and _is_digit(ar[j]):
                 if ar[j] != "0":
                     an = bn = 1
                     break
                 j -= 1
         ai = i
-        while ai < len(ar) and ar[ai].isdigit():
-            an = an * 10 + int(ar[ai])
+        while ai < len(ar) and _is_digit(ar[ai]):
+            an = _wrap64(an * 10 + ord(ar[ai]) - 48)
             ai += 1
         bi = i
-        while bi < len(br) and br[bi].isdigit():
-            bn = bn * 10 + int(br[bi])
+        while bi < len(br) and _is_digit(br[bi]):
+            bn = _wrap64(bn * 10 + ord(br[bi]) - 48)
             bi += 1
         if an != bn:
             return an < bn

@@ -333,3 +333,17 @@ def test_hypothesis_graphs_match_oracle(doc, image, sel):
               rbac_seed=3, creation_timestamp_s=TS)
     a, b = _both(g, og, **kw)
     assert a == b
+
+
+def test_key_order_unicode_classes():
+    """yaml.v2 sorter.go keyList.Less classifies runes with Go's
+    unicode.IsLetter (L*) and unicode.IsDigit (Nd), and a digit counts as
+    rune - '0': a nonspacing mark (U+0EB4) is no letter, an Arabic-Indic
+    three (U+0663) is a digit worth 1587, a superscript two no digit.
+    Expected order derived by hand from those rules."""
+    g, og = _graphs(os.path.join(HERE, "golden", "topologies", "1-service.yaml"))
+    sel = {"true": "1", "ິ": "2", "a٣": "3", "a2": "4", "x²": "5"}
+    a, b = _both(g, og, service_node_selector=sel, creation_timestamp_s=TS)
+    assert a == b
+    block = a.split("nodeSelector:\n", 1)[1].splitlines()[:5]
+    assert [ln.strip().split(":")[0] for ln in block] == ["ິ", "a2", "a٣", '"true"', "x²"]
