@@ -259,13 +259,14 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     value = total / elapsed
     npos = d.info.n_positions
     # algorithmic bytes of one step, R = row bytes (4 or 8):
-    # queue pass 2R per (position, trace) (arrival row read, start / fused
-    # finish written), up pass 3R per (non-fused position, trace) (start,
-    # arrival row, finish) + R per (child edge, trace); arrivals / finalize /
-    # records ~60 B per trace
+    # the rows the queue and finish passes read and write per trace
+    # (isim_des_info row_reads / row_writes: the plan's own count — fused
+    # leaves, caller-recorded durations, finishes without the start row), the
+    # status bits (written once, read once: n_pos / 4 B), arrivals / per-trace
+    # 500 counts / finalize ~44 B, records 16 B
     R = 8 if wide[0] else 4
-    nf = d.info.n_fused
-    alg_bytes = B * (R * (2 * npos + 3 * (npos - nf) + (npos - 1)) + 44 + (0 if args.no_records else 16))
+    rows = d.info.row_reads + d.info.row_writes
+    alg_bytes = B * (R * rows + npos // 4 + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = occupancy = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary_c5.json")

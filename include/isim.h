@@ -322,6 +322,8 @@ typedef struct {
   int32_t table_rows;            /* rows of the DES table (reachable services) */
   int32_t n_fused;               /* leaf positions finished in their queue pass (no up pass) */
   int32_t cyclic;                /* 1: the call-step schedule is cyclic (fixed-point passes) */
+  int32_t row_reads;             /* rows one trace's batch reads (queue + finish passes, one pass), 4 or 8 B each */
+  int32_t row_writes;            /* rows it writes (the algorithmic bytes of bench.py's roofline) */
 } isim_des_info;
 
 ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);

@@ -801,6 +801,10 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   out->table_rows = (int32_t)h->prog.row_svc.size();
   for (const auto &q : h->des.pos) out->n_fused += (q.flags & isim::kDesFlagFused) ? 1 : 0;
   out->cyclic = h->des.cyclic ? 1 : 0;
+  uint32_t rr = 0, rw = 0;
+  isim::des_row_traffic(h->des, rr, rw);
+  out->row_reads = (int32_t)rr;
+  out->row_writes = (int32_t)rw;
   return ISIM_OK;
 }
 

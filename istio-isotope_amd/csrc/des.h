@@ -163,6 +163,11 @@ int des_launch(const DesLaunch &L, void *stream);
 // one 32-byte state per (position, chunk of 4096 traces); zeroed per batch.
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n);
 
+// Rows one trace reads and writes in a batch's queue and finish passes (one
+// pass of a cyclic schedule): what des.hip's kernels move per trace, 4 or 8
+// bytes each (the algorithmic bytes of the roofline).
+void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes);
+
 // Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is
 // outside the DES class.
 int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err);

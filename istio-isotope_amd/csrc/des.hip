@@ -64,7 +64,7 @@ constexpr uint32_t kDesUpThreads = 256;
 // to 65536 replicas; the host checks the batch's arrival span)
 __device__ __forceinline__ uint32_t rep_bits(uint32_t reps) { return reps > 1 ? 32u - __builtin_clz(reps - 1u) : 0u; }
 #ifndef ISIM_DES_DOWN_THREADS
-#define ISIM_DES_DOWN_THREADS 512
+#define ISIM_DES_DOWN_THREADS 256  // round 3: 512 -> 256 threads per queue-pass workgroup, 36.9 -> 36.4 ms per c5 step
 #endif
 constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-position queue pass
 #ifndef ISIM_DES_MIX
@@ -1606,7 +1606,7 @@ __global__ void __launch_bounds__(kDownThreads, N32 ? ISIM_DES_PIPE32_WAVES : IS
 // children past kUpCB (hubs) follow in batches.  `ch`: the child positions,
 // staged in LDS by the workgroup when they fit.
 #ifndef ISIM_DES_UP_CB
-#define ISIM_DES_UP_CB 3
+#define ISIM_DES_UP_CB 2  // round 3: 3 -> 2 (with the 256-thread queue pass: 36.4 -> 36.1 ms per c5 step)
 #endif
 #ifndef ISIM_DES_UP_WAVES
 #define ISIM_DES_UP_WAVES 6  // waves per SIMD the up pass is compiled for (80 VGPRs: no spills)

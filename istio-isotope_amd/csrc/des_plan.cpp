@@ -72,6 +72,32 @@ ScriptShape shape_of(const Service &s) {
 
 }  // namespace
 
+void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes) {
+  reads = writes = 0;
+  const uint32_t np = (uint32_t)plan.pos.size();
+  // flagged callees per caller (des_up records their durations)
+  std::vector<uint32_t> nd(np, 0);
+  for (uint32_t v = 1; v < np; ++v)
+    if (plan.pos[v].flags & kDesFlagParentDur) ++nd[plan.pos[v].parent];
+  for (uint32_t v = 0; v < np; ++v) {
+    const DesPos &q = plan.pos[v];
+    // queue pass (fast, zero-hold or sort path): the arrival row (the entry's
+    // arrivals are per-trace extras), the start or fused finish row
+    reads += v ? 1 : 0;
+    writes += 1;
+    if (q.flags & kDesFlagFused) continue;
+    // finish pass: the children's finishes, the start row unless the finish
+    // needs none and no callee's duration is recorded here, the arrival row
+    // when the position records its own durations, the finish row
+    reads += q.child_cnt;
+    reads += (q.flags & kDesFlagNoStart) && nd[v] == 0 ? 0 : 1;
+    reads += v && !(q.flags & kDesFlagParentDur) ? 1 : 0;
+    writes += 1;
+  }
+  reads += (uint32_t)plan.steps.size() * 2;  // step begins: a row read and written per BK row
+  writes += (uint32_t)plan.steps.size();
+}
+
 int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err) {
   out = DesPlan();
   if (!p.static_walk || p.stream_nodes == 0) {

@@ -97,7 +97,8 @@ class MultiId(C.Structure):
 
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
-                ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32)]
+                ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32),
+                ("row_reads", C.c_int32), ("row_writes", C.c_int32)]
 
 
 # every function declared in include/isim.h: name -> (restype, argtypes)

@@ -411,3 +411,34 @@ def test_cyclic_mode_b_and_wide(gpu):
     r2, s2, t2 = c.d.serve(7, 3000, wide=True)
     assert np.array_equal(r1, r2) and np.array_equal(s1, s2) and np.array_equal(t1, t2)
 
+
+
+# ---- round 3: callers record their callees' durations (kDesFlagParentDur:
+# the first kDesDurKids = 8 non-fused callees), finishes without the start
+# row (kDesFlagNoStart: every callee's hop cost >= the call step's longest
+# sleep), 32-bit queue keys per 64-trace group
+def _wide_fanout(n_mid=12, conc_sleep_every=2, err=0.02):
+    svcs = [{"name": "r", "isEntrypoint": True, "errorRate": err,
+             "script": [{"sleep": "1ms"}, [{"call": f"c{i}"} for i in range(n_mid)]]}]
+    for i in range(n_mid):
+        step = [{"call": f"l{i}_{j}"} for j in range(3)]
+        if i % conc_sleep_every == 0:
+            step.append({"sleep": "5ms"})  # longer than the hop cost: the finish needs the start row
+        svcs.append({"name": f"c{i}", "errorRate": err, "script": [{"sleep": "2ms"}, step]})
+        for j in range(3):
+            svcs.append({"name": f"l{i}_{j}", "errorRate": err, "script": [{"sleep": "1ms"}]})
+    return {"services": svcs}
+
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+@pytest.mark.parametrize("mean", [400_000, 3_000_000])
+def test_caller_recorded_durations(gpu, mode, mean):
+    # 12 non-leaf callees of the entry: 8 recorded by the entry's finish
+    # block, 4 by their own; half the callers need their start row
+    DesCase(_wide_fanout(), mean, error_mode=mode).compare(5, 9000)
+
+
+def test_group_bases_long_gaps(gpu):
+    # 64-trace groups spanning ~1.3 s of arrivals (20 ms mean gap): the
+    # group-relative rows and keys near their 32-bit range, ragged batch
+    DesCase(_wide_fanout(6, 1, 0.05), 20_000_000).compare(1 << 32, 4099)
