@@ -124,6 +124,9 @@ struct DesPlan {
   // every pipelined position's holds and offsets fit the 32-bit queue keys
   // (des.hip down1_chunk_n32: hold < 2^25, off and a leaf's floor < 2^30)
   bool pipe_n32 = false;
+  // no step begins and every finish constant (off, floor, post) below 2^30:
+  // des_up's finish quads in 32-bit arithmetic (des.hip up_quad32)
+  bool up_n32 = false;
   uint32_t rounds() const { return (uint32_t)arr_off.size() - 1; }
 };
 

@@ -1747,10 +1747,124 @@ __device__ __forceinline__ void up_quad(const DesK &k, const DesPos &P, uint32_t
   }
 }
 
+// up_quad for narrow rows in 32-bit arithmetic (round 3): every value below
+// 2^31 + 2^30 (row values < 2^31, the host-checked off / floor / post
+// < 2^30: DesPlan::up_n32), so no 64-bit time in the quad — fewer VGPRs,
+// more waves of loads in flight.  The same results as up_quad<uint32_t, ...>.
+template <bool FULL, bool OWN, bool DK, bool NS>
+__device__ __forceinline__ void up_quad32(const DesK &k, const DesPos &P, uint32_t v, uint64_t b0, uint64_t te,
+                                          uint32_t *fin, const uint32_t *arow, uint32_t off32, bool leaf, bool pdur,
+                                          const uint32_t *mrow, const uint32_t *ch, const uint32_t (&id0)[kUpCB<uint32_t>],
+                                          uint32_t *hist, const uint8_t *lut, const UpKids &dk, uint64_t &ss,
+                                          uint64_t &dsum0, uint64_t &dsum1, uint32_t &n500, bool &bad) {
+  using T = uint32_t;
+  __asm__ volatile("" : "+v"(b0));  // opaque to loop strength reduction (down1_chunk)
+  const uint64_t n = FULL ? b0 + kPer : te;
+  const uint32_t cnt = leaf ? 0u : P.child_cnt;
+  T ar[kPer], mr[kPer];
+  T f0[kUpCB<T>][kPer];
+  if constexpr (OWN) load4t<T>(arow, b0, n, ar);
+  if constexpr (NS) {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) mr[i] = 0;
+  } else {
+    load4t<T>(mrow, b0, n, mr);
+  }
+  const uint32_t stm = des_status4(k, v, b0);
+#pragma unroll
+  for (uint32_t j = 0; j < kUpCB<T>; ++j)
+    if (j < cnt) load4t<T>(row<T>(k.WF, k.ld, id0[j]), b0, n, f0[j]);
+  const uint32_t floor32 = (uint32_t)P.floor, post32 = leaf ? 0u : (uint32_t)P.post;
+  uint32_t m[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    m[i] = NS ? 0u : mr[i] + floor32;  // NS: max_c F(c) >= S + floor
+    if constexpr (DK) ss += FULL || b0 + i < te ? (uint64_t)mr[i] : 0;
+  }
+  uint32_t sto = 0;  // children's 500s, bit i
+  auto take = [&](const T (&f)[kPer]) {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+      const T tc = f[i] & 0x7FFFFFFFu;
+      m[i] = tc > m[i] ? tc : m[i];
+      sto |= (f[i] >> 31) << i;
+    }
+  };
+#pragma unroll
+  for (uint32_t j = 0; j < kUpCB<T>; ++j)
+    if (j < cnt) take(f0[j]);
+  for (uint32_t c = kUpCB<T>; c < cnt; c += kUpCB<T>) {
+    T f[kUpCB<T>][kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kUpCB<T>; ++j)
+      if (c + j < cnt) load4t<T>(row<T>(k.WF, k.ld, ch[c + j]), b0, n, f[j]);
+#pragma unroll
+    for (uint32_t j = 0; j < kUpCB<T>; ++j)
+      if (c + j < cnt) take(f[j]);
+  }
+  T o[kPer];
+  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin}, big = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint64_t t = b0 + i;
+    o[i] = 0;
+    if (FULL || t < te) {
+      const uint32_t F = m[i] + post32;
+      const uint32_t own = (stm >> i) & 1u;
+      const uint32_t st = k.modeb ? (own | ((sto >> i) & 1u)) : own;
+      // OWN: the duration; a caller-recorded position: its finish (the
+      // caller subtracts the arrival); the entry: 0 (des_finalize)
+      const uint32_t dur = OWN ? F - (ar[i] + off32) : pdur ? F : 0u;
+      big |= F;
+      o[i] = F | (st << 31);
+      if (st && !k.quiet) atomicAdd(k.E + t, 1u);
+      n500 += st;
+      dsum1 += st ? dur : 0u;
+      dsum0 += st ? 0u : dur;
+      if constexpr (OWN) bin[i] = st * ISIM_N_PROM + des_prom_bucket32(lut, dur);
+    }
+  }
+  bad |= (big >> 31) != 0u;
+  if constexpr (OWN) hist_add4<FULL>(hist, bin);
+  if (k.changed) track4<T>(k, fin, b0, n, o);
+  if constexpr (FULL) store4t<T>(fin, b0, n, o);
+  else {
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i)
+      if (b0 + i < te) fin[b0 + i] = o[i];
+  }
+  if constexpr (DK) {
+    // the flagged callees' durations F(c) - (S + off(c)) (up_quad)
+    for (uint32_t j = 0; j < dk.nd; ++j) {
+      T f[kPer];
+      load4t<T>(row<T>(k.WF, k.ld, dk.dch[j]), b0, n, f);
+      const uint32_t offc = (uint32_t)dk.doff[j];
+      uint32_t cb[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin};
+#pragma unroll
+      for (uint32_t i = 0; i < kPer; ++i) {
+        if (FULL || b0 + i < te) {
+          const uint32_t dur = (f[i] & 0x7FFFFFFFu) - (mr[i] + offc);
+          const uint32_t st = f[i] >> 31;
+          cb[i] = st * ISIM_N_PROM + des_prom_bucket32(lut, dur);
+          if (st) {
+            atomicAdd(dk.ds5 + j, (unsigned long long)mr[i]);
+            atomicAdd(dk.dn5 + j, 1u);
+          }
+        }
+      }
+      hist_add4<FULL>(dk.dhist + j * 2 * ISIM_N_PROM, cb);
+    }
+  }
+}
+
 // ---- up pass: finish times, statuses, per-service durations.
 // (position, trace-range) blocks; 4 consecutive traces per thread.
-template <typename T>
-__global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK k) {
+#ifndef ISIM_DES_UP32_WAVES
+#define ISIM_DES_UP32_WAVES 7  // 69 VGPRs: no spills at 7 (35.6 -> 35.4 ms per c5 step), 8 spill
+#endif
+// N32: narrow rows and every finish constant below 2^30 (DesPlan::up_n32): up_quad32
+template <typename T, bool N32>
+__global__ void __launch_bounds__(kDesUpThreads, N32 ? ISIM_DES_UP32_WAVES : ISIM_DES_UP_WAVES) des_up(DesK k) {
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
   __shared__ uint64_t red[3 * kDesUpThreads / 64];
   __shared__ __attribute__((aligned(4))) uint8_t lut[4 * kBucketLutWords];
@@ -1780,6 +1894,7 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
   const T *base_t = X.bk_last == kDesNone ? nullptr : row<T>(k.BK, k.ld, X.bk_last);
   const uint32_t c_max_from = X.bk_last == kDesNone ? 0u : X.last_child;
   uint64_t dsum0 = 0, dsum1 = 0, n500 = 0, ss = 0;
+  uint32_t n500_32 = 0;
   bool bad = false;
   // rows read: the arrival row when the block records the durations, and the
   // row F's floor starts from (the last step's begin, or S)
@@ -1802,12 +1917,21 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
 #pragma unroll
     for (uint32_t j = 0; j < kUpCB<T>; ++j) id0[j] = j < cnt ? ch[j] : 0u;
     for (uint64_t b0 = tb + (uint64_t)threadIdx.x * kPer; b0 < te; b0 += (uint64_t)kPer * kDesUpThreads) {
-      if (b0 + kPer <= te)
-        up_quad<T, true, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
-                                      lut, dk, ss, dsum0, dsum1, n500, bad);
-      else
-        up_quad<T, false, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
-                                       lut, dk, ss, dsum0, dsum1, n500, bad);
+      if constexpr (N32 && sizeof(T) == 4) {
+        if (b0 + kPer <= te)
+          up_quad32<true, OWN, DK, NS>(k, P, v, b0, te, fin, arow, (uint32_t)off, leaf, pdur, mrow, ch, id0, hist, lut,
+                                       dk, ss, dsum0, dsum1, n500_32, bad);
+        else
+          up_quad32<false, OWN, DK, NS>(k, P, v, b0, te, fin, arow, (uint32_t)off, leaf, pdur, mrow, ch, id0, hist, lut,
+                                        dk, ss, dsum0, dsum1, n500_32, bad);
+      } else {
+        if (b0 + kPer <= te)
+          up_quad<T, true, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
+                                        lut, dk, ss, dsum0, dsum1, n500, bad);
+        else
+          up_quad<T, false, OWN, DK, NS>(k, P, v, b0, te, fin, arow, off, leaf, pdur, mrow, c_max_from, ch, id0, hist,
+                                         lut, dk, ss, dsum0, dsum1, n500, bad);
+      }
     }
   };
   using tt = std::true_type;
@@ -1849,6 +1973,7 @@ __global__ void __launch_bounds__(kDesUpThreads, ISIM_DES_UP_WAVES) des_up(DesK 
     if (own) run(gch, tt{}, ff{}, ff{});
     else run(gch, ff{}, ff{}, ff{});
   }
+  n500 += n500_32;
   flag_overflow(k, bad);
   if (k.quiet) return;
   if (nd) {
@@ -2361,7 +2486,12 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       const uint32_t width = pl.fin_off[gi + 1] - pl.fin_off[gi];
       k.level_begin = pl.fin_off[gi];
       k.splits = splits_for(width);
-      hipLaunchKernelGGL(des_up<T>, dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+      bool n32 = false;
+      if constexpr (sizeof(T) == 4) {
+        n32 = pl.up_n32 && !std::getenv("ISIM_DES_NO_UP32");
+        if (n32) hipLaunchKernelGGL((des_up<T, true>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
+      }
+      if (!n32) hipLaunchKernelGGL((des_up<T, false>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
     }
   }
   return 0;

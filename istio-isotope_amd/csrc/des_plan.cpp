@@ -486,6 +486,9 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     }
     r = e;
   }
+  out.up_n32 = !out.general && !out.cyclic;
+  for (const DesPos &ps : out.pos)
+    out.up_n32 = out.up_n32 && ps.off < (1ull << 30) && ps.floor < (1ull << 30) && ps.post < (1ull << 30);
   out.pipe_n32 = !out.pipe.empty();
   for (uint32_t v : out.pipe_pos) {
     const DesPos &ps = out.pos[v];
