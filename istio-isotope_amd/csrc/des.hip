@@ -70,6 +70,12 @@ constexpr uint32_t kDownThreads = ISIM_DES_DOWN_THREADS;  // one-workgroup-per-p
 #ifndef ISIM_DES_MIX
 #define ISIM_DES_MIX 1  // fused and other single-replica positions of a round in one queue launch
 #endif
+#ifndef ISIM_DES_FIN_BLOCKS
+#define ISIM_DES_FIN_BLOCKS 512  // des_finalize workgroups (each flushes the stats header by atomics; 2048 -> 512: -0.05 ms)
+#endif
+#ifndef ISIM_DES_MAX_SPLITS
+#define ISIM_DES_MAX_SPLITS 256u  // (position x trace-range) blocks per position (uncapped -> 256: 35.5 -> 34.8 ms per c5 step)
+#endif
 #ifndef ISIM_DES_SPLIT_TARGET
 #define ISIM_DES_SPLIT_TARGET 8192  // (position x trace-range) blocks per up / step-begin launch
 #endif
@@ -2386,10 +2392,15 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
   const size_t sort_tmp_bytes = sort_temp_bytes(m_max);
   k.sort_pos = L.d_sort_pos;
   // (position or row) x trace-range blocks: enough to fill the chip, >= 256 traces each
+  // and at most ISIM_DES_MAX_SPLITS per position: every block flushes its
+  // histogram and sums into the position's one table row by memory-side
+  // atomics, which serialise per address (a one-position level in 4,096
+  // blocks: ~90 us of atomics for 25 MB of rows)
   auto splits_for = [&](uint32_t width) {
     uint64_t sp = (ISIM_DES_SPLIT_TARGET + width - 1) / width;
     const uint64_t cap = (L.n_traces + 255) / 256;
     sp = sp < cap ? sp : cap;
+    sp = sp < ISIM_DES_MAX_SPLITS ? sp : ISIM_DES_MAX_SPLITS;
     return (uint32_t)(sp ? sp : 1);
   };
   // the plan's variant order (des_plan.cpp): [single fused | single | replicated fused | replicated]
@@ -2589,7 +2600,7 @@ int des_launch(const DesLaunch &L, void *stream_) {
   }
   if (pass(k)) return 1;
   uint64_t fin_blocks = (L.n_traces + kDesUpThreads - 1) / kDesUpThreads;
-  fin_blocks = fin_blocks < 2048 ? fin_blocks : 2048;
+  fin_blocks = fin_blocks < ISIM_DES_FIN_BLOCKS ? fin_blocks : ISIM_DES_FIN_BLOCKS;
   if (narrow) hipLaunchKernelGGL(des_finalize<uint32_t>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
   else hipLaunchKernelGGL(des_finalize<uint64_t>, dim3((uint32_t)fin_blocks), dim3(kDesUpThreads), 0, stream, k);
   if (L.n_slots > 0) {  // executed calls: every trace makes mult[slot] calls through each site
