@@ -31,6 +31,12 @@ constexpr uint32_t kDesFlagFused = 4u;    // fast-path leaf: finished by its que
 constexpr uint32_t kDesFlagParentDur = 8u;
 constexpr uint32_t kDesDurShift = 8;
 constexpr uint32_t kDesDurKids = 8;       // per caller
+// rows are relative to the arrival of the trace's group of kDesGroupTraces
+// (one DPP row of the 32-bit-key queue pass: 16 lanes x kDesN32Per traces);
+// the 32-bit keys need (t - t_group) x hold < 2^31
+constexpr uint32_t kDesN32Per = 4;
+constexpr uint64_t kDesGroupTraces = 16ull * kDesN32Per;
+constexpr uint64_t kDesN32HoldMax = (1ull << 31) / kDesGroupTraces;
 constexpr uint32_t kDesUpChildLds = 1024; // callers with more children record none (their ids are not staged in LDS)
 // non-fused position whose finish needs no start row: one call step, no step
 // begins, and every callee's hop cost at least the step's longest sleep, so
@@ -122,7 +128,7 @@ struct DesPlan {
   std::vector<uint32_t> pipe_pos;    // round order, within a round non-fused first
   std::vector<uint32_t> pipe_dep;    // per pipe_pos: the position whose start row it waits on (kDesNone: none)
   // every pipelined position's holds and offsets fit the 32-bit queue keys
-  // (des.hip down1_chunk_n32: hold < 2^25, off and a leaf's floor < 2^30)
+  // (des.hip down1_chunk_n32: hold < kDesN32HoldMax, off and a leaf's floor < 2^30)
   bool pipe_n32 = false;
   // no step begins and every finish constant (off, floor, post) below 2^30:
   // des_up's finish quads in 32-bit arithmetic (des.hip up_quad32)

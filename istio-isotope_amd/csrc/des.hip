@@ -350,7 +350,9 @@ __device__ __forceinline__ void flag_overflow(const DesK &k, bool bad) {
 }
 
 // the time every row value of trace t is relative to: its group's first arrival
-constexpr uint64_t kDesGrp = 64;
+constexpr uint32_t kN32 = kDesN32Per;            // consecutive traces per thread in the 32-bit-key queue chunks
+constexpr uint64_t kDesGrp = kDesGroupTraces;     // a trace group = one DPP row of the 32-bit-key queue pass
+constexpr uint64_t kN32HoldMax = kDesN32HoldMax;  // (t - t_g) h < 2^31
 __device__ __forceinline__ uint64_t des_gbase(const DesK &k, uint64_t t) { return k.A[t & ~(kDesGrp - 1)]; }
 
 // relative arrival of position v (pp = pos[v]) for trace t
@@ -1084,16 +1086,17 @@ __device__ __forceinline__ int32_t row_max_scan32(int32_t v) {
   return v;
 }
 
-// the finish of one thread's 4 traces with 32-bit keys from the prefix p
+// the finish of one thread's KP traces with 32-bit keys from the prefix p
 // (FULL: all below N; else the traces past N are left out)
-template <bool FUSED, bool FULL = true>
-__device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, int32_t p, const int32_t (&key)[kPer],
-                                                 const uint32_t (&x)[kPer], uint32_t floor32, uint32_t stm,
-                                                 uint32_t (&out)[kPer], uint32_t *hist, const uint8_t *lut, QAcc &q) {
-  uint32_t bin[kPer] = {kNoBin, kNoBin, kNoBin, kNoBin}, big = 0;
+template <bool FUSED, bool FULL, uint32_t KP>
+__device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, int32_t p, const int32_t (&key)[KP],
+                                                 const uint32_t (&x)[KP], uint32_t floor32, uint32_t stm,
+                                                 uint32_t (&out)[KP], uint32_t *hist, const uint8_t *lut, QAcc &q) {
+  uint32_t bin[KP], big = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) {
+  for (uint32_t i = 0; i < KP; ++i) {
     out[i] = 0;
+    bin[i] = kNoBin;
     if (!FULL && base + i >= k.N) continue;
     p = max_i32(p, key[i]);
     const uint32_t w = (uint32_t)p - (uint32_t)key[i];  // the wait S - a (< 2^32: exact)
@@ -1116,51 +1119,126 @@ __device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, i
     out[i] = val;
   }
   q.bad |= (big >> 31) != 0u;
-  if constexpr (FUSED) hist_add4<FULL>(hist, bin);
+  if constexpr (FUSED) {
+#pragma unroll
+    for (uint32_t h = 0; h < KP; h += 4) {
+      const uint32_t b4[4] = {bin[h], bin[h + 1], bin[h + 2], bin[h + 3]};
+      hist_add4<FULL>(hist, b4);
+    }
+  }
+}
+
+// a narrow row's KP values [base, base + KP) of a chunk of kN32 x
+// kDownThreads traces from c0 (16-B accesses; SC1: the pipelined pass's
+// hand-off form, sc1 buffer accesses; past N: per value)
+template <bool SC1, bool FULL, uint32_t KP>
+__device__ __forceinline__ void load_rowk(const uint32_t *p, uint64_t c0, uint64_t base, uint64_t N, uint32_t (&x)[KP]) {
+  if constexpr (FULL) {
+    if constexpr (SC1) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t *>(p + c0), (short)0, (int)(4 * KP * kDownThreads), kRsrcWord3);
+      const uint32_t vo = (uint32_t)(base - c0) * 4u;
+#pragma unroll
+      for (uint32_t h = 0; h < KP; h += 4) {
+        const des_v4u w = __builtin_amdgcn_raw_buffer_load_b128(r, vo + 4 * h, 0, kSc1);
+        x[h] = w.x;
+        x[h + 1] = w.y;
+        x[h + 2] = w.z;
+        x[h + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t h = 0; h < KP; h += 4) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(p + base + h);
+        x[h] = v.x;
+        x[h + 1] = v.y;
+        x[h + 2] = v.z;
+        x[h + 3] = v.w;
+      }
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < KP; ++i)
+      x[i] = base + i < N ? (SC1 ? __hip_atomic_load(p + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : p[base + i])
+                          : 0u;
+  }
+}
+template <bool SC1, bool FULL, uint32_t KP>
+__device__ __forceinline__ void store_rowk(uint32_t *p, uint64_t c0, uint64_t base, uint64_t N, const uint32_t (&x)[KP]) {
+  if constexpr (FULL) {
+    if constexpr (SC1) {
+      const __amdgpu_buffer_rsrc_t r =
+          __builtin_amdgcn_make_buffer_rsrc(p + c0, (short)0, (int)(4 * KP * kDownThreads), kRsrcWord3);
+      const uint32_t vo = (uint32_t)(base - c0) * 4u;
+#pragma unroll
+      for (uint32_t h = 0; h < KP; h += 4) {
+        const des_v4u w = {x[h], x[h + 1], x[h + 2], x[h + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(w, r, vo + 4 * h, 0, kSc1);
+      }
+    } else {
+#pragma unroll
+      for (uint32_t h = 0; h < KP; h += 4) {
+#if ISIM_NT_ROWS
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4u{x[h], x[h + 1], x[h + 2], x[h + 3]}, reinterpret_cast<v4u *>(p + base + h));
+#else
+        *reinterpret_cast<uint4 *>(p + base + h) = make_uint4(x[h], x[h + 1], x[h + 2], x[h + 3]);
+#endif
+      }
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < KP; ++i)
+      if (base + i < N) {
+        if constexpr (SC1) __hip_atomic_store(p + base + i, x[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else p[base + i] = x[i];
+      }
+  }
 }
 
 // down1_chunk for narrow rows (FULL: a whole chunk; ENTRY: the entry, whose
-// group-relative arrival is A_t - G; else the caller's row `par`); `jh0` =
-// (t - t_g) h of the thread's first trace (the caller's per-position
+// group-relative arrival is A_t - G; else the caller's row `par`), kN32
+// consecutive traces per thread: a DPP row (16 lanes) holds one trace group;
+// `jh0` = (t - t_g) h of the thread's first trace (the caller's per-position
 // constant).  The same results as down1_chunk<uint32_t, FUSED, FULL, ...>.
 template <bool FUSED, bool HAND_IN, bool HAND_OUT, bool FULL = true, bool ENTRY = false>
 __device__ __forceinline__ void down1_chunk_n32(const DesK &k, const DesPos &P, uint32_t v, const uint32_t *par,
                                                 uint32_t *out, uint64_t c0, int64_t *wtot, int64_t &carry,
                                                 uint32_t *hist, const uint8_t *lut, QAcc &q, uint32_t chunk,
                                                 uint32_t jh0) {
-  constexpr uint32_t NW = kDownThreads / 64;
+  constexpr uint32_t NW = kDownThreads / 64, KP = kN32;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t N = k.N;
-  uint64_t base = c0 + (uint64_t)threadIdx.x * kPer;
+  uint64_t base = c0 + (uint64_t)threadIdx.x * KP;
   __asm__ volatile("" : "+v"(base));  // (down1_chunk)
-  const uint64_t n = FULL ? base + kPer : N;
   const uint64_t tg = base & ~(kDesGrp - 1);
   const uint64_t g = FULL || tg < N ? k.A[tg] : 0;  // every lane of a group with a trace below N
-  uint32_t x[kPer], xo = 0;
+  uint32_t x[KP], xo = 0;
   if constexpr (ENTRY) {
-    uint64_t at[kPer];
-    load4n<uint64_t>(k.A, base, n, at);
     uint64_t d = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-      const uint64_t r = FULL || base + i < N ? at[i] - g : 0;
+    for (uint32_t i = 0; i < KP; ++i) {
+      const uint64_t r = FULL || base + i < N ? k.A[base + i] - g : 0;
       d |= r;
       x[i] = (uint32_t)r;
     }
     q.bad |= (d >> 31) != 0;
   } else {
-    uint32_t ar[kPer];
-    if constexpr (HAND_IN) load_row_sc1<uint32_t, FULL>(par, c0, base, N, ar);
-    else load4t<uint32_t>(par, base, n, ar);
+    uint32_t ar[KP];
+    load_rowk<HAND_IN, FULL, KP>(par, c0, base, N, ar);
     const uint32_t off32 = (uint32_t)P.off;
 #pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) x[i] = ar[i] + off32;
+    for (uint32_t i = 0; i < KP; ++i) x[i] = ar[i] + off32;
   }
-  const uint32_t stm = FUSED ? des_status4(k, v, base) : 0u;
+  // own error statuses, bit i (base % KP == 0: one status word, nothing past N)
+  const uint32_t stm = FUSED && base < N ? (k.stbits[(uint64_t)v * k.st_wpr + (base >> 5)] >> (base & 31u)) &
+                                               ((1u << KP) - 1u)
+                                         : 0u;
   const uint32_t hold32 = (uint32_t)P.hold;
-  int32_t key[kPer], kt = INT32_MIN;
+  int32_t key[KP], kt = INT32_MIN;
 #pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) {
+  for (uint32_t i = 0; i < KP; ++i) {
     xo |= x[i];
     key[i] = FULL || base + i < N ? (int32_t)(x[i] - (jh0 + i * hold32)) : INT32_MIN;
     kt = max_i32(kt, key[i]);
@@ -1187,18 +1265,25 @@ __device__ __forceinline__ void down1_chunk_n32(const DesK &k, const DesPos &P, 
   const int64_t pr = max_i64(pre, e) - kb;  // the group's prefix, relative
   q.bad |= (FULL || base < N) && pr > (int64_t)INT32_MAX;
   const int32_t p0 = pr < (int64_t)INT32_MIN ? INT32_MIN : pr > (int64_t)INT32_MAX ? INT32_MAX : (int32_t)pr;
-  uint32_t o[kPer];
-  queue_finish_n32<FUSED, FULL>(k, base, max_i32(p0, exc), key, x, (uint32_t)P.floor, stm, o, hist, lut, q);
-  if constexpr (FUSED) track4<uint32_t>(k, out, base, N, o);  // a fused leaf's row is final (F)
-  if constexpr (HAND_OUT) store_row_sc1<uint32_t, FULL>(out, c0, base, N, o);
-  else store4t<uint32_t>(out, base, n, o);
+  uint32_t o[KP];
+  queue_finish_n32<FUSED, FULL, KP>(k, base, max_i32(p0, exc), key, x, (uint32_t)P.floor, stm, o, hist, lut, q);
+  if constexpr (FUSED) {
+    if (k.changed) {  // a fused leaf's row is final (F)
+#pragma unroll
+      for (uint32_t h = 0; h < KP; h += 4) {
+        const uint32_t o4[4] = {o[h], o[h + 1], o[h + 2], o[h + 3]};
+        track4<uint32_t>(k, out, base + h, N, o4);
+      }
+    }
+  }
+  store_rowk<HAND_OUT, FULL, KP>(out, c0, base, N, o);
 }
 
 // whether a position's whole chunks take the 32-bit keys, and the thread's (t - t_g) h
 template <typename T, bool FUSED>
 __device__ __forceinline__ bool n32_ok(const DesPos &P, const void *par, uint32_t &jh0) {
-  jh0 = (threadIdx.x & 15u) * kPer * (uint32_t)P.hold;
-  return sizeof(T) == 4 && par != nullptr && P.hold < (1ull << 25) && P.off < (1ull << 30) &&
+  jh0 = (threadIdx.x & 15u) * kN32 * (uint32_t)P.hold;
+  return sizeof(T) == 4 && par != nullptr && P.hold < kN32HoldMax && P.off < (1ull << 30) &&
          (!FUSED || P.floor < (1ull << 30));
 }
 
@@ -1227,8 +1312,9 @@ __device__ __forceinline__ void down1_body(const DesK &k, uint32_t v) {
   uint32_t jh0;
   if (n32_ok<T, FUSED>(P, par, jh0)) {
     if constexpr (sizeof(T) == 4) {
+      constexpr uint64_t CH32 = (uint64_t)kN32 * kDownThreads;
 #pragma unroll 1
-      for (; c0 + CH <= N; c0 += CH) {
+      for (; c0 + CH32 <= N; c0 += CH32) {
         down1_chunk_n32<FUSED, false, false>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q, 0, jh0);
         buf ^= 1u;
       }
@@ -1531,11 +1617,12 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
   constexpr uint64_t CH = (uint64_t)kPer * kDownThreads;
   uint64_t c0 = 0;
   if constexpr (N32 && sizeof(T) == 4) {
-    const uint32_t jh0 = (threadIdx.x & 15u) * kPer * (uint32_t)P.hold;
+    const uint32_t jh0 = (threadIdx.x & 15u) * kN32 * (uint32_t)P.hold;
+    constexpr uint64_t CH32 = (uint64_t)kN32 * kDownThreads;
     auto chunks = [&](auto entry_t) {
       constexpr bool ENTRY = decltype(entry_t)::value;
 #pragma unroll 1
-      for (; c0 + CH <= N; c0 += CH, ++chunk) {
+      for (; c0 + CH32 <= N; c0 += CH32, ++chunk) {
         wait();
         down1_chunk_n32<FUSED, HAND_IN, HAND_OUT, true, ENTRY>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q,
                                                                chunk, jh0);
@@ -1551,17 +1638,8 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
     if (par) chunks(std::false_type{});
     else chunks(std::true_type{});
   } else {
-    uint32_t jh0;
-    if (n32_ok<T, FUSED>(P, par, jh0)) {
-      if constexpr (sizeof(T) == 4) {
-#pragma unroll 1
-        for (; c0 + CH <= N; c0 += CH, ++chunk) {
-          wait();
-          down1_chunk_n32<FUSED, HAND_IN, HAND_OUT>(k, P, v, par, out, c0, wtot[buf], carry, hist, lut, q, chunk, jh0);
-          buf ^= 1u;
-        }
-      }
-    }
+    // (no 32-bit chunks here: a caller and its callees must count chunks of
+    // one size, and this launch has positions the 32-bit keys do not fit)
 #pragma unroll 1
     for (; c0 + CH <= N; c0 += CH, ++chunk) {
       wait();

@@ -492,7 +492,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   out.pipe_n32 = !out.pipe.empty();
   for (uint32_t v : out.pipe_pos) {
     const DesPos &ps = out.pos[v];
-    out.pipe_n32 = out.pipe_n32 && ps.hold < (1ull << 25) && ps.off < (1ull << 30) &&
+    out.pipe_n32 = out.pipe_n32 && ps.hold < kDesN32HoldMax && ps.off < (1ull << 30) &&
                    (!(ps.flags & kDesFlagFused) || ps.floor < (1ull << 30));
   }
   // finishes without the start row (kDesFlagNoStart; ISIM_DES_NO_NOSTART
