@@ -731,6 +731,15 @@ static bool empty_coll(const Y &y) {
 
 static void emit_node(Emitter &e, const Y &y, int parent_indent, bool in_mapping_value);
 
+// yaml_emitter_check_simple_key (emitterc.go) for a string key: at most 128
+// bytes and no line break; else a complex key ("? key" then ": value")
+static bool simple_key(const std::string &k) {
+  if (k.size() > 128) return false;
+  for (size_t i = 0; i < k.size(); i += utf8_width((unsigned char)k[i]))
+    if (is_break_at(k, i)) return false;
+  return true;
+}
+
 // block mapping whose keys sit at column `indent`
 static void emit_map(Emitter &e, const Y &m, int indent) {
   std::vector<const std::pair<std::string, Y> *> kv;
@@ -738,9 +747,19 @@ static void emit_map(Emitter &e, const Y &m, int indent) {
   std::stable_sort(kv.begin(), kv.end(), [](auto *a, auto *b) { return key_less(a->first, b->first); });
   for (const auto *p : kv) {
     e.write_indent(indent);
-    emit_scalar(e, str(p->first), indent + 2, true);
-    e.indicator(":", false, false, false);
-    emit_node(e, p->second, indent, true);
+    if (simple_key(p->first)) {  // yaml_emitter_emit_block_mapping_key / _value, simple
+      emit_scalar(e, str(p->first), indent + 2, true);
+      e.indicator(":", false, false, false);
+      emit_node(e, p->second, indent, true);
+    } else {
+      // "? " key (breaks allowed), then ": " at the mapping's indent; the
+      // value follows at an indention point, so a sequence there is indented
+      e.indicator("?", true, false, true);
+      emit_scalar(e, str(p->first), indent + 2, false);
+      e.write_indent(indent);
+      e.indicator(":", true, false, true);
+      emit_node(e, p->second, indent, false);
+    }
   }
 }
 

@@ -183,6 +183,16 @@ class _Dumper(yaml.Dumper):
     chosen below with yaml.v2's rules."""
     yaml_implicit_resolvers: Dict[str, Any] = {}
 
+    def check_simple_key(self):
+        """libyaml's (yaml.v2 emitterc.go yaml_emitter_check_simple_key) rule
+        for a scalar key: at most 128 BYTES and not multiline, empty allowed
+        (PyYAML: fewer than 128 characters, not empty)."""
+        if isinstance(self.event, yaml.ScalarEvent):
+            if self.analysis is None:
+                self.analysis = self.analyze_scalar(self.event.value)
+            return len(self.event.value.encode("utf-8")) <= 128 and not self.analysis.multiline
+        return super().check_simple_key()
+
 
 def _repr_str(d: yaml.Dumper, s: str):
     if "\n" in s:

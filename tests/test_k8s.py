@@ -347,3 +347,24 @@ def test_key_order_unicode_classes():
     assert a == b
     block = a.split("nodeSelector:\n", 1)[1].splitlines()[:5]
     assert [ln.strip().split(":")[0] for ln in block] == ["ິ", "a2", "a٣", '"true"', "x²"]
+
+
+def test_complex_keys():
+    """yaml.v2 (libyaml emitterc.go yaml_emitter_check_simple_key) writes a
+    key of more than 128 BYTES as a complex key: "? key" (folded at 80
+    columns), then ": value" at the mapping's indent.  Hand-derived layout."""
+    g, og = _graphs(os.path.join(HERE, "golden", "topologies", "1-service.yaml"))
+    sel = {"x" * 128: "a", "y" * 129: "b", "é" * 64: "c", "é" * 65: "d", ("word " * 30).strip(): "e"}
+    a, b = _both(g, og, service_node_selector=sel, creation_timestamp_s=TS)
+    assert a == b
+    block = a.split("nodeSelector:\n", 1)[1].split("      volumes:", 1)[0]
+    w = "word " * 15
+    assert block == ("        ? " + w.strip() + "\n"  # keyList order: w < x < y < é (letters by code point)
+                     "          " + w.strip() + "\n"
+                     "        : e\n"
+                     "        " + "x" * 128 + ": a\n"
+                     "        ? " + "y" * 129 + "\n"
+                     "        : b\n"
+                     "        " + "é" * 64 + ": c\n"
+                     "        ? " + "é" * 65 + "\n"
+                     "        : d\n")
