@@ -2500,7 +2500,8 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       kp.chain_ticket = tickets + 4 * r + 2;
       bool n32 = false;
       if constexpr (sizeof(T) == 4) {
-        n32 = pl.pipe_n32 && !std::getenv("ISIM_DES_NO_PIPE32");
+        static const bool off = std::getenv("ISIM_DES_NO_PIPE32") != nullptr;  // A/B switch, read once
+        n32 = pl.pipe_n32 && !off;
         if (n32) hipLaunchKernelGGL((des_down_pipe<T, true>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
       }
       if (!n32) hipLaunchKernelGGL((des_down_pipe<T, false>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
@@ -2577,7 +2578,8 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       k.splits = splits_for(width);
       bool n32 = false;
       if constexpr (sizeof(T) == 4) {
-        n32 = pl.up_n32 && !std::getenv("ISIM_DES_NO_UP32");
+        static const bool off = std::getenv("ISIM_DES_NO_UP32") != nullptr;  // A/B switch, read once
+        n32 = pl.up_n32 && !off;
         if (n32) hipLaunchKernelGGL((des_up<T, true>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
       }
       if (!n32) hipLaunchKernelGGL((des_up<T, false>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);

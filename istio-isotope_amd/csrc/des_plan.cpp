@@ -90,7 +90,7 @@ void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes) {
     // needs none and no callee's duration is recorded here, the arrival row
     // when the position records its own durations, the finish row
     reads += q.child_cnt;
-    reads += (q.flags & kDesFlagNoStart) && nd[v] == 0 ? 0 : 1;
+    reads += (q.flags & kDesFlagNoStart) && nd[v] == 0 && q.child_cnt <= kDesUpChildLds ? 0 : 1;
     reads += v && !(q.flags & kDesFlagParentDur) ? 1 : 0;
     writes += 1;
   }
