@@ -442,3 +442,11 @@ def test_group_bases_long_gaps(gpu):
     # 64-trace groups spanning ~1.3 s of arrivals (20 ms mean gap): the
     # group-relative rows and keys near their 32-bit range, ragged batch
     DesCase(_wide_fanout(6, 1, 0.05), 20_000_000).compare(1 << 32, 4099)
+
+
+@pytest.mark.parametrize("mean", [500_000, 3_000_000])
+def test_single_service_with_hold(gpu, mean):
+    # the entry is a fused leaf (its queue pass records its durations;
+    # des_finalize must not add them again), ragged batch
+    doc = {"services": [{"name": "a", "isEntrypoint": True, "errorRate": 0.2, "script": [{"sleep": "1ms"}]}]}
+    DesCase(doc, mean).compare(7, 3001)
