@@ -40,6 +40,9 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "des.h"
+#ifndef ISIM_DES_N32_FOLD
+#define ISIM_DES_N32_FOLD 1  // 32-bit queue finish: waits summed in pairs, duration sums derived, 500s under one branch
+#endif
 #ifndef ISIM_NT_ROWS
 #define ISIM_NT_ROWS 1  // row stores of fused leaves and finishes nontemporal: keep L2 for the A_t re-reads
 #endif
@@ -1092,15 +1095,21 @@ template <bool FUSED, bool FULL, uint32_t KP>
 __device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, int32_t p, const int32_t (&key)[KP],
                                                  const uint32_t (&x)[KP], uint32_t floor32, uint32_t stm,
                                                  uint32_t (&out)[KP], uint32_t *hist, const uint8_t *lut, QAcc &q) {
-  uint32_t bin[KP], big = 0;
+  static_assert(KP % 2 == 0, "waits are summed in pairs");
+  uint32_t bin[KP], wv[KP], big = 0, cnt = 0;
 #pragma unroll
   for (uint32_t i = 0; i < KP; ++i) {
     out[i] = 0;
     bin[i] = kNoBin;
+    wv[i] = 0;
     if (!FULL && base + i >= k.N) continue;
+    if constexpr (!FULL) ++cnt;
     p = max_i32(p, key[i]);
     const uint32_t w = (uint32_t)p - (uint32_t)key[i];  // the wait S - a (< 2^32: exact)
+#if !ISIM_DES_N32_FOLD
     q.wsum += w;
+#endif
+    wv[i] = w;
     q.wmax32 = w > q.wmax32 ? w : q.wmax32;
     uint32_t val = w + x[i];  // S - G (no wrap unless the batch is redone)
     big |= w | val;           // a wait or start at or above 2^31: redone with 64-bit rows
@@ -1108,16 +1117,40 @@ __device__ __forceinline__ void queue_finish_n32(const DesK &k, uint64_t base, i
       const uint32_t F = val + floor32;
       const uint32_t st = (stm >> i) & 1u;
       const uint32_t dur = w + floor32;  // F - a
+#if !ISIM_DES_N32_FOLD
       if (st && !k.quiet) atomicAdd(k.E + base + i, 1u);
       q.n5 += st;
       q.dsum += dur;
       q.d1 += st ? dur : 0u;
+#endif
       bin[i] = st * ISIM_N_PROM + des_prom_bucket32(lut, dur);
       big |= F;
       val = F | (st << 31);
     }
     out[i] = val;
   }
+#if ISIM_DES_N32_FOLD
+  // the sums once per call: a pair of waits fits 32 bits (each is below 2^31,
+  // or `big` redoes the batch with 64-bit rows and these statistics are not
+  // committed); the durations' sum is the waits' plus n x floor; the 500s
+  // (rare: stm is almost always 0 wave-wide) under one branch
+  uint64_t ws = 0;
+#pragma unroll
+  for (uint32_t h = 0; h < KP; h += 2) ws += (uint64_t)(wv[h] + wv[h + 1]);
+  q.wsum += ws;
+  if constexpr (FUSED) {
+    q.dsum += ws + (uint64_t)(FULL ? KP : cnt) * floor32;
+    if (stm) {
+#pragma unroll
+      for (uint32_t i = 0; i < KP; ++i)
+        if ((stm >> i) & 1u) {
+          if (!k.quiet) atomicAdd(k.E + base + i, 1u);
+          q.n5 += 1;
+          q.d1 += wv[i] + floor32;
+        }
+    }
+  }
+#endif
   q.bad |= (big >> 31) != 0u;
   if constexpr (FUSED) {
 #pragma unroll
