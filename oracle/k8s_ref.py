@@ -19,9 +19,14 @@ an implementation independent of the product's (csrc/k8s.cpp) — driven with
 yaml.v2's own choices restated on top: keys in keyList.Less order
 (yaml.v2 sorter.go), strings that yaml.v2's resolve() would read back as
 another type in double quotes, multi-line strings in literal style, numbers
-with strconv.FormatFloat(f, 'g', -1, 64).  Known divergence of PyYAML from
-yaml.v2 (not exercised by the tests): NEL and characters beyond the BMP are
-printable for PyYAML, escaped by yaml.v2.
+with strconv.FormatFloat(f, 'g', -1, 64).  PyYAML departs from libyaml in
+three places; two are replaced here: simple-key length (bytes vs characters,
+`check_simple_key`) and double-quoted folding (libyaml breaks ONLY at a space
+past column 80 and drops that space into the break; PyYAML also breaks right
+after an escape sequence and keeps the space as `\\ `, so
+`write_double_quoted` is libyaml's).  The third is not exercised by the tests:
+in the scalar analysis that picks the style, NEL and characters beyond the BMP
+count as printable for PyYAML but not for yaml.v2.
 
 EXT rules shared with the product (the reference is not deterministic):
 creationTimestamp = the caller's unix seconds (reference: time.Now()); RBAC
@@ -192,6 +197,44 @@ class _Dumper(yaml.Dumper):
                 self.analysis = self.analyze_scalar(self.event.value)
             return len(self.event.value.encode("utf-8")) <= 128 and not self.analysis.multiline
         return super().check_simple_key()
+
+    def write_double_quoted(self, text, split=True):
+        """libyaml's yaml_emitter_write_double_quoted (yaml.v2 emitterc.go):
+        a line is folded ONLY at a single space past best_width that is not the
+        scalar's first or last character; the space becomes the line break and a
+        following space is escaped with a backslash.  PyYAML also breaks right
+        after an escape sequence and keeps the folded space as an escaped
+        break, so its own routine is replaced here."""
+        self.write_indicator('"', True)
+        spaces = False
+        n = len(text)
+        for i, ch in enumerate(text):
+            printable = ('\x20' <= ch <= '\x7E' or (self.allow_unicode and (
+                '\xA0' <= ch <= '\uD7FF' or '\uE000' <= ch <= '\uFFFD')))
+            if not printable or ch in '"\\\x85\u2028\u2029\uFEFF':
+                if ch in self.ESCAPE_REPLACEMENTS:
+                    data = '\\' + self.ESCAPE_REPLACEMENTS[ch]
+                elif ch <= '\xFF':
+                    data = '\\x%02X' % ord(ch)
+                elif ch <= '\uFFFF':
+                    data = '\\u%04X' % ord(ch)
+                else:
+                    data = '\\U%08X' % ord(ch)
+                spaces = False
+            elif ch == ' ':
+                if split and not spaces and self.column > self.best_width and 0 < i < n - 1:
+                    self.write_indent()
+                    data = '\\' if text[i + 1] == ' ' else ''
+                else:
+                    data = ' '
+                spaces = True
+            else:
+                data = ch
+                spaces = False
+            if data:
+                self.column += len(data)
+                self.stream.write(data.encode(self.encoding) if self.encoding else data)
+        self.write_indicator('"', False)
 
 
 def _repr_str(d: yaml.Dumper, s: str):
