@@ -359,16 +359,22 @@ def make_multi(rank, world, local):
     err = ""
     mid = None
     try:
-        mid = Multi.get_id()  # RCCL loads on this rank (rank 0's id is the one used)
+        # every local step that can fail runs here, before the collective
+        # creation: RCCL loads, the device can be selected, an id can be drawn
+        Multi.precheck(local)
+        mid = Multi.get_id()  # rank 0's id is the one used
     except Exception as e:
-        err = f"isim_multi_get_id failed on rank {rank}: {e}"
+        err = f"isim_multi_precheck / isim_multi_get_id failed on rank {rank}: {e}"
     if not agree(mid is not None):
-        print(err or "isim_multi_get_id failed on another rank", file=sys.stderr)
+        print(err or "isim_multi_precheck / isim_multi_get_id failed on another rank", file=sys.stderr)
         return None, "torch.distributed all_reduce (isim_multi_get_id failed)"
     obj = [mid if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     multi = None
     try:
+        # collective; if a peer never enters it (a failure the pre-check could
+        # not see), libisim's non-blocking creation gives up after
+        # ISIM_MULTI_TIMEOUT_S with ECOMM, and the agreement below still runs
         multi = Multi.init_rank(obj[0], world, rank, local)
     except Exception as e:
         err = f"isim_multi_init_rank failed on rank {rank}: {e}"

@@ -83,7 +83,7 @@ func (h *Handler) Serve(device int, begin uint64, recs []TraceRecord) ([]uint64,
 		rp = &recs[0]
 	}
 	rc := C.isim_serve(h.h, C.int(device), C.uint64_t(begin), C.uint64_t(len(recs)), rp,
-		(*C.uint64_t)(unsafe.Pointer(&stats[0])))
+		u64ptr(stats))
 	return stats, lastErr(rc)
 }
 
@@ -134,18 +134,35 @@ func (h *Handler) ServeUnderLoad(device int, begin uint64, meanGapNs uint64, rec
 	}
 	// 32-bit rows; a batch with a latency >= 2^31 ns is rerun with 64-bit rows inside the call
 	rc := C.isim_serve_des(h.h, C.int(device), &p, C.uint64_t(begin), C.uint64_t(len(recs)), rp,
-		(*C.uint64_t)(unsafe.Pointer(&stats[0])), (*C.uint64_t)(unsafe.Pointer(&table[0])))
+		u64ptr(stats), u64ptr(table))
 	return stats, table, lastErr(rc)
 }
 
 type Multi struct{ m *C.isim_multi }
 
+// u64ptr passes an empty slice as NULL (libisim then reports EINVAL) instead
+// of panicking on &s[0].
+func u64ptr(s []uint64) *C.uint64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint64_t)(unsafe.Pointer(&s[0]))
+}
+
 // NewMultiNode drives every listed device from this process (ncclCommInitAll).
 func NewMultiNode(devices []int32) (*Multi, error) {
 	var m *C.isim_multi
+	if len(devices) == 0 {
+		return nil, lastErr(C.isim_multi_init_all(nil, 0, &m)) // libisim's EINVAL and message
+	}
 	rc := C.isim_multi_init_all((*C.int)(unsafe.Pointer(&devices[0])), C.int(len(devices)), &m)
 	return &Multi{m}, lastErr(rc)
 }
+
+// MultiPrecheck makes the local checks of NewMultiRank (RCCL loads, the
+// device can be selected) before the collective creation, so the ranks can
+// agree on them out of band first.
+func MultiPrecheck(device int) error { return lastErr(C.isim_multi_precheck(C.int(device))) }
 
 // MultiID is created on rank 0 and shipped to the other ranks (e.g. over gRPC).
 func MultiID() ([128]byte, error) {
@@ -176,7 +193,7 @@ func (h *Handler) ServeSharded(m *Multi, begin, perRank uint64, recs []TraceReco
 		rp = &recs[0] // n_local * perRank records
 	}
 	rc := C.isim_serve_multi(h.h, m.m, C.uint64_t(begin), C.uint64_t(perRank), rp,
-		(*C.uint64_t)(unsafe.Pointer(&stats[0])))
+		u64ptr(stats))
 	return stats, lastErr(rc)
 }
 

@@ -361,7 +361,16 @@ typedef struct {
 } isim_multi_id;
 /* New communicator id (on ONE process; send its 128 bytes to every rank). */
 ISIM_API int isim_multi_get_id(isim_multi_id *id);
-/* This process is rank `rank` of n_ranks, on HIP device `device` (ncclCommInitRank; collective over the ranks). */
+/* Local checks a rank makes BEFORE the collective creation, so that the
+ * ranks can agree on them out of band first: RCCL loads and `device` can be
+ * selected.  No communication. */
+ISIM_API int isim_multi_precheck(int device);
+/* This process is rank `rank` of n_ranks, on HIP device `device` (ncclCommInitRank; collective over the ranks).
+ * Created non-blocking (ncclCommInitRankConfig, blocking = 0) when RCCL has it, and polled: if the
+ * peers do not all arrive within ISIM_MULTI_TIMEOUT_S seconds (environment, default 600) the
+ * communicator is aborted and ISIM_ECOMM returned.  Collectives and isim_serve_multi's wait are polled
+ * the same way (hipStreamQuery + ncclCommGetAsyncError), so a rank whose peer aborted or never came
+ * returns ISIM_ECOMM instead of waiting forever. */
 ISIM_API int isim_multi_init_rank(const isim_multi_id *id, int n_ranks, int rank, int device, isim_multi **out);
 /* One process, n_devices local devices = ranks 0..n-1 in the order given (ncclCommInitAll). */
 ISIM_API int isim_multi_init_all(const int *devices, int n_devices, isim_multi **out);

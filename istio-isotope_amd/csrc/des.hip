@@ -354,6 +354,11 @@ __device__ __forceinline__ void flag_overflow(const DesK &k, bool bad) {
 
 // the time every row value of trace t is relative to: its group's first arrival
 constexpr uint32_t kN32 = kDesN32Per;            // consecutive traces per thread in the 32-bit-key queue chunks
+// pipe_body's callers and callees hand chunks off by chunk INDEX (st_flag /
+// the wait on a chunk), and the 32-bit and 64-bit branches step through
+// chunks of kN32 and kPer traces per thread: the indices only name the same
+// traces while both sizes agree.
+static_assert(kN32 == kPer, "32-bit and 64-bit queue chunks must cover the same traces");
 constexpr uint64_t kDesGrp = kDesGroupTraces;     // a trace group = one DPP row of the 32-bit-key queue pass
 constexpr uint64_t kN32HoldMax = kDesN32HoldMax;  // (t - t_g) h < 2^31
 __device__ __forceinline__ uint64_t des_gbase(const DesK &k, uint64_t t) { return k.A[t & ~(kDesGrp - 1)]; }

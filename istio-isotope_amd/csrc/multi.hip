@@ -18,7 +18,10 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <mutex>
 #include <new>
 #include <string>
@@ -43,6 +46,8 @@ struct Rccl {
   decltype(&ncclCommInitAll) CommInitAll = nullptr;
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
   decltype(&ncclCommAbort) CommAbort = nullptr;  // optional
+  decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;  // optional: non-blocking init
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;    // optional: polled waits
   decltype(&ncclAllReduce) AllReduce = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
@@ -72,6 +77,8 @@ const Rccl &rccl() {
            sym(r.GroupEnd, "ncclGroupEnd") && sym(r.GetErrorString, "ncclGetErrorString");
     if (!r.ok) r.why = "RCCL library lacks an nccl* entry point";
     (void)sym(r.CommAbort, "ncclCommAbort");
+    (void)sym(r.CommInitRankConfig, "ncclCommInitRankConfig");
+    (void)sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
   });
   return r;
 }
@@ -113,6 +120,16 @@ __global__ void scatter_words(uint64_t *tab, const uint64_t *in, uint32_t rows, 
   if (i < rows) tab[(uint64_t)i * row_words + w] = in[i];
 }
 
+// How long a rank waits for its peers (communicator creation, a collective)
+// before it aborts the communicator and returns ISIM_ECOMM: a peer that failed
+// locally before entering a collective never arrives, and over xGMI nothing
+// else tells the waiting rank.  ISIM_MULTI_TIMEOUT_S (seconds), default 600.
+double multi_timeout_s() {
+  const char *e = std::getenv("ISIM_MULTI_TIMEOUT_S");
+  const double v = e ? std::atof(e) : 0.0;
+  return v > 0 ? v : 600.0;
+}
+
 }  // namespace
 
 struct isim_multi {
@@ -123,6 +140,7 @@ struct isim_multi {
   std::vector<uint64_t *> scratch; // per local device: MAX-word staging of a DES table (grown on demand)
   std::vector<uint64_t> scratch_words;
   bool aborted = false;            // isim_multi_abort: comms aborted, handle only freeable
+  bool nonblocking = false;        // comms created with blocking = 0: calls may return ncclInProgress
   ~isim_multi() {
     const Rccl &R = rccl();
     for (size_t i = 0; i < comms.size(); ++i) {
@@ -141,6 +159,75 @@ int stats_words_of(const isim_handler *h, uint64_t &words, uint32_t &rows) {
   words = info.stats_words;
   rows = (uint32_t)info.n_reachable;
   return ISIM_OK;
+}
+
+// Waits until no local communicator of m is ncclInProgress (a non-blocking
+// communicator's init, or the enqueue of a group), polling
+// ncclCommGetAsyncError; on an asynchronous error or after the timeout the
+// communicator is aborted and ISIM_ECOMM returned.
+int settle(isim_multi *m, const char *what) {
+  const Rccl &R = rccl();
+  if (!m->nonblocking || !R.CommGetAsyncError) return ISIM_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  const double limit = multi_timeout_s();
+  for (;;) {
+    bool pending = false;
+    for (ncclComm_t c : m->comms) {
+      if (!c) continue;
+      ncclResult_t a = ncclSuccess;
+      const ncclResult_t q = R.CommGetAsyncError(c, &a);
+      if (q != ncclSuccess || (a != ncclSuccess && a != ncclInProgress)) {
+        const std::string why = R.GetErrorString(q != ncclSuccess ? q : a);
+        (void)isim_multi_abort(m);
+        return mfail(ISIM_ECOMM, std::string(what) + ": " + why);
+      }
+      pending = pending || a == ncclInProgress;
+    }
+    if (!pending) return ISIM_OK;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      (void)isim_multi_abort(m);
+      return mfail(ISIM_ECOMM, std::string(what) + ": no answer from the peer ranks within ISIM_MULTI_TIMEOUT_S");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+// Waits for the local streams after a collective: hipStreamQuery polled
+// beside ncclCommGetAsyncError, so that a peer that aborted (or never came)
+// ends this rank's wait with ISIM_ECOMM after the timeout instead of a
+// hipStreamSynchronize that never returns.  Returns the first failure.
+int wait_streams(isim_multi *m, const std::vector<void *> &streams) {
+  const Rccl &R = rccl();
+  const auto t0 = std::chrono::steady_clock::now();
+  const double limit = multi_timeout_s();
+  std::vector<bool> done(streams.size(), false);
+  for (;;) {
+    bool all = true;
+    for (size_t i = 0; i < streams.size(); ++i) {
+      if (done[i]) continue;
+      if (hipSetDevice(m->devices[i]) != hipSuccess) return mfail(ISIM_EHIP, "hipSetDevice failed");
+      const hipError_t q = hipStreamQuery((hipStream_t)streams[i]);
+      if (q == hipSuccess) {
+        done[i] = true;
+        continue;
+      }
+      if (q != hipErrorNotReady) return mfail(ISIM_EHIP, std::string("walk or all-reduce failed: ") + hipGetErrorString(q));
+      all = false;
+      if (R.CommGetAsyncError && m->comms[i]) {
+        ncclResult_t a = ncclSuccess;
+        if (R.CommGetAsyncError(m->comms[i], &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
+          (void)isim_multi_abort(m);
+          return mfail(ISIM_ECOMM, std::string("all-reduce: ") + R.GetErrorString(a));
+        }
+      }
+    }
+    if (all) return ISIM_OK;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      (void)isim_multi_abort(m);
+      return mfail(ISIM_ECOMM, "all-reduce: no answer from the peer ranks within ISIM_MULTI_TIMEOUT_S");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
 }
 
 }  // namespace
@@ -170,9 +257,21 @@ int isim_multi_init_rank(const isim_multi_id *id, int n_ranks, int rank, int dev
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   ncclComm_t c = nullptr;
-  const ncclResult_t e = R.CommInitRank(&c, n_ranks, u, rank);
+  // non-blocking when RCCL offers it: the creation is polled with a timeout,
+  // so a peer that failed before reaching its own init cannot hold this rank
+  // inside ncclCommInitRank forever
+  const bool nb = R.CommInitRankConfig && R.CommGetAsyncError;
+  ncclResult_t e;
+  if (nb) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    e = R.CommInitRankConfig(&c, n_ranks, u, rank, &cfg);
+  } else {
+    e = R.CommInitRank(&c, n_ranks, u, rank);
+  }
   (void)hipSetDevice(prev);
-  if (e != ncclSuccess) {
+  if (e != ncclSuccess && !(nb && e == ncclInProgress)) {
+    if (c && R.CommAbort) (void)R.CommAbort(c);
     delete m;
     return mfail(ISIM_ECOMM, std::string("ncclCommInitRank: ") + R.GetErrorString(e));
   }
@@ -182,6 +281,11 @@ int isim_multi_init_rank(const isim_multi_id *id, int n_ranks, int rank, int dev
   m->comms = {c};
   m->scratch = {nullptr};
   m->scratch_words = {0};
+  m->nonblocking = nb;
+  if (const int rc = settle(m, "ncclCommInitRank")) {
+    delete m;
+    return rc;
+  }
   *out = m;
   return ISIM_OK;
 }
@@ -212,6 +316,18 @@ int isim_multi_init_all(const int *devices, int n_devices, isim_multi **out) {
 }
 
 void isim_multi_free(isim_multi *m) { delete m; }
+
+int isim_multi_precheck(int device) {
+  if (device < 0) return mfail(ISIM_EINVAL, "bad argument");
+  const Rccl &R = rccl();
+  if (!R.ok) return mfail(ISIM_ECOMM, R.why);
+  int prev = 0;
+  HIPCHK(hipGetDevice(&prev));
+  const hipError_t e = hipSetDevice(device);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return mfail(ISIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return ISIM_OK;
+}
 
 int isim_multi_abort(isim_multi *m) {
   if (!m) return mfail(ISIM_EINVAL, "null argument");
@@ -257,9 +373,13 @@ int isim_stats_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *
     GRPCHK(R.AllReduce(s + lo, s + lo, hi - lo, ncclUint64, ncclMax, m->comms[i], st));
     GRPCHK(R.AllReduce(s + hi, s + hi, words - hi, ncclUint64, ncclSum, m->comms[i], st));
   }
-  GRPCHK(R.GroupEnd());
-  (void)hipSetDevice(prev);
-  return ISIM_OK;
+  {
+    const ncclResult_t e = R.GroupEnd();
+    (void)hipSetDevice(prev);
+    if (e != ncclSuccess && !(m->nonblocking && e == ncclInProgress))
+      return mfail(ISIM_ECOMM, std::string("ncclGroupEnd: ") + R.GetErrorString(e));
+  }
+  return settle(m, "stats all-reduce");
 }
 
 int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *m, uint64_t *const *d_tables,
@@ -296,7 +416,17 @@ int isim_des_table_allreduce_device(const isim_handler *h, isim_multi *m, uint64
     GRPCHK(R.AllReduce(d_tables[i], d_tables[i], (size_t)rows * W, ncclUint64, ncclSum, m->comms[i], st));
     GRPCHK(R.AllReduce(m->scratch[i], m->scratch[i], rows, ncclUint64, ncclMax, m->comms[i], st));
   }
-  GRPCHK(R.GroupEnd());
+  {
+    const ncclResult_t e = R.GroupEnd();
+    if (e != ncclSuccess && !(m->nonblocking && e == ncclInProgress)) {
+      (void)hipSetDevice(prev);
+      return mfail(ISIM_ECOMM, std::string("ncclGroupEnd: ") + R.GetErrorString(e));
+    }
+  }
+  if (const int rc = settle(m, "DES table all-reduce")) {
+    (void)hipSetDevice(prev);
+    return rc;
+  }
   for (size_t i = 0; i < m->devices.size(); ++i) {
     HIPCHK(hipSetDevice(m->devices[i]));
     hipStream_t st = hip_streams ? (hipStream_t)hip_streams[i] : nullptr;
@@ -341,9 +471,11 @@ int isim_serve_multi(isim_handler *h, isim_multi *m, uint64_t trace_begin, uint6
   // peer ranks' all-reduce fails (ECOMM) instead of waiting for this rank
   if (rc != ISIM_OK && m->n_ranks > (int)L) (void)isim_multi_abort(m);
   if (rc == ISIM_OK) rc = isim_stats_allreduce_device(h, m, d_stats.data(), streams.data());
+  // polled, not hipStreamSynchronize: a peer that aborted ends the wait (ECOMM)
+  if (rc == ISIM_OK) rc = wait_streams(m, streams);
   for (size_t i = 0; i < L && rc == ISIM_OK; ++i) {
-    if (hipSetDevice(m->devices[i]) != hipSuccess || hipStreamSynchronize((hipStream_t)streams[i]) != hipSuccess) {
-      rc = mfail(ISIM_EHIP, "walk or all-reduce failed");
+    if (hipSetDevice(m->devices[i]) != hipSuccess) {
+      rc = mfail(ISIM_EHIP, "hipSetDevice failed");
       break;
     }
     if (i == 0 && h_stats && hipMemcpy(h_stats, d_stats[0], words * 8, hipMemcpyDeviceToHost) != hipSuccess)

@@ -79,6 +79,11 @@ class Multi:
         self.n_ranks, self.n_local, self.first_rank = n.value, loc.value, first.value
 
     @staticmethod
+    def precheck(device: int) -> None:
+        """isim_multi_precheck: RCCL loads and `device` can be selected (local, no communication)."""
+        native.check(native.load().isim_multi_precheck(device))
+
+    @staticmethod
     def get_id() -> bytes:
         mid = native.MultiId()
         native.check(native.load().isim_multi_get_id(C.byref(mid)))

@@ -18,7 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 from dataclasses import dataclass, field
-from typing import Optional, Any, List, Optional
+from typing import Any, List, Optional
 
 from . import native
 from .yamljson import yaml_to_json

@@ -123,7 +123,7 @@ def test_shard_ranges_partition():
     assert ids == list(range(world * steps * batch))
 
 
-def _make_multi_worker(rank, world, port, scenario, q):
+def _make_multi_worker(rank, world, port, scenario, q, arrived):
     """bench.make_multi's collective choice with a stand-in for isim.dist.Multi
     (no RCCL on a CPU): every rank must come out with the same decision."""
     import sys
@@ -138,6 +138,11 @@ def _make_multi_worker(rank, world, port, scenario, q):
         closed = False
 
         @staticmethod
+        def precheck(local):
+            if scenario == "precheck_fails_on_1" and rank == 1:
+                raise RuntimeError("hipSetDevice")
+
+        @staticmethod
         def get_id():
             if scenario == "id_fails_on_1" and rank == 1:
                 raise RuntimeError("no RCCL here")
@@ -145,8 +150,17 @@ def _make_multi_worker(rank, world, port, scenario, q):
 
         @staticmethod
         def init_rank(mid, w, r, local):
-            if scenario == "init_fails_on_0" and r == 0:
+            # ncclCommInitRank is collective: a rank returns only once every
+            # rank has entered it, or (libisim's non-blocking creation) with
+            # ECOMM after ISIM_MULTI_TIMEOUT_S, modelled here as 3 s
+            if scenario == "init_fails_on_0" and r == 0:  # entered, then failed: the peer got its comm
+                arrived[r].set()
                 raise RuntimeError("ncclCommInitRank")
+            if scenario == "init_local_fails_on_0" and r == 0:
+                raise RuntimeError("local failure before entering ncclCommInitRank")
+            arrived[r].set()
+            if not all(e.wait(timeout=3.0) for e in arrived):
+                raise RuntimeError("ISIM_ECOMM: no answer from the peer ranks within ISIM_MULTI_TIMEOUT_S")
             return FakeMulti()
 
         def close(self):
@@ -158,16 +172,21 @@ def _make_multi_worker(rank, world, port, scenario, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scenario", ["ok", "id_fails_on_1", "init_fails_on_0"])
+@pytest.mark.parametrize("scenario", ["ok", "id_fails_on_1", "precheck_fails_on_1", "init_fails_on_0",
+                                      "init_local_fails_on_0"])
 def test_make_multi_is_collective(scenario):
-    """a local failure on one rank (loading RCCL / drawing the
-    id, or creating the communicator) sends EVERY rank to the torch.distributed
-    merge, and a rank that did create a communicator frees it."""
+    """ADVICE rounds 2-3: a local failure on one rank (loading RCCL, selecting
+    the device, drawing the id, or creating the communicator) sends EVERY rank
+    to the torch.distributed merge, and a rank that did create a communicator
+    frees it.  init_local_fails_on_0: rank 0 fails before it enters the
+    collective creation; rank 1 waits inside it until the (modelled) timeout,
+    then both agree on the fallback."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_make_multi_worker, args=(r, world, port, scenario, q)) for r in range(world)]
+    arrived = [ctx.Event() for _ in range(world)]
+    procs = [ctx.Process(target=_make_multi_worker, args=(r, world, port, scenario, q, arrived)) for r in range(world)]
     for p in procs:
         p.start()
     got = sorted(q.get(timeout=300) for _ in range(world))

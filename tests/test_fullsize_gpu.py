@@ -182,6 +182,8 @@ def test_config3_bench_batch(gpu):
     assert np.all(f["site_calls"] == n * L)
     _launch_edge_windows(c, rec, begin, n, L)
     _sampled_windows(c, rec, begin, n * L, windows=6, seed=3)
+    # the full stats (per service, per site, svc_dur) of an oracle-sized window through the same handler
+    c.compare(begin + 3 * n // 2, 1 << 14)
 
 
 def test_config3_bench_batch_mode_b(gpu):
@@ -199,6 +201,7 @@ def test_config3_bench_batch_mode_b(gpu):
     assert 0.2 < f["n_500"] / (n * L) < 0.8
     _launch_edge_windows(c, rec, begin, n, L)
     _sampled_windows(c, rec, begin, n * L, windows=4, seed=4)
+    c.compare(begin + 3 * n // 2, 1 << 14)
 
 
 def test_config4_bench_batch(gpu):

@@ -126,3 +126,88 @@ def test_two_ranks_product_shards_merge_to_union(gpu, kind):
             assert np.array_equal(r, urec[b:b + batch]), (rank, s)
     # and the host merge of the two ranks' merged-per-step buffers is the same rule
     assert np.array_equal(stats_merge(h, np.zeros_like(ust), ust), ust)
+
+
+def test_precheck(gpu):
+    """isim_multi_precheck: the local steps a rank agrees on before the
+    collective creation (RCCL loads, the device can be selected)."""
+    Multi.precheck(0)
+    with pytest.raises(isim.IsimError):
+        Multi.precheck(4096)  # no such device: EHIP, no communication attempted
+
+
+_LONE_RANK = r"""
+import os, sys, time
+sys.path[:0] = [os.environ["ISIM_ROOT"], os.path.join(os.environ["ISIM_ROOT"], "istio-isotope_amd")]
+import isim
+from isim import native
+from isim.dist import Multi
+os.environ["ISIM_MULTI_TIMEOUT_S"] = "5"
+t0 = time.time()
+try:
+    Multi.init_rank(Multi.get_id(), 2, 0, 0)   # rank 1 never comes
+    print("CREATED")
+except isim.IsimError as e:
+    print("ERR", e.code, round(time.time() - t0, 1), e)
+"""
+
+
+def test_init_rank_times_out_without_peer(gpu):
+    """a rank whose peer never enters ncclCommInitRank (it
+    failed locally first) must not wait forever: libisim creates the
+    communicator non-blocking and gives up after ISIM_MULTI_TIMEOUT_S with
+    ISIM_ECOMM.  Run in a child process under a hard limit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ISIM_ROOT=root)
+    out = subprocess.run([sys.executable, "-c", _LONE_RANK], env=env, capture_output=True, text=True, timeout=90)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith(("ERR", "CREATED"))]
+    assert line, out.stdout + out.stderr
+    parts = line[0].split()
+    assert parts[0] == "ERR" and int(parts[1]) == isim.ECOMM, line[0]
+    assert 4.0 <= float(parts[2]) < 60.0, line[0]
+
+
+def _abort_worker(rank, world, port, q):
+    import torch  # noqa: F401  (RCCL from torch's bundle, as in bench.py)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ISIM_MULTI_TIMEOUT_S="60")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    obj = [Multi.get_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    m = Multi.init_rank(obj[0], world, rank, rank)
+    dist.barrier()
+    h = _handler("static")
+    try:
+        if rank == 0:
+            m.abort()  # a local failure before the collective
+            q.put((rank, "aborted"))
+        else:
+            m.serve(h, 0, 4096)
+            q.put((rank, "no error"))
+    except isim.IsimError as e:
+        q.put((rank, e.code))
+    m.close()
+    dist.destroy_process_group()
+
+
+def test_peer_abort_returns_ecomm(gpu):
+    """rank 0 aborts the communicator before the stats
+    all-reduce; rank 1, which walked its shard and entered the collective,
+    returns ISIM_ECOMM (polled wait) instead of hanging.  Needs two GPUs
+    (RCCL refuses two ranks on one device); skipped on the one-GPU box."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_abort_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got[0] == "aborted" and got[1] == isim.ECOMM, got
