@@ -45,6 +45,9 @@ BENCH_BATCH = {
     # workgroup's LDS, the flush, the tail) amortises further: 2^24 / 2^25
     # / 2^26 traces per launch 5.82 / 6.06 / 6.23 G traces/s (1 GB of records)
     "c4": 1 << 26,
+    # config 3's graph with a probability on every call: the lane tree walk
+    # over a 10,000-position tree
+    "c3p": 1 << 22,
     # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
     # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
     # the pipelined queue pass's fill and drain (2^16 20.8,
@@ -61,7 +64,10 @@ def parse():
     # 2^24 traces (256 MB of records) per launch: the per-launch flush and
     # tail amortise (config 3: 2^22 335, 2^23 339, 2^24 340 M traces/s)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c4", "c5"])
+    ap.add_argument("--prob", type=int, default=50, help="c3p: the probability on every call (1..99)")
+    ap.add_argument("--no-wave-leg", action="store_true",
+                    help="c3p: skip the wave-interpreter leg (kinds 2/3, ISIM_FLAG_WAVE_WALK) on the same graph")
     ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
                     "fill the records (the library default) instead of walking every trace")
     ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
@@ -81,8 +87,8 @@ def parse():
     return args
 
 
-def build_graph(config: str):
-    from isim.generators import config2_topology, config3_topology, mesh_topology
+def build_graph(config: str, prob: int = 50):
+    from isim.generators import config2_topology, config3_topology, config3p_topology, mesh_topology
     from isim.yamljson import obj_to_json, yaml_to_json
     if config == "c1":
         j = yaml_to_json(open(os.path.join(ROOT, "tests", "golden", "topologies", "canonical.yaml"), "rb").read())
@@ -97,6 +103,11 @@ def build_graph(config: str):
         j = obj_to_json(mesh_topology())
         desc = {"workload": "100k-service 8-layer mesh, fan-out 3 at probability 30, numReplicas + responseSize",
                 "services": 100000}
+    elif config == "c3p":
+        j = obj_to_json(config3p_topology(prob))
+        desc = {"workload": f"config 3's 10k-service graph with probability {prob} on every call (the reference "
+                            "runtime's only randomness, executable.go:84-90): dynamic walk, lane tree walk",
+                "services": 10000, "probability": prob}
     elif config == "c5":
         j = obj_to_json(config3_topology())
         desc = {"workload": "config 3's 10k-service graph + per-replica worker-pool contention: open-loop Poisson "
@@ -541,7 +552,7 @@ def main():
         multi, merge_label = make_multi(rank, world, local)
     else:
         multi, merge_label = None, f"torch.distributed all_reduce ({backend} rehearsal)"
-    json_text, desc = build_graph(args.config)
+    json_text, desc = build_graph(args.config, args.prob)
     # every trace is walked unless --fill: a draw-free static walk (config 2)
     # is otherwise walked once and filled, which is not a walk rate
     params = isim.SimParams(error_mode=isim.MODE_B if args.mode == "B" else isim.MODE_A,
@@ -615,6 +626,9 @@ def main():
     }
     if args.config == "c3" and args.mode == "A" and not args.no_mode_b:
         line.update(mode_b_legs(args, json_text, rank, world, dev, multi))
+    if args.config == "c3p" and not args.no_wave_leg:
+        line["wave_walk"] = wave_walk_leg(args, json_text, params, rank, world, dev, multi)
+        line["speedup_vs_wave_walk"] = value / line["wave_walk"]["value"]
     if rank == 0 and world == 1 and not args.no_cpu:
         # config 1 is defined on the CPU interpreter: time it on the whole
         # 1M-trace workload; other configs on a bounded sample
@@ -626,6 +640,30 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         teardown(multi)
+
+
+def wave_walk_leg(args, json_text, params, rank, world, dev, multi=None):
+    """The same dynamic walk on the round-1 wave interpreter (kinds 2/3,
+    ISIM_FLAG_WAVE_WALK: a wave walks its 64 traces in lock step over the
+    union of their call paths), at a smaller batch: the rate the lane tree
+    walk replaces."""
+    import numpy as np
+    import torch
+
+    import isim
+    p = isim.SimParams(error_mode=params.error_mode, flags=params.flags | isim.native.FLAG_WAVE_WALK)
+    h = isim.Handler(isim.ServiceGraph.from_json(json_text), None, p)
+    B = max(1 << 16, args.batch >> 4)
+    stats = torch.zeros(h.info.stats_words, dtype=torch.int64, device=dev)
+    recs = None if args.no_records else torch.empty((B, 2), dtype=torch.int64, device=dev)
+    steps = 3
+    elapsed, kern_ms = time_walk(h, steps, 1, B, recs, stats, rank, world, dev, multi)
+    f = h.fold(stats.cpu().numpy().view(np.uint64))
+    total = steps * B * world
+    assert f["n_traces"] == total
+    return {"value": total / elapsed, "unit": "traces/s", "batch": B, "steps": steps, "kernel_ms": kern_ms,
+            "kernel_kind": h.launch_info(torch.cuda.current_device())["kernel_kind"],
+            "hop_visits_per_trace": f["sum_hops"] / total}
 
 
 def c1_error_path(args, json_text, params, rank, world, dev, multi=None):

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -75,8 +76,12 @@ struct DevState {
   uint32_t *d_des_pipe = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
   isim::TreeExt *d_tree_ext = nullptr;  // kind 7: per position (the nodes are d_prog)
+  isim::TreeStep *d_tree_step = nullptr;   // kind 7: per position, the rare step facts
   isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
-  bool tree_ext_lds = false;            // kind 7: TreeExt copied to LDS
+  uint32_t *d_sum_row = nullptr;        // kind 7: per LDS sum index, its row
+  uint32_t *d_slot_tc = nullptr;        // kind 7: per slot, the leaf callee's latency
+  uint32_t *d_spill = nullptr;          // kind 7: frames below the register stack
+  uint32_t spill_lanes = 0;
 };
 
 void free_dev(DevState &d) {
@@ -85,7 +90,8 @@ void free_dev(DevState &d) {
                   d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
                   (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
                   (void *)d.d_des_pipe,
-                  d.d_des_ext, d.d_des_steps, (void *)d.d_tree_ext, (void *)d.d_tree_dyn})
+                  d.d_des_ext, d.d_des_steps, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
+                  (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill})
     if (q) (void)hipFree(q);
   d = DevState();
 }
@@ -203,27 +209,36 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B)
     st.kind = (h->params.flags & ISIM_FLAG_BIT_STACK) ? (p.max_depth <= 32 ? 5u : 4u) : 6u;
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
-  // dynamic walks: the lane tree walk (kind 7) when the unrolled tree and its
-  // LDS tables fit (one 1024-thread workgroup per CU); else the wave walk
+  // dynamic walks: the lane tree walk (kind 7) when the unrolled tree was
+  // built and its LDS layout placed (program.cpp place_tree); else the wave walk
   bool tree = false;
-  if (!p.static_walk && !p.tree_nodes.empty() && !(h->params.flags & ISIM_FLAG_WAVE_WALK)) {
-    const uint32_t P = (uint32_t)p.tree_nodes.size(), S = (uint32_t)p.n_slots, R = (uint32_t)p.row_svc.size();
-    // the TreeExt records in LDS too when they fit (their reads are on the
-    // per-lane dependency chain; from HBM they left the waves waiting)
-    const uint32_t D = p.tree_dyn_words;
-    bool ext_lds = isim::tree_lds_bytes(P, S, R, D, true) <= lds_max;
-    if (const char *e = std::getenv("ISIM_TREE_EXT_HBM"); e && e[0] == '1') ext_lds = false;  // A/B experiments
-    const uint32_t need = isim::tree_lds_bytes(P, S, R, D, ext_lds);
-    if (need <= lds_max) {
-      tree = true;
-      st.kind = 7;
-      st.tree_ext_lds = ext_lds;
-      st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames, ext_lds,
-                                    (p.tree_flags & isim::kTreeAnyConc) != 0);
-      st.threads = isim::kWgThreads;
-      st.lds_bytes = need;
-      st.lds_counters = 1;
+  if (!p.static_walk && !p.tree_nodes.empty() && !(h->params.flags & ISIM_FLAG_WAVE_WALK) &&
+      p.tree_layout.bytes <= lds_max) {
+    tree = true;
+    st.kind = 7;
+    st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames,
+                                  p.tree_frames > isim::kTreeRegFrames, p.tree_layout.nodes_lds != 0,
+                                  (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0);
+    st.lds_bytes = p.tree_layout.bytes;
+    st.lds_counters = 1;
+    // the workgroup size with the most resident waves per CU (registers and
+    // the LDS layout both bound it: two 768-thread workgroups = 24 waves when
+    // the kernel fits 80 VGPRs and the layout half the LDS); ISIM_TREE_THREADS
+    // forces one (A/B experiments)
+    HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)st.lds_bytes));
+    uint32_t best_t = isim::kWgThreads, best_res = 0;
+    for (uint32_t t : {1024u, 768u, 512u}) {
+      int pc = 0;
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, (const void *)st.kernel, (int)t, st.lds_bytes));
+      if ((uint32_t)pc * t / 64u > best_res) {
+        best_res = (uint32_t)pc * t / 64u;
+        best_t = t;
+      }
     }
+    if (const char *e = std::getenv("ISIM_TREE_THREADS"); e && std::atoi(e) >= 64)
+      best_t = std::min<uint32_t>(isim::kWgThreads, (uint32_t)std::atoi(e) & ~63u);
+    st.threads = best_t;
   }
   if (!p.static_walk && !tree) {
     // dynamic walks keep per-lane frame stacks in LDS (waves x frames x 64
@@ -279,9 +294,16 @@ int build_device(isim_handler *h, int device, DevState &st) {
   HIPCHK(hipMemcpy(st.d_prog, src, bytes, hipMemcpyHostToDevice));
   if (tail) HIPCHK(hipMemset((char *)st.d_prog + bytes, 0, tail));
   if (tree) {
-    HIPCHK(hipMalloc(&st.d_tree_ext, p.tree_ext.size() * sizeof(isim::TreeExt)));
-    HIPCHK(hipMemcpy(st.d_tree_ext, p.tree_ext.data(), p.tree_ext.size() * sizeof(isim::TreeExt),
-                     hipMemcpyHostToDevice));
+    auto up = [&](auto *&dst, const auto &v) -> int {
+      using T = typename std::decay_t<decltype(v)>::value_type;
+      HIPCHK(hipMalloc(&dst, std::max<size_t>(1, v.size()) * sizeof(T)));
+      if (!v.empty()) HIPCHK(hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+      return ISIM_OK;
+    };
+    if (const int rc = up(st.d_tree_ext, p.tree_ext)) return rc;
+    if (const int rc = up(st.d_tree_step, p.tree_step)) return rc;
+    if (const int rc = up(st.d_sum_row, p.sum_row)) return rc;
+    if (const int rc = up(st.d_slot_tc, p.slot_tc)) return rc;
     HIPCHK(hipMalloc(&st.d_tree_dyn, std::max<size_t>(1, p.tree_dyn.size()) * sizeof(isim::TreeDynRow)));
     if (!p.tree_dyn.empty())
       HIPCHK(hipMemcpy(st.d_tree_dyn, p.tree_dyn.data(), p.tree_dyn.size() * sizeof(isim::TreeDynRow),
@@ -324,7 +346,14 @@ int build_device(isim_handler *h, int device, DevState &st) {
   // that no workgroup can count past 2^32 at one site (traces x calls
   // through the site per trace)
   st.max_mult = std::max<uint64_t>(1, p.hops_upper);
-  if (tree) st.max_mult = std::max<uint32_t>(1, p.tree_mult);
+  if (tree) {
+    st.max_mult = std::max<uint32_t>(1, p.tree_mult);
+    if (p.tree_frames > isim::kTreeRegFrames) {  // the spill area: frames below the 8 register frames
+      st.spill_lanes = st.max_blocks * st.threads;
+      const size_t words = (size_t)(p.tree_frames - 8u) * isim::kTreeSpillWords * st.spill_lanes;
+      HIPCHK(hipMalloc(&st.d_spill, words * sizeof(uint32_t)));
+    }
+  }
   if (is_stream(st.kind)) {
     st.max_mult = 1;
     for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
@@ -565,12 +594,18 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.close_slot = st->d_close_slot;
   kp.close_end = st->d_close_end;
   kp.tree_ext = st->d_tree_ext;
+  kp.tree_step = st->d_tree_step;
   kp.tree_dyn = st->d_tree_dyn;
+  kp.sum_row = st->d_sum_row;
+  kp.slot_tc = st->d_slot_tc;
+  kp.spill = st->d_spill;
+  kp.spill_lanes = st->spill_lanes;
   kp.n_pos = (uint32_t)h->prog.tree_nodes.size();
   kp.n_rows = (uint32_t)h->prog.row_svc.size();
   kp.n_dyn = (uint32_t)h->prog.tree_dyn.size();
   kp.dyn_words = h->prog.tree_dyn_words;
   kp.tree_flags = h->prog.tree_flags;
+  kp.lay = h->prog.tree_layout;
   const uint64_t per_wave = is_stream(st->kind) ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;

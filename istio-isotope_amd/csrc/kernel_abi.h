@@ -74,15 +74,21 @@ constexpr uint32_t kDurRowMask = 0xFFFFFFu;
 // invocation tree unrolled over every POTENTIAL invocation (each reachable
 // call command, probabilistic or not) in preorder; a trace walks it on its
 // own lane, skipping the subtree of a call its draw skips.  Position 0 is the
-// entry.  Nodes live in LDS (16 B); the rest of a position in HBM (TreeExt).
+// entry.  What every visit of a position needs (TreeNode, 8 B) lives in LDS
+// when it fits, else is read from global memory (L2-resident); what an
+// executed position needs (TreeExt, 16 B) and the rare step facts (TreeStep)
+// are read from global memory.
 enum TreeFlag : uint8_t {
   TF_STEP = 1,        // first call of its step in the caller's script (the step begins here)
   TF_CONC = 2,        // the step is concurrent
   TF_LEAF = 4,        // the callee makes no calls
   TF_ERR_ALWAYS = 8,  // callee errorRate 1
-  TF_ERR_DRAW = 16,   // 0 < callee errorRate < 1: draw against thr
+  TF_ERR_DRAW = 16,   // 0 < callee errorRate < 1: draw against TreeExt.thr
   TF_PROBK0 = 32,     // the callee's script has a probabilistic call among its first 4 calls (its skip
                       // residues, Philox block (t, hop, 1, 0), are drawn when it opens)
+  TF_XPRE = 64,       // TF_STEP: the step begin adds TreeStep.pre (mode B; mode A folds every step's pre
+                      // into the caller's TreeExt.tc: without aborts every step runs)
+  TF_XCMAX = 128,     // TF_STEP|TF_CONC: the concurrent step starts at TreeStep.cmax0 (its longest sleep)
 };
 // Program.tree_flags / KParams.tree_flags: what the walk contains
 constexpr uint32_t kTreeAnyProb = 1;  // some position is a probabilistic call
@@ -95,29 +101,58 @@ struct TreeNode {
   uint8_t prob;    // 1..99: draw to skip; 0: always called
   uint8_t flags;   // TF_*
   uint16_t slot;   // stats slot of the call site
-  uint32_t thr;    // callee error threshold (TF_ERR_DRAW)
-  uint32_t pre;    // TF_STEP: time the caller spends between its previous call step and this step
 };
-static_assert(sizeof(TreeNode) == 16, "TreeNode must be 16 bytes");
+static_assert(sizeof(TreeNode) == 8, "TreeNode must be 8 bytes");
 struct TreeExt {
   uint32_t H;      // hop cost of the call
-  uint32_t tc;     // leaf callee: its latency; else the time after its last call step
-  uint32_t cmax0;  // TF_STEP|TF_CONC: the longest sleep sub-command of the step
-  uint32_t row;    // callee duration-table row (bits 0-15) | LDS word offset of the row's bucket table
-                   // (bits 16-31; kTreeStaticRow: the row's duration bucket never varies)
+  uint32_t tc;     // leaf callee: its latency; else the time after its last call step (mode A: + the
+                   // pre of every call step of its script)
+  uint32_t row;    // non-leaf callee: index (bits 0-15) | placement (bits 16-31): the LDS word offset of
+                   // the row's bucket table, kTreeStaticRow, kTreeGlobalDyn or kTreeGlobalStatic
+  uint32_t thr;    // callee error threshold (TF_ERR_DRAW)
 };
 static_assert(sizeof(TreeExt) == 16, "TreeExt must be 16 bytes");
-constexpr uint32_t kTreeDynBucket = 0xFFu;   // slot_tbkt: the callee's bucket varies per invocation
-constexpr uint32_t kTreeStaticRow = 0xFFFFu;
-// A row whose invocation durations span several duration buckets
-// (prom_bucket(tmin) < prom_bucket(tmax)) counts them in an LDS table of the
-// workgroup: a header word (b_lo | width << 8), then [code 200|500][width]
-// u32 counts of buckets b_lo .. b_lo + width - 1; flushed once per workgroup.
+struct TreeStep {
+  uint32_t pre;    // TF_XPRE: time the caller spends between its previous call step and this step
+  uint32_t cmax0;  // TF_XCMAX: the longest sleep sub-command of the concurrent step
+};
+static_assert(sizeof(TreeStep) == 8, "TreeStep must be 8 bytes");
+// Placement of a non-leaf callee's duration row (TreeExt.row bits 16-31).  In
+// LDS (a sum index in bits 0-15): its code-200 duration sum, and when its
+// bucket varies (prom_bucket(tmin) < prom_bucket(tmax)) a bucket table of the
+// workgroup: a header word (b_lo | width << 8), then [code 200|500][width] u32
+// counts; flushed once per workgroup.  In global memory (the duration-table
+// row in bits 0-15; rows the LDS budget does not hold, coldest first): sums,
+// and buckets when they vary, by global atomics per response.  A static
+// bucket follows from the slot counters at the flush.
+constexpr uint32_t kTreeStaticRow = 0xFFFFu;     // LDS sum, static bucket
+constexpr uint32_t kTreeGlobalDyn = 0xFFFEu;     // global sum and bucket
+constexpr uint32_t kTreeGlobalStatic = 0xFFFDu;  // global sum, static bucket
+constexpr uint32_t kTreeDynBucket = 0xFFu;       // slot_tbkt: the callee's bucket varies per invocation
+constexpr uint32_t kTreeLeafSlot = 1u << 23;     // slot_tbkt: the callee is a leaf (sums from the counters)
+constexpr uint32_t kTreeRowMask = 0xFFFFu;       // slot_tbkt / sum_row: the row (tree programs: < 2^16 rows)
 struct TreeDynRow {
   uint32_t row, off, b_lo, width;  // off: word offset of the header in the LDS tables
 };
 constexpr uint32_t kTreeMaxPositions = 0xFFFFu;  // u16 sizes and slots
-constexpr uint32_t kTreeMaxFrames = 16;          // open calling invocations below the current one
+constexpr uint32_t kTreeRegFrames = 16;          // deepest register stack; deeper walks spill (kTreeMaxFrames)
+constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations below the current one
+constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
+// LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
+// workgroups per CU, and the whole CU.
+constexpr uint32_t kTreeLdsHalf = 80u * 1024u;
+constexpr uint32_t kTreeLdsFull = 160u * 1024u;
+// Layout chosen by the host (program.cpp place_tree): LDS byte offsets.
+struct TreeLayout {
+  uint32_t off_cnt;     // [2][n_slots] u32: executed calls, callee 500s
+  uint32_t off_sums;    // [n_sum] u64: code-200 duration sums of the LDS rows
+  uint32_t off_dyn;     // dyn_words u32: the bucket tables
+  uint32_t off_nodes;   // [n_pos] TreeNode (nodes_lds)
+  uint32_t bytes;       // total
+  uint32_t nodes_lds;   // 1: the nodes in LDS; 0: read from global memory
+  uint32_t wg_per_cu;   // 2: the layout fits kTreeLdsHalf
+  uint32_t n_sum;       // LDS sum rows
+};
 
 // Scalar kernel arguments (the program, records and stats pointers are
 // separate __restrict__ kernel arguments so program fetches become s_load).
@@ -138,12 +173,18 @@ struct KParams {
   const uint32_t *close_slot;    // kind 6: per close, the call-site slot of the closing invocation
   const uint32_t *close_end;     // kind 6: per chunk, closes up to and including it
   const TreeExt *tree_ext;       // kind 7: per position (the nodes are the `prog` argument)
+  const TreeStep *tree_step;     // kind 7: per position (read under TF_XPRE / TF_XCMAX)
   const TreeDynRow *tree_dyn;    // kind 7: rows with an LDS bucket table
+  const uint32_t *sum_row;       // kind 7: per LDS sum index, its duration-table row
+  const uint32_t *slot_tc;       // kind 7: per slot, the leaf callee's latency
+  uint32_t *spill;               // kind 7: frames below the register stack ([level][word][lane])
+  uint32_t spill_lanes;          // kind 7: lanes of the spill area (grid x workgroup size)
   uint32_t n_pos;                // kind 7: positions of the unrolled tree
-  uint32_t n_rows;               // kind 7: duration-table rows (LDS sums)
+  uint32_t n_rows;               // kind 7: duration-table rows
   uint32_t n_dyn;                // kind 7: entries of tree_dyn
   uint32_t dyn_words;            // kind 7: LDS words of the bucket tables
   uint32_t tree_flags;           // kind 7: kTreeAny*
+  TreeLayout lay;                // kind 7: LDS layout
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to
@@ -168,23 +209,16 @@ constexpr uint32_t kHistWords = 2 * ISIM_N_PROM + 2 * ISIM_N_LOG2;
 // 5 draw stream + mode-B bit stack, 6 draw stream + mode-B close list,
 // 7 lane tree walk (dynamic walks, tree.hip; `frames` = register stack depth).
 void *walk_kernel(int kind, bool modeb, bool lds_counters);
-void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds, bool conc);
-// LDS layout of the kind-7 kernel: accumulators, histograms, per-slot
-// counters (u32 calls, u32 500s), per-row u64 duration sums (code 200), the
-// bucket tables of the varying rows, the nodes, and (ext_lds) the TreeExt
-// records.
-constexpr uint32_t tree_lds_sums_offset(uint32_t n_slots) {
-  return (kLdsAccBytes + kHistWords * 4u + 8u * n_slots + 7u) & ~7u;
-}
-constexpr uint32_t tree_lds_dyn_offset(uint32_t n_slots, uint32_t n_rows) {
-  return tree_lds_sums_offset(n_slots) + 8u * n_rows;
-}
-constexpr uint32_t tree_lds_nodes_offset(uint32_t n_slots, uint32_t n_rows, uint32_t dyn_words) {
-  return (tree_lds_dyn_offset(n_slots, n_rows) + 4u * dyn_words + 15u) & ~15u;
-}
-constexpr uint32_t tree_lds_bytes(uint32_t n_pos, uint32_t n_slots, uint32_t n_rows, uint32_t dyn_words,
-                                  bool ext_lds) {
-  return tree_lds_nodes_offset(n_slots, n_rows, dyn_words) + (ext_lds ? 32u : 16u) * n_pos;
+// kind 7 variant (tree.hip, compiled once per mode and concurrency):
+// register-stack depth (4, 6, 8, 12, 16; `spill`: 8 registers + the rest in
+// global memory), nodes in LDS or global, the error-block cache.
+void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw);
+void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw);
+void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw);
+void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw);
+inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw) {
+  if (modeb) return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw) : tree_kernel_m1c0(frames, spill, nodes_lds, draw);
+  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw) : tree_kernel_m0c0(frames, spill, nodes_lds, draw);
 }
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

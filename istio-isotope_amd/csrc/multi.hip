@@ -321,11 +321,18 @@ int isim_multi_precheck(int device) {
   if (device < 0) return mfail(ISIM_EINVAL, "bad argument");
   const Rccl &R = rccl();
   if (!R.ok) return mfail(ISIM_ECOMM, R.why);
-  int prev = 0;
+  int count = 0, prev = 0;
+  HIPCHK(hipGetDeviceCount(&count));
+  // checked against the count first: a failed hipSetDevice would leave the
+  // error as the thread's last HIP error, for the caller's next HIP check
+  if (device >= count) return mfail(ISIM_EHIP, "no HIP device " + std::to_string(device));
   HIPCHK(hipGetDevice(&prev));
   const hipError_t e = hipSetDevice(device);
   (void)hipSetDevice(prev);
-  if (e != hipSuccess) return mfail(ISIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return mfail(ISIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
   return ISIM_OK;
 }
 

@@ -70,22 +70,103 @@ ScriptTimes script_times(const Service &sv) {
 
 }  // namespace
 
+// LDS layout of the lane tree walk (kernel_abi.h TreeLayout): the per-slot
+// counters always; the nodes when they fit; then the non-leaf callees'
+// duration rows (a u64 sum, and a bucket table when the bucket varies),
+// hottest first (expected invocations per trace), the rest in global memory.
+// Tried in order: nodes in LDS within half the CU (two 1024-thread workgroups
+// per CU), nodes in LDS within the whole CU, nodes in global memory within
+// half, then within the whole CU; the first whose fixed part fits and which
+// holds every row wins, else the first whose fixed part fits.
+static bool place_tree(Program &out, const std::vector<double> &row_heat, const std::vector<uint32_t> &row_bw,
+                       const std::vector<char> &row_nonleaf) {
+  const uint32_t P = (uint32_t)out.tree_nodes.size(), S = (uint32_t)out.n_slots;
+  const uint32_t R = (uint32_t)out.row_svc.size();
+  const uint32_t head = kLdsAccBytes + kHistWords * 4u;
+  // rows by heat (the entry's row, 0, is the end-to-end histogram: no LDS row)
+  std::vector<uint32_t> order;
+  for (uint32_t r = 1; r < R; ++r)
+    if (row_nonleaf[r]) order.push_back(r);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return row_heat[a] > row_heat[b]; });
+  struct Cand {
+    bool nodes;
+    uint32_t limit;
+  };
+  const Cand cands[4] = {{true, kTreeLdsHalf}, {true, kTreeLdsFull}, {false, kTreeLdsHalf}, {false, kTreeLdsFull}};
+  int pick = -1;
+  for (int pass = 0; pass < 2 && pick < 0; ++pass) {
+    for (int i = 0; i < 4 && pick < 0; ++i) {
+      uint32_t fixed = ((head + 8u * S + 7u) & ~7u) + (cands[i].nodes ? 8u * P + 8u : 0u);
+      if (fixed > cands[i].limit) continue;
+      uint32_t all = fixed;
+      for (uint32_t r : order) all += 8u + 4u * (row_bw[r] ? 1u + 2u * row_bw[r] : 0u);
+      if (pass == 1 || all <= cands[i].limit) pick = i;
+    }
+  }
+  if (pick < 0) return false;
+  const Cand c = cands[pick];
+  TreeLayout &L = out.tree_layout;
+  L = TreeLayout{};
+  L.nodes_lds = c.nodes ? 1u : 0u;
+  L.wg_per_cu = c.limit == kTreeLdsHalf ? 2u : 1u;
+  L.off_cnt = head;
+  L.off_sums = (head + 8u * S + 7u) & ~7u;
+  uint32_t room = c.limit - L.off_sums - (c.nodes ? 8u * P + 8u : 0u);
+  // rows into LDS while they fit: a sum word, and the bucket table when the bucket varies
+  out.tree_row_place.assign(R, kTreeGlobalStatic);
+  out.sum_row.clear();
+  out.tree_dyn.clear();
+  out.tree_dyn_words = 0;
+  std::vector<uint32_t> lds_rows;
+  for (uint32_t r : order) {
+    const uint32_t need = 8u + 4u * (row_bw[r] ? 1u + 2u * row_bw[r] : 0u);
+    if (need <= room && out.sum_row.size() < 0xFFFFu && out.tree_dyn_words + 4096u < 0xFFF0u) {
+      room -= need;
+      lds_rows.push_back(r);
+      out.sum_row.push_back(r);
+    } else {
+      out.tree_row_place[r] = row_bw[r] ? kTreeGlobalDyn : kTreeGlobalStatic;
+    }
+  }
+  out.tree_row_index.assign(R, 0);
+  for (uint32_t i = 0; i < (uint32_t)out.sum_row.size(); ++i) {
+    const uint32_t r = out.sum_row[i];
+    out.tree_row_index[r] = i;
+    if (row_bw[r]) {
+      out.tree_row_place[r] = out.tree_dyn_words;
+      out.tree_dyn.push_back(TreeDynRow{r, out.tree_dyn_words, out.tree_row_blo[r], row_bw[r]});
+      out.tree_dyn_words += 1u + 2u * row_bw[r];
+    } else {
+      out.tree_row_place[r] = kTreeStaticRow;
+    }
+  }
+  for (uint32_t r = 0; r < R; ++r)
+    if (out.tree_row_place[r] == kTreeGlobalDyn || out.tree_row_place[r] == kTreeGlobalStatic)
+      out.tree_row_index[r] = r;
+  L.n_sum = (uint32_t)out.sum_row.size();
+  L.off_dyn = L.off_sums + 8u * L.n_sum;
+  L.off_nodes = (L.off_dyn + 4u * out.tree_dyn_words + 7u) & ~7u;
+  L.bytes = L.off_nodes + (c.nodes ? 8u * P : 0u);
+  return L.bytes <= c.limit;
+}
+
 // The unrolled tree of potential invocations for the lane tree walk
 // (kernel_abi.h TreeNode/TreeExt, tree_walk.h); leaves out.tree_nodes empty
 // with the reason in out.tree_why when the walk does not fit it.
 static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Site> &sites,
-                const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
-                const std::vector<uint64_t> &tmin, const std::vector<char> &leaf) {
+                       const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
+                       const std::vector<uint64_t> &tmin, const std::vector<char> &leaf, bool modeb) {
   out.tree_nodes.clear();
   out.tree_ext.clear();
-  if (out.max_latency >= (1ull << 32)) {
-    out.tree_why = "latency bound >= 2^32 ns (the tree walk keeps u32 time)";
-    return;
-  }
-  if (out.n_slots > (int32_t)kTreeMaxPositions) {
-    out.tree_why = "more than 65535 call sites";
-    return;
-  }
+  out.tree_step.clear();
+  auto give_up = [&](const char *why) {
+    out.tree_nodes.clear();
+    out.tree_ext.clear();
+    out.tree_step.clear();
+    out.tree_why = why;
+  };
+  if (out.max_latency >= (1ull << 32)) return give_up("latency bound >= 2^32 ns (the tree walk keeps u32 time)");
+  if (out.n_slots > (int32_t)kTreeMaxPositions) return give_up("more than 65535 call sites");
   const int32_t n = (int32_t)g.services.size();
   std::vector<ScriptTimes> shape(n);
   std::vector<char> shaped(n, 0);
@@ -96,34 +177,27 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     }
     return shape[s];
   };
-  if (out.row_svc.size() > kTreeStaticRow) {
-    out.tree_why = "more than 65534 reachable services";
-    return;
-  }
-  // rows whose durations may fall in several buckets get an LDS bucket table
-  // (the entry's row is the end-to-end histogram: no table)
-  out.tree_dyn.clear();
-  out.tree_dyn_words = 0;
-  std::vector<uint32_t> dyn_off(out.row_svc.size(), kTreeStaticRow);
-  for (size_t r = 1; r < out.row_svc.size(); ++r) {
+  const uint32_t R = (uint32_t)out.row_svc.size();
+  if (R > kTreeGlobalStatic) return give_up("more than 65532 reachable services");
+  // per row: bucket range of the durations (a table when it spans several buckets), non-leaf
+  std::vector<uint32_t> row_bw(R, 0);
+  std::vector<char> row_nonleaf(R, 0);
+  std::vector<double> row_heat(R, 0.0);
+  out.tree_row_blo.assign(R, 0);
+  for (uint32_t r = 1; r < R; ++r) {
     const int32_t s = out.row_svc[r];
+    row_nonleaf[r] = leaf[s] ? 0 : 1;
     const uint32_t lo = prom_bucket_ns(tmin[s]), hi = prom_bucket_ns(out.svc_time[s]);
-    if (lo == hi) continue;
-    if (out.tree_dyn_words + 1 + 2 * (hi - lo + 1) >= kTreeStaticRow) {
-      out.tree_why = "too many duration-bucket table words";
-      return;
-    }
-    dyn_off[r] = out.tree_dyn_words;
-    out.tree_dyn.push_back(TreeDynRow{(uint32_t)r, out.tree_dyn_words, lo, hi - lo + 1});
-    out.tree_dyn_words += 1 + 2 * (hi - lo + 1);
+    out.tree_row_blo[r] = lo;
+    if (lo != hi && !leaf[s]) row_bw[r] = hi - lo + 1;
   }
-  auto row_word = [&](int32_t s) -> uint32_t {
-    return (uint32_t)out.svc_row[s] | (dyn_off[out.svc_row[s]] << 16);
-  };
-  auto slot_word = [&](int32_t s) -> uint32_t {
-    const uint32_t b = prom_bucket_ns(tmin[s]) == prom_bucket_ns(out.svc_time[s]) ? prom_bucket_ns(tmin[s])
-                                                                                   : kTreeDynBucket;
-    return (uint32_t)out.svc_row[s] | (b << 24);
+  // the time a script spends outside its call steps when every step runs (mode A: folded into tc)
+  auto own_time = [&](int32_t s) -> uint64_t {
+    const ScriptTimes &t = shape_of(s);
+    uint64_t v = t.tail;
+    if (!modeb)
+      for (const CallShape &cs : t.calls) v += cs.step_first ? cs.pre : 0;
+    return v;
   };
   auto err_flags = [&](int32_t s) -> uint8_t {
     if (thr[s] >= (1ull << 32)) return TF_ERR_ALWAYS;
@@ -135,37 +209,33 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     for (int32_t si : svc_sites[s]) {
       const Site &st = sites[si];
       if (st.k < 4 && st.prob >= 1 && st.prob <= 99) probk0[s] = 1;
-      if (st.k >= kTreeMaxCalls) {
-        out.tree_why = "a script with more than 8188 calls";
-        return;
-      }
+      if (st.k >= kTreeMaxCalls) return give_up("a script with more than 8188 calls");
     }
   out.tree_flags = 0;
-  out.slot_tbkt.assign(out.n_slots, 0);
-  for (int32_t sl = 0; sl < out.n_slots; ++sl) out.slot_tbkt[sl] = slot_word(out.slot_callee[sl]);
   std::vector<uint32_t> through(out.n_slots, 0);
-  // positions whose callee's row has an LDS bucket table: a table word counts
-  // every invocation of that row in a workgroup (u32), like a slot counter
-  std::vector<uint32_t> row_through(out.row_svc.size(), 0);
-  // preorder DFS over call sites; frame = (service, next call index, position, open calling invocations)
+  std::vector<uint32_t> row_through(R, 0);
+  std::vector<int32_t> pos_callee;  // per position: the callee service
+  // preorder DFS over call sites; frame = (service, next call index, position, path probability)
   struct Frame {
     int32_t svc;
     size_t next;
     uint32_t pos;
+    double heat;
   };
   std::vector<Frame> stack;
   const int32_t e = out.entry;
   TreeNode root{};
   root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e) | (probk0[e] ? TF_PROBK0 : 0));
   if (root.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
-  root.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
   TreeExt rx{};
-  rx.tc = (uint32_t)shape_of(e).tail;
-  rx.row = (uint32_t)out.svc_row[e] | (kTreeStaticRow << 16);  // the entry's row is filled from the histograms
+  rx.tc = (uint32_t)own_time(e);
+  rx.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
   out.tree_nodes.push_back(root);
   out.tree_ext.push_back(rx);
+  out.tree_step.push_back(TreeStep{});
+  pos_callee.push_back(e);
   uint32_t max_open = leaf[e] ? 0u : 1u;
-  if (!leaf[e]) stack.push_back({e, 0, 0});
+  if (!leaf[e]) stack.push_back({e, 0, 0, 1.0});
   while (!stack.empty()) {
     Frame &top = stack.back();
     if (top.next < svc_sites[top.svc].size()) {
@@ -173,42 +243,37 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       const Site &st = sites[svc_sites[top.svc][j]];
       const CallShape &cs = shape_of(top.svc).calls[j];
       const int32_t c = st.callee;
-      if (out.tree_nodes.size() >= kTreeMaxPositions) {
-        out.tree_nodes.clear();
-        out.tree_ext.clear();
-        out.tree_why = "more than 65535 potential invocations";
-        return;
-      }
+      if (out.tree_nodes.size() >= kTreeMaxPositions) return give_up("more than 65535 potential invocations");
+      if (st.k > 0xFFFFu) return give_up("a script with more than 65536 calls");
       TreeNode nd{};
-      nd.k = (uint16_t)std::min<uint32_t>(st.k, 0xFFFFu);
-      if (st.k > 0xFFFFu) {
-        out.tree_nodes.clear();
-        out.tree_ext.clear();
-        out.tree_why = "a script with more than 65536 calls";
-        return;
-      }
+      nd.k = (uint16_t)st.k;
       nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
+      const bool xpre = modeb && cs.step_first && cs.pre != 0;
+      const bool xcmax = cs.step_first && cs.conc && cs.cmax0 != 0;
       nd.flags = (uint8_t)((cs.step_first ? TF_STEP : 0) | (cs.conc ? TF_CONC : 0) | (leaf[c] ? TF_LEAF : 0) |
-                           err_flags(c) | (probk0[c] ? TF_PROBK0 : 0));
+                           err_flags(c) | (probk0[c] ? TF_PROBK0 : 0) | (xpre ? TF_XPRE : 0) |
+                           (xcmax ? TF_XCMAX : 0));
       if (nd.prob) out.tree_flags |= kTreeAnyProb;
       if (nd.flags & TF_CONC) out.tree_flags |= kTreeAnyConc;
       if (nd.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
       const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
       nd.slot = (uint16_t)slot;
       through[slot] += 1;
-      if (dyn_off[out.svc_row[c]] != kTreeStaticRow) row_through[out.svc_row[c]] += 1;
-      nd.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
-      nd.pre = (uint32_t)cs.pre;
+      const uint32_t row = (uint32_t)out.svc_row[c];
+      if (row_bw[row]) row_through[row] += 1;
+      const double heat = top.heat * (nd.prob ? nd.prob / 100.0 : 1.0);
+      row_heat[row] += heat;
       TreeExt x{};
       x.H = (uint32_t)st.hop;
-      x.tc = (uint32_t)shape_of(c).tail;
-      x.cmax0 = (uint32_t)cs.cmax0;
-      x.row = row_word(c);
+      x.tc = (uint32_t)own_time(c);
+      x.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
       const uint32_t pos = (uint32_t)out.tree_nodes.size();
       out.tree_nodes.push_back(nd);
       out.tree_ext.push_back(x);
+      out.tree_step.push_back(TreeStep{(uint32_t)cs.pre, (uint32_t)cs.cmax0});
+      pos_callee.push_back(c);
       if (!leaf[c]) {
-        stack.push_back({c, 0, pos});
+        stack.push_back({c, 0, pos, heat});
         max_open = std::max<uint32_t>(max_open, (uint32_t)stack.size());
       }
     } else {
@@ -220,15 +285,30 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   for (size_t i = 0; i < out.tree_nodes.size(); ++i)
     if (out.tree_nodes[i].size == 0) out.tree_nodes[i].size = 1;  // leaf positions
   out.tree_frames = max_open ? max_open - 1 : 0;
-  if (out.tree_frames > kTreeMaxFrames) {
-    out.tree_nodes.clear();
-    out.tree_ext.clear();
-    out.tree_why = "more than 17 nested calling invocations";
-    return;
+  if (out.tree_frames > kTreeMaxFrames) return give_up("more than 65 nested calling invocations");
+  if (!place_tree(out, row_heat, row_bw, row_nonleaf)) return give_up("the per-slot counters do not fit in LDS");
+  // the row words of the non-leaf callees (the entry's row is filled from the histograms)
+  for (size_t i = 1; i < out.tree_nodes.size(); ++i) {
+    const int32_t c = pos_callee[i];
+    if (leaf[c]) continue;
+    const uint32_t r = (uint32_t)out.svc_row[c];
+    out.tree_ext[i].row = out.tree_row_index[r] | (out.tree_row_place[r] << 16);
+  }
+  out.tree_ext[0].row = kTreeStaticRow << 16;
+  // per slot: the callee's row, its static bucket (kTreeDynBucket when it varies), leaf flag and latency
+  out.slot_tbkt.assign(out.n_slots, 0);
+  out.slot_tc.assign(out.n_slots, 0);
+  for (int32_t sl = 0; sl < out.n_slots; ++sl) {
+    const int32_t s = out.slot_callee[sl];
+    const uint32_t r = (uint32_t)out.svc_row[s];
+    const uint32_t b = (leaf[s] || !row_bw[r]) ? prom_bucket_ns(tmin[s]) : kTreeDynBucket;
+    out.slot_tbkt[sl] = r | (leaf[s] ? kTreeLeafSlot : 0u) | (b << 24);
+    out.slot_tc[sl] = leaf[s] ? (uint32_t)out.svc_time[s] : 0u;
   }
   out.tree_mult = 1;
   for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
-  for (uint32_t m : row_through) out.tree_mult = std::max(out.tree_mult, m);
+  for (uint32_t r = 0; r < R; ++r)
+    if (out.tree_row_place[r] < kTreeGlobalStatic) out.tree_mult = std::max(out.tree_mult, row_through[r]);
   out.tree_why.clear();
 }
 
@@ -595,7 +675,7 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     err = "program too large";
     return ISIM_EINVAL;
   }
-  if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf);
+  if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf, p.error_mode == ISIM_MODE_B);
   return ISIM_OK;
 }
 

@@ -49,13 +49,19 @@ struct Program {
   // invocations when it fits (tree_nodes empty otherwise; tree_why says why)
   std::vector<TreeNode> tree_nodes;
   std::vector<TreeExt> tree_ext;
-  std::vector<uint32_t> slot_tbkt;  // per slot: callee row | static duration bucket << 24 (kTreeDynBucket)
-  std::vector<TreeDynRow> tree_dyn; // rows whose duration bucket varies: their LDS bucket tables
+  std::vector<TreeStep> tree_step;
+  std::vector<uint32_t> slot_tbkt;  // per slot: callee row | kTreeLeafSlot | static duration bucket << 24
+                                    // (kTreeDynBucket: it varies)
+  std::vector<uint32_t> slot_tc;    // per slot: the leaf callee's latency (0 for a calling callee)
+  std::vector<TreeDynRow> tree_dyn; // LDS rows whose duration bucket varies: their LDS bucket tables
   uint32_t tree_dyn_words = 0;
-  uint32_t tree_frames = 0;         // register-stack frames the walk needs (open calling invocations - 1)
+  std::vector<uint32_t> sum_row;    // per LDS sum index: its row
+  std::vector<uint32_t> tree_row_place, tree_row_index, tree_row_blo;  // per row (place_tree)
+  TreeLayout tree_layout{};
+  uint32_t tree_frames = 0;         // frames the walk needs (open calling invocations - 1)
   uint32_t tree_mult = 0;           // most positions through one slot or into one bucket-table row (LDS u32
                                     // counter overflow guard)
-  uint32_t tree_flags = 0;          // kTreeAnyProb | kTreeAnyDraw
+  uint32_t tree_flags = 0;          // kTreeAnyProb | kTreeAnyDraw | kTreeAnyConc
   std::string tree_why;
 };
 

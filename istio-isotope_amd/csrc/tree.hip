@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "kernel_abi.h"
 #include "tree_walk.h"
 #include "walk_dev.h"
@@ -50,22 +52,40 @@ __device__ __forceinline__ void lds_add(unsigned long long *p, unsigned long lon
   __hip_atomic_fetch_add((lds_u64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Row of a duration-table word (row | bucket << 24).  The empty asm hides the
-// 24-bit mask from the AMDGPU backend (ROCm 7.2 LLVM): with the mask's known
-// bits it formed a u24 multiply for the row offset, dropped the AND, and then
-// selected v_mad_u64_u32, which multiplies all 32 bits — the atomic's address
-// ran off by bucket x 9 GB (hipErrorIllegalAddress on rows with bucket > 0).
+// Row of a duration-table word.  The empty asm hides the mask from the
+// AMDGPU backend (ROCm 7.2 LLVM): with the mask's known bits it formed a u24
+// multiply for the row offset, dropped the AND, and then selected
+// v_mad_u64_u32, which multiplies all 32 bits — the atomic's address ran off
+// by bucket x 9 GB (hipErrorIllegalAddress on rows with bucket > 0).
 __device__ __forceinline__ uint32_t dur_row(uint32_t w) {
-  uint32_t r = w & kDurRowMask;
+  uint32_t r = w & kTreeRowMask;
   asm volatile("" : "+v"(r));
   return r;
 }
 
+// Node accessors of tree_walk.h: LDS (ds_read_b64) or global memory
+// (global_load_dwordx2, L2-resident).
+struct LdsNodes {
+  const __attribute__((address_space(3))) unsigned long long *p;
+  __device__ __forceinline__ tw::NodeW load(uint32_t i) const {
+    const unsigned long long v = p[i];
+    return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
+};
+struct GlobalNodes {
+  const unsigned long long *__restrict__ p;
+  __device__ __forceinline__ tw::NodeW load(uint32_t i) const {
+    const unsigned long long v = p[i];
+    return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
+};
+
 struct TreeSink {
   uint32_t *cnt;                // LDS [2][n_slots]: executed calls, callee 500s
-  unsigned long long *sum200;   // LDS [n_rows]
+  unsigned long long *sum200;   // LDS [n_sum]
   uint32_t *dyn;                // LDS bucket tables of the varying rows
   uint64_t *svc_tab;            // HBM duration table, or null (ISIM_FLAG_NO_SVC_DUR)
+  const uint32_t *sum_row;      // per LDS sum index: its row (code-500 sums go to HBM)
   uint32_t n_slots;
 #ifdef ISIM_TREE_DEBUG
   uint32_t n_pos, n_rows;
@@ -85,62 +105,73 @@ struct TreeSink {
 #endif
     lds_add(cnt + slot, 1u);
   }
+  // a leaf callee: its duration is static (bucket and sums follow from the counters at the flush)
+  __device__ __forceinline__ void resp_leaf(uint32_t slot, bool st) {
+#ifdef TREE_NO_SINK
+    return;
+#endif
+    if (st) lds_add(cnt + n_slots + slot, 1u);
+  }
   __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
 #ifdef TREE_NO_SINK
     return;
 #endif
 #ifdef ISIM_TREE_DEBUG
-    if (slot >= n_slots || (roww & kDurRowMask) >= n_rows) { atomicOr(dbg, 32ull); return; }
+    if (slot >= n_slots) { atomicOr(dbg, 32ull); return; }
 #endif
     if (st) lds_add(cnt + n_slots + slot, 1u);
     if (!svc_tab) return;
-    const uint32_t row = roww & 0xFFFFu, off = roww >> 16;
-    if (off != kTreeStaticRow) {  // the row's LDS bucket table: header b_lo | width << 8
-      const uint32_t hdr = dyn[off], lo = hdr & 0xFFu, w = hdr >> 8;
+    const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
+    if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // a cold row: sums (and varying buckets) by global atomics
+      unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(idx) * ISIM_SVC_DUR_WORDS);
+      if (place == kTreeGlobalDyn) atomicAdd(r + (st ? ISIM_N_PROM : 0u) + prom_bucket(T), 1ull);
+      atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
+      return;
+    }
+    if (place != kTreeStaticRow) {  // the row's LDS bucket table: header b_lo | width << 8
+      const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
       uint32_t b = prom_bucket(T) - lo;
       b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
-      lds_add(dyn + off + 1u + (st ? w : 0u) + b, 1u);
+      lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
     }
     if (st) {
-      unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(row) * ISIM_SVC_DUR_WORDS);
+      unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS);
       atomicAdd(r + 2 * ISIM_N_PROM + 1, (unsigned long long)T);
     } else {
-      lds_add(sum200 + row, (unsigned long long)T);
+      lds_add(sum200 + idx, (unsigned long long)T);
     }
   }
 };
 
-template <bool MODEB, int FRAMES, bool EXTL, bool CONC>
-__global__ void __launch_bounds__(kWgThreads, 1)
+// Waves per SIMD the register allocation must allow: 6 for stacks of up to 8
+// frames (80 VGPRs: two 768-thread workgroups per CU), 4 for deeper stacks.
+#ifndef TREE_WPE
+#define TREE_WPE 6
+#endif
+template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW>
+__global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
   extern __shared__ __align__(16) unsigned char lds[];
-  const uint32_t S = kp.n_slots, R = kp.n_rows, P = kp.n_pos;
+  const uint32_t S = kp.n_slots, P = kp.n_pos;
+  const TreeLayout &lay = kp.lay;
   Ctx c{};
   c.records = records;
   c.gstats = gstats;
   c.svc_tab = kp.svc_dur ? gstats + ISIM_ST_SVC_DUR(S) : nullptr;
   c.acc = reinterpret_cast<WgAcc *>(lds);
   c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
-  c.cnt = c.hist + kHistWords;
+  c.cnt = reinterpret_cast<uint32_t *>(lds + lay.off_cnt);
   c.n_slots = S;
-  const uint32_t off = tree_lds_nodes_offset(S, R, kp.dyn_words);
-  unsigned long long *sum200 = reinterpret_cast<unsigned long long *>(lds + tree_lds_sums_offset(S));
-  uint32_t *dyn = reinterpret_cast<uint32_t *>(lds + tree_lds_dyn_offset(S, R));
-  TreeNode *nodes = reinterpret_cast<TreeNode *>(lds + off);
-  TreeExt *lext = reinterpret_cast<TreeExt *>(lds + off + 16u * P);
-  // zero the accumulators (everything before the nodes), copy the tree in
+  unsigned long long *sum200 = reinterpret_cast<unsigned long long *>(lds + lay.off_sums);
+  uint32_t *dyn = reinterpret_cast<uint32_t *>(lds + lay.off_dyn);
+  // zero the accumulators (everything before the nodes), copy the nodes in
   uint32_t *z = reinterpret_cast<uint32_t *>(lds);
-  for (uint32_t i = threadIdx.x; i < off / 4u; i += blockDim.x) z[i] = 0;
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(gnodes);
-    uint4 *dst = reinterpret_cast<uint4 *>(nodes);
+  for (uint32_t i = threadIdx.x; i < lay.off_nodes / 4u; i += blockDim.x) z[i] = 0;
+  if constexpr (NLDS) {
+    const uint2 *src = reinterpret_cast<const uint2 *>(gnodes);
+    uint2 *dst = reinterpret_cast<uint2 *>(lds + lay.off_nodes);
     for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) dst[i] = src[i];
-    if constexpr (EXTL) {
-      const uint4 *xs = reinterpret_cast<const uint4 *>(kp.tree_ext);
-      uint4 *xd = reinterpret_cast<uint4 *>(lext);
-      for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) xd[i] = xs[i];
-    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < kp.n_dyn; i += blockDim.x) {
@@ -148,13 +179,20 @@ __global__ void __launch_bounds__(kWgThreads, 1)
     dyn[d.off] = d.b_lo | (d.width << 8);
   }
   __syncthreads();
-  TreeSink sink{c.cnt, sum200, dyn, c.svc_tab, S};
+  TreeSink sink{c.cnt, sum200, dyn, c.svc_tab, kp.sum_row, S};
 #ifdef ISIM_TREE_DEBUG
   sink.n_pos = P;
-  sink.n_rows = R;
+  sink.n_rows = kp.n_rows;
   sink.dbg = reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_DES_RETRY);
 #endif
-  const TreeExt *__restrict__ ext = EXTL ? lext : kp.tree_ext;
+  using Nodes = std::conditional_t<NLDS, LdsNodes, GlobalNodes>;
+  Nodes nodes;
+  if constexpr (NLDS)
+    nodes.p = (const __attribute__((address_space(3))) unsigned long long *)(lds + lay.off_nodes);
+  else
+    nodes.p = reinterpret_cast<const unsigned long long *>(gnodes);
+  const TreeExt *__restrict__ ext = kp.tree_ext;
+  const TreeStep *__restrict__ stp = kp.tree_step;
 
   const uint32_t wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
   const uint64_t n = kp.n_traces;
@@ -179,33 +217,43 @@ __global__ void __launch_bounds__(kWgThreads, 1)
   bool dry = b >= n_batches;
   uint64_t nxt = dry ? 0 : b * 64, lim = dry ? 0 : (b * 64 + 64 < n ? b * 64 + 64 : n);
   const uint64_t lt = ((uint64_t)1 << lane_id()) - 1;  // lanes below this one
-  tw::Lane<FRAMES, MODEB, CONC> L;
+  tw::Lane<FRAMES, MODEB, CONC, SPILL, DRAW> L;
+  if constexpr (SPILL) {
+    L.sp = kp.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    L.sp_stride = kp.spill_lanes;
+  }
   bool active = false;  // the lane holds a trace whose record is not yet written
-  uint64_t idx = 0;
-  uint64_t a_lat = 0, a_hops = 0, a_err = 0, a_lat500 = 0, a_max = 0, a_notmin = 0;
-  uint32_t a_n500 = 0, a_ntr = 0;
+  uint32_t idx = 0;     // launches hold fewer than 2^31 traces (api.hip max_launch_traces)
+  // per-lane sums in 32 bits (a latency sum that wraps carries 2^32 into the
+  // workgroup's u64 accumulator at once); trace and 500 counts follow from
+  // the histograms at the flush
+  uint32_t a_lat = 0, a_lat500 = 0, a_hops = 0, a_err = 0, a_max = 0, a_min = 0xFFFFFFFFu;
   while (true) {
     // responded traces: record, histograms, sums
     const uint64_t fin = ballot(active && L.done);
     if (fin) {
       const bool mine = lane_in(fin);
-      const uint64_t lat = L.lat;
+      const uint32_t lat = L.lat;
       const bool is500 = L.root500;
       if (mine) {
         uint4 r;
-        r.x = (uint32_t)lat;
+        r.x = lat;
         r.y = 0u;
         r.z = L.hopn;
         r.w = (is500 ? 0x80000000u : 0u) | L.errh;
         if (c.records) *reinterpret_cast<uint4 *>(c.records + idx) = r;
-        a_lat += lat;
+        const uint32_t nl = a_lat + lat;
+        if (nl < a_lat) lds_add(&c.acc->sum_latency, 1ull << 32);
+        a_lat = nl;
+        if (is500) {
+          const uint32_t n5 = a_lat500 + lat;
+          if (n5 < a_lat500) lds_add(&c.acc->sum_latency500, 1ull << 32);
+          a_lat500 = n5;
+        }
         a_hops += L.hopn;
         a_err += L.errh;
-        a_n500 += is500 ? 1u : 0u;
-        a_lat500 += is500 ? lat : 0u;
-        a_ntr += 1;
         a_max = lat > a_max ? lat : a_max;
-        a_notmin = ~lat > a_notmin ? ~lat : a_notmin;
+        a_min = lat < a_min ? lat : a_min;
         active = false;
       }
 #ifndef TREE_NO_HIST
@@ -243,26 +291,38 @@ __global__ void __launch_bounds__(kWgThreads, 1)
       idle &= ~took;
     }
     if (!ballot(active)) break;  // every trace of the wave's batches has responded
-    if (active && !L.done) L.step(nodes, ext, sink, kp.seed_lo, kp.seed_hi);
+    if (active && !L.done) L.step(nodes, ext, stp, sink, kp.seed_lo, kp.seed_hi);
   }
   // the wave's sums into the workgroup accumulators
   {
     const uint64_t s_lat = wave_sum64(a_lat), s_hops = wave_sum64(a_hops), s_err = wave_sum64(a_err);
-    const uint64_t s_500 = wave_sum64(a_lat500), s_n500 = wave_sum64(a_n500), s_ntr = wave_sum64(a_ntr);
-    const uint64_t mx = wave_max64(a_max), nmn = wave_max64(a_notmin);
-    if (lane_id() == 0 && s_ntr) {
-      atomicAdd(&c.acc->sum_latency, (unsigned long long)s_lat);
-      atomicAdd(&c.acc->sum_hops, (unsigned long long)s_hops);
-      atomicAdd(&c.acc->sum_err, (unsigned long long)s_err);
-      atomicAdd(&c.acc->n500, (unsigned long long)s_n500);
-      atomicAdd(&c.acc->ntr, (unsigned long long)s_ntr);
-      atomicAdd(&c.acc->sum_latency500, (unsigned long long)s_500);
+    const uint64_t s_500 = wave_sum64(a_lat500);
+    const uint64_t mx = wave_max64(a_max), nmn = wave_max64(~(uint64_t)a_min);
+    if (lane_id() == 0) {
+      lds_add(&c.acc->sum_latency, (unsigned long long)s_lat);
+      lds_add(&c.acc->sum_hops, (unsigned long long)s_hops);
+      lds_add(&c.acc->sum_err, (unsigned long long)s_err);
+      lds_add(&c.acc->sum_latency500, (unsigned long long)s_500);
       atomicMax(&c.acc->max, (unsigned long long)mx);
       atomicMax(&c.acc->notmin, (unsigned long long)nmn);
     }
   }
   if (lane_id() == 0 && atomicAdd(kp.work + kWorkQueues * kWorkLine, 1ull) == stride - 1) {
     for (uint32_t i = 0; i <= kWorkQueues; ++i) atomicExch(kp.work + i * kWorkLine, 0ull);
+  }
+  __syncthreads();
+  // the workgroup's trace and 500 counts: its end-to-end histogram
+  if (threadIdx.x < 64) {
+    uint32_t n2 = 0, n5 = 0;
+    if (threadIdx.x < ISIM_N_PROM) {
+      n2 = c.hist[threadIdx.x];
+      n5 = c.hist[ISIM_N_PROM + threadIdx.x];
+    }
+    const uint64_t t2 = wave_sum64(n2), t5 = wave_sum64(n5);
+    if (threadIdx.x == 0) {
+      c.acc->ntr = t2 + t5;
+      c.acc->n500 = t5;
+    }
   }
   __syncthreads();
   // ---- flush the workgroup's accumulators (coalesced over slots / rows)
@@ -276,14 +336,21 @@ __global__ void __launch_bounds__(kWgThreads, 1)
     for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
       const uint32_t w = slot_tbkt[s], bk = w >> 24;
       const uint32_t calls = c.cnt[s], errs = c.cnt[S + s];
-      if (bk == kTreeDynBucket || calls == 0) continue;
+      if (calls == 0) continue;
       unsigned long long *row = tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS;
-      if (calls != errs) atomicAdd(row + bk, (unsigned long long)(calls - errs));
-      if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
+      if (bk != kTreeDynBucket) {
+        if (calls != errs) atomicAdd(row + bk, (unsigned long long)(calls - errs));
+        if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
+      }
+      if (w & kTreeLeafSlot) {  // a leaf callee lasts its latency every time
+        const unsigned long long tc = kp.slot_tc[s];
+        if (calls != errs && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * (calls - errs));
+        if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
+      }
     }
-    for (uint32_t r = threadIdx.x; r < R; r += blockDim.x)
-      if (sum200[r]) atomicAdd(tab + (uint64_t)r * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, sum200[r]);
-    // the varying rows' bucket tables: one thread per (row, word)
+    for (uint32_t r = threadIdx.x; r < lay.n_sum; r += blockDim.x)
+      if (sum200[r]) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, sum200[r]);
+    // the varying LDS rows' bucket tables: one thread per (row, word)
     for (uint32_t i = threadIdx.x; i < kp.dyn_words; i += blockDim.x) {
       const uint32_t v = dyn[i];
       if (!v) continue;
@@ -322,20 +389,35 @@ __global__ void __launch_bounds__(kWgThreads, 1)
 
 }  // namespace dev
 
-// Register-stack depths compiled: the smallest that holds the graph's frames;
-// TreeExt in LDS when it fits (ext_lds), else read from HBM; walks without
-// concurrent steps keep no step maxima (CONC = false).
-template <bool EXTL, bool CONC>
-static void *tree_pick(bool modeb, uint32_t frames) {
+// The variants of one (mode, concurrency) pair: this file is compiled once
+// per pair (Makefile: tree_m<MODEB>c<CONC>.o) so the 96 kernels build in
+// parallel.  Register-stack depths: the smallest of 4, 6, 8, 12, 16 that
+// holds the graph's frames, else 8 registers + a global spill; nodes in LDS
+// when the layout holds them; the error-block cache only with error draws.
+#ifndef TREE_MODEB
+#define TREE_MODEB 0
+#endif
+#ifndef TREE_CONC
+#define TREE_CONC 0
+#endif
+template <bool NLDS, bool DRAW>
+static void *tree_pick(uint32_t frames, bool spill) {
   using namespace dev;
-  if (frames <= 4) return modeb ? (void *)&isim_tree<true, 4, EXTL, CONC> : (void *)&isim_tree<false, 4, EXTL, CONC>;
-  if (frames <= 8) return modeb ? (void *)&isim_tree<true, 8, EXTL, CONC> : (void *)&isim_tree<false, 8, EXTL, CONC>;
-  return modeb ? (void *)&isim_tree<true, 16, EXTL, CONC> : (void *)&isim_tree<false, 16, EXTL, CONC>;
+  constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
+  if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW>;
+  if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW>;
+  if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW>;
+  if (frames <= 8) return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW>;
+  if (frames <= 12) return (void *)&isim_tree<M, 12, false, NLDS, C, DRAW>;
+  return (void *)&isim_tree<M, 16, false, NLDS, C, DRAW>;
 }
 
-void *tree_kernel(bool modeb, uint32_t frames, bool ext_lds, bool conc) {
-  if (conc) return ext_lds ? tree_pick<true, true>(modeb, frames) : tree_pick<false, true>(modeb, frames);
-  return ext_lds ? tree_pick<true, false>(modeb, frames) : tree_pick<false, false>(modeb, frames);
+#define TREE_CAT2(a, b, c) a##b##c
+#define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
+void *TREE_CAT(tree_kernel_m, TREE_MODEB, TREE_CAT(c, TREE_CONC, ))(uint32_t frames, bool spill, bool nodes_lds,
+                                                                      bool draw) {
+  if (nodes_lds) return draw ? tree_pick<true, true>(frames, spill) : tree_pick<true, false>(frames, spill);
+  return draw ? tree_pick<false, true>(frames, spill) : tree_pick<false, false>(frames, spill);
 }
 
 }  // namespace isim

@@ -78,30 +78,27 @@ TW_PRAGMA_UNROLL  // unrolled: config 4 7.28 -> 7.18 ms (the loop's SALU counter
   }
 }
 
-// A TreeNode / TreeExt as ONE 16-byte load (the kernel's copies live in LDS:
-// one ds_read_b128 instead of a narrow read per field), fields unpacked by
-// shifts.  Layout: kernel_abi.h.
+// A TreeNode as ONE 8-byte load, fields unpacked by shifts (layout:
+// kernel_abi.h).  The kernel reads nodes from LDS or global memory through
+// an accessor with `NodeW load(uint32_t p) const` (tree.hip); the CPU check
+// through CpuNodes.
 struct NodeW {
-  uint32_t w0, w1, w2, w3;  // size | k << 16, prob | flags << 8 | slot << 16, thr, pre
+  uint32_t w0, w1;  // size | k << 16, prob | flags << 8 | slot << 16
   ISIM_TW uint32_t size() const { return w0 & 0xFFFFu; }
   ISIM_TW uint32_t k() const { return w0 >> 16; }
   ISIM_TW uint32_t prob() const { return w1 & 0xFFu; }
   ISIM_TW uint32_t flags() const { return (w1 >> 8) & 0xFFu; }
   ISIM_TW uint32_t slot() const { return w1 >> 16; }
-  ISIM_TW uint32_t thr() const { return w2; }
-  ISIM_TW uint32_t pre() const { return w3; }
 };
-static_assert(sizeof(TreeNode) == sizeof(NodeW), "TreeNode is four words");
-ISIM_TW NodeW load_node(const TreeNode *nodes, uint32_t p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint4 v = reinterpret_cast<const uint4 *>(nodes)[p];
-  return NodeW{v.x, v.y, v.z, v.w};
-#else
-  NodeW n;
-  __builtin_memcpy(&n, nodes + p, sizeof n);
-  return n;
-#endif
-}
+static_assert(sizeof(TreeNode) == sizeof(NodeW), "TreeNode is two words");
+struct CpuNodes {
+  const TreeNode *p;
+  ISIM_TW NodeW load(uint32_t i) const {
+    NodeW n;
+    __builtin_memcpy(&n, p + i, sizeof n);
+    return n;
+  }
+};
 ISIM_TW TreeExt load_ext(const TreeExt *ext, uint32_t p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint4 v = reinterpret_cast<const uint4 *>(ext)[p];
@@ -130,8 +127,9 @@ ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return (a % 100u) | (b % 100u) << 7 | (c % 100u) << 14 | (d % 100u) << 21;
 }
 
-// Sink: call(slot) per executed call; resp(slot, row word, T, status) per
-// response of a called invocation (the entry's is the trace result).
+// Sink: call(slot) per executed call; resp_leaf(slot, status) per response
+// of a leaf callee (its duration is static); resp(slot, row word, T,
+// status) per response of a calling callee (the entry's is the trace result).
 //
 // One step() is a MACRO step: close the current invocation if the walk has
 // passed its subtree, then process position p (a call: skip it, run a leaf
@@ -142,7 +140,12 @@ ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // drawn once, when it opens, and kept in its frame (f_res), so returning from
 // a callee never recomputes the caller's block and the scans need no draw.
 // CONC: the walk has concurrent steps (without them no frame keeps a step max).
-template <int FRAMES, bool MODEB, bool CONC = true>
+// SPILL: calling invocations deeper than FRAMES below the current one are kept
+// in memory at sp[(level * kTreeSpillWords + word) * sp_stride] (the kernel:
+// global memory, one column per lane; the CPU check: a vector).
+// DRAW: some callee draws its error against a threshold (without, no error
+// block is cached: 5 registers fewer).
+template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true>
 struct Lane {
   uint32_t t_lo = 0, t_hi = 0;
   uint32_t p = 0, d = 0, end = 0, hopn = 0, errh = 0;
@@ -154,13 +157,15 @@ struct Lane {
   // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time
   uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1],
       s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
+  uint32_t *sp = nullptr;  // SPILL: this lane's column of the spill area
+  uint32_t sp_stride = 1;
   // cached error block: words of Philox (t, ek_blk, 0, 0)
   uint32_t ek_blk = 0xFFFFFFFFu, e0 = 0, e1 = 0, e2 = 0, e3 = 0;
 
   // k0, k1: the Philox key (wave-uniform: passed in, never stored per lane)
-  ISIM_TW bool own_error(uint32_t hop, uint8_t flags, uint32_t thr, uint32_t k0, uint32_t k1) {
+  ISIM_TW bool own_error(uint32_t hop, uint32_t flags, uint32_t thr, uint32_t k0, uint32_t k1) {
     if (flags & TF_ERR_ALWAYS) return true;
-    if (!(flags & TF_ERR_DRAW)) return false;
+    if (!DRAW || !(flags & TF_ERR_DRAW)) return false;
     const uint32_t b = hop >> 2;
     if (b != ek_blk) {
       uint32_t a = t_lo, bb = t_hi, c = b, dd = 0;
@@ -209,14 +214,24 @@ struct Lane {
   }
 
   ISIM_TW void push() {
+    const uint32_t pe = f_pos | (end << 16), hf = f_hop | (f_fl << 16);
+    if (SPILL && d >= (uint32_t)FRAMES) {
+      uint32_t *q = sp + (d - (uint32_t)FRAMES) * kTreeSpillWords * sp_stride;
+      q[0] = pe;
+      q[sp_stride] = hf;
+      q[2 * sp_stride] = f_res;
+      q[3 * sp_stride] = f_acc;
+      q[4 * sp_stride] = f_cmax;
+    } else {
 TW_PRAGMA_UNROLL
-    for (int i = 0; i < FRAMES; ++i) {
-      const bool m = d == (uint32_t)i;
-      s_pe[i] = m ? (f_pos | (end << 16)) : s_pe[i];
-      s_hf[i] = m ? (f_hop | (f_fl << 16)) : s_hf[i];
-      s_res[i] = m ? f_res : s_res[i];
-      s_acc[i] = m ? f_acc : s_acc[i];
-      if (CONC) s_cmax[i] = m ? f_cmax : s_cmax[i];
+      for (int i = 0; i < FRAMES; ++i) {
+        const bool m = d == (uint32_t)i;
+        s_pe[i] = m ? pe : s_pe[i];
+        s_hf[i] = m ? hf : s_hf[i];
+        s_res[i] = m ? f_res : s_res[i];
+        s_acc[i] = m ? f_acc : s_acc[i];
+        if (CONC) s_cmax[i] = m ? f_cmax : s_cmax[i];
+      }
     }
     ++d;
   }
@@ -224,14 +239,23 @@ TW_PRAGMA_UNROLL
   ISIM_TW void pop() {
     --d;
     uint32_t pe = 0, hf = 0, r = 0, a = 0, c = 0;
+    if (SPILL && d >= (uint32_t)FRAMES) {
+      const uint32_t *q = sp + (d - (uint32_t)FRAMES) * kTreeSpillWords * sp_stride;
+      pe = q[0];
+      hf = q[sp_stride];
+      r = q[2 * sp_stride];
+      a = q[3 * sp_stride];
+      c = q[4 * sp_stride];
+    } else {
 TW_PRAGMA_UNROLL
-    for (int i = 0; i < FRAMES; ++i) {
-      const bool m = d == (uint32_t)i;
-      pe = m ? s_pe[i] : pe;
-      hf = m ? s_hf[i] : hf;
-      r = m ? s_res[i] : r;
-      a = m ? s_acc[i] : a;
-      if (CONC) c = m ? s_cmax[i] : c;
+      for (int i = 0; i < FRAMES; ++i) {
+        const bool m = d == (uint32_t)i;
+        pe = m ? s_pe[i] : pe;
+        hf = m ? s_hf[i] : hf;
+        r = m ? s_res[i] : r;
+        a = m ? s_acc[i] : a;
+        if (CONC) c = m ? s_cmax[i] : c;
+      }
     }
     f_pos = pe & 0xFFFFu;
     end = pe >> 16;
@@ -243,10 +267,11 @@ TW_PRAGMA_UNROLL
   }
 
   // The step begin of call position p (TF_STEP: the previous concurrent step
-  // ends, the non-call time since the previous call step is added, a
-  // concurrent step starts) on copies of the frame's time and flags; returns
-  // false when the script has failed (mode B: it runs no further step).
-  ISIM_TW bool step_begin(const NodeW &n, const TreeExt *ext, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
+  // ends, the non-call time since the previous call step is added — mode B
+  // only, TF_XPRE: mode A folds it into the caller's tc —, a concurrent step
+  // starts) on copies of the frame's time and flags; returns false when the
+  // script has failed (mode B: it runs no further step).
+  ISIM_TW bool step_begin(const NodeW &n, const TreeStep *stp, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
     if (!(n.flags() & TF_STEP)) return true;
     if (CONC && (fl & FL_INCONC)) {
       acc += cm;
@@ -254,11 +279,14 @@ TW_PRAGMA_UNROLL
       fl &= ~(FL_INCONC | FL_CERR);
     }
     if (MODEB && (fl & FL_FAILED)) return false;
-    acc += n.pre();
-    if (CONC && (n.flags() & TF_CONC)) {
-      fl |= FL_INCONC;
-      cm = load_ext(ext, p).cmax0;
+    if (n.flags() & (TF_XPRE | TF_XCMAX)) {
+      const TreeStep x = stp[p];
+      if (MODEB) acc += x.pre;  // TF_XPRE is never set in mode A (pre is 0 here then)
+      cm = x.cmax0;
+    } else {
+      cm = 0;
     }
+    if (CONC && (n.flags() & TF_CONC)) fl |= FL_INCONC;
     return true;
   }
 
@@ -268,8 +296,8 @@ TW_PRAGMA_UNROLL
   }
 
   // close f_pos: its response folds into its caller (false: the entry responded)
-  template <class Sink>
-  ISIM_TW bool close(const TreeNode *nodes, const TreeExt *ext, Sink &sink) {
+  template <class Nodes, class Sink>
+  ISIM_TW bool close(const Nodes &nodes, const TreeExt *ext, Sink &sink) {
     uint32_t T = f_acc, fl = f_fl;
     if (CONC && (fl & FL_INCONC)) {
       T += f_cmax;
@@ -286,7 +314,7 @@ TW_PRAGMA_UNROLL
       root500 = st;
       return false;
     }
-    sink.resp(load_node(nodes, f_pos).slot(), x.row, T, st);
+    sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
     const uint32_t c = x.H + T;
     const bool cc = (fl & FL_CONC_CHILD) != 0;
     pop();
@@ -295,10 +323,11 @@ TW_PRAGMA_UNROLL
   }
 
   // process call position p (p < end)
-  template <class Sink>
-  ISIM_TW void process(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
-    const NodeW n = load_node(nodes, p);
-    if (!step_begin(n, ext, f_acc, f_fl, f_cmax)) {  // mode B: the script stops, close at the subtree's end
+  template <class Nodes, class Sink>
+  ISIM_TW void process(const Nodes &nodes, const TreeExt *ext, const TreeStep *stp, Sink &sink, uint32_t k0,
+                       uint32_t k1) {
+    const NodeW n = nodes.load(p);
+    if (!step_begin(n, stp, f_acc, f_fl, f_cmax)) {  // mode B: the script stops, close at the subtree's end
       p = end;
       return;
     }
@@ -314,11 +343,12 @@ TW_PRAGMA_UNROLL
       }
     }
     const uint32_t hop = hopn++;
-    const bool own = own_error(hop, n.flags(), n.thr(), k0, k1);
+    const uint32_t fl = n.flags();
     const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
     if (!entry) sink.call(n.slot());
-    if (n.flags() & TF_LEAF) {
+    if (fl & TF_LEAF) {
       const TreeExt x = load_ext(ext, p);
+      const bool own = own_error(hop, fl, x.thr, k0, k1);
       errh += own ? 1u : 0u;
       if (entry) {
         done = true;
@@ -326,29 +356,32 @@ TW_PRAGMA_UNROLL
         root500 = own;
         return;
       }
-      sink.resp(n.slot(), x.row, x.tc, own);
-      fold(x.H + x.tc, own, (n.flags() & TF_CONC) != 0);
+      sink.resp_leaf(n.slot(), own);
+      fold(x.H + x.tc, own, (fl & TF_CONC) != 0);
       p += 1;
       return;
     }
+    const bool own =
+        (DRAW && (fl & TF_ERR_DRAW)) ? own_error(hop, fl, load_ext(ext, p).thr, k0, k1) : (fl & TF_ERR_ALWAYS) != 0;
     if (!entry) push();
     f_pos = p;
     f_acc = 0;
     f_cmax = 0;
     f_hop = hop;
-    const bool pk = (n.flags() & TF_PROBK0) != 0;
+    const bool pk = (fl & TF_PROBK0) != 0;
     f_res = pk ? residues(hop, 0, k0, k1) : 0u;
-    f_fl = (own ? FL_OWN : 0u) | ((n.flags() & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
+    f_fl = (own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
     end = p + n.size();
     p += 1;
   }
 
   // pass call position p if its skip draw (already in f_res) says skip
-  ISIM_TW bool scan(const TreeNode *nodes, const TreeExt *ext) {
-    const NodeW n = load_node(nodes, p);
+  template <class Nodes>
+  ISIM_TW bool scan(const Nodes &nodes, const TreeStep *stp) {
+    const NodeW n = nodes.load(p);
     if (!n.prob() || (((f_fl >> KB_SHIFT) & KB_NONE) != ((uint32_t)n.k() >> 2)) || !skipped(n)) return false;
     uint32_t acc = f_acc, fl = f_fl, cm = f_cmax;
-    if (!step_begin(n, ext, acc, fl, cm)) return false;
+    if (!step_begin(n, stp, acc, fl, cm)) return false;
     f_acc = acc;
     f_fl = fl;
     f_cmax = cm;
@@ -357,23 +390,21 @@ TW_PRAGMA_UNROLL
   }
 
   // One macro step (see above).
-  template <class Sink>
-  ISIM_TW void step(const TreeNode *nodes, const TreeExt *ext, Sink &sink, uint32_t k0, uint32_t k1) {
+  template <class Nodes, class Sink>
+  ISIM_TW void step(const Nodes &nodes, const TreeExt *ext, const TreeStep *stp, Sink &sink, uint32_t k0,
+                    uint32_t k1) {
 #ifdef ISIM_TREE_DEBUG
-    if (sink.bad(p, f_pos, d, FRAMES)) {
+    if (sink.bad(p, f_pos, d, SPILL ? (int)kTreeMaxFrames : FRAMES)) {
       done = true;
       return;
     }
 #endif
     if (p >= end && !close(nodes, ext, sink)) return;
-#ifdef TW_CLOSE2S
-    if (p >= end && !close(nodes, ext, sink)) return;
-#endif
-    if (p < end) process(nodes, ext, sink, k0, k1);
+    if (p < end) process(nodes, ext, stp, sink, k0, k1);
     bool go = !done;
 TW_PRAGMA_UNROLL
     for (int i = 0; i < kScan; ++i) {
-      go = go && p < end && scan(nodes, ext);
+      go = go && p < end && scan(nodes, stp);
     }
     // and close the invocation if the walk has passed its subtree: a chain of
     // subtrees ending together takes half the steps (config 4: 12.5 -> 10.4

@@ -23,7 +23,7 @@ restatements of isotope's Python generators; they emit the same YAML schema).
 from __future__ import annotations
 
 import collections
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 import numpy as np
 
@@ -87,9 +87,11 @@ def barabasi_tree(n: int, power: float, zero_appeal: float, seed: int) -> np.nda
 def realistic_topology(n: int = 10, model: str = "multitier", seed: int = 42,
                        concurrent: bool = False, sleep_ms=None, error_rate=None,
                        request_size: int = 128, response_size: int = 128,
-                       num_replicas: int = 1) -> Dict[str, Any]:
+                       num_replicas: int = 1, probability: Optional[int] = None) -> Dict[str, Any]:
     """sleep_ms=(lo, hi) adds a leading sleep U{lo..hi} ms per service;
-    error_rate=(lo, hi) sets errorRate U[lo, hi] per service."""
+    error_rate=(lo, hi) sets errorRate U[lo, hi] per service; probability
+    (1..100) is set on every call command (request_command.go:30-32, the
+    reference runtime's only randomness: executable.go:84-90)."""
     power, zero_appeal = MODELS[model]
     parent = barabasi_tree(n, power, zero_appeal, seed)
     children: List[List[int]] = [[] for _ in range(n)]
@@ -102,7 +104,8 @@ def realistic_topology(n: int = 10, model: str = "multitier", seed: int = 42,
         script: List[Any] = []
         if sleep_ms is not None:
             script.append({"sleep": f"{int(rng.integers(sleep_ms[0], sleep_ms[1] + 1))}ms"})
-        calls = [{"call": f"mock-{c}"} for c in children[i]]
+        calls = [{"call": f"mock-{c}"} if probability is None else
+                 {"call": {"service": f"mock-{c}", "probability": probability}} for c in children[i]]
         if calls:
             script.extend([calls] if concurrent else calls)
         svc["script"] = script
@@ -142,6 +145,14 @@ def config3_topology(n: int = 10_000, seed: int = 42) -> Dict[str, Any]:
     sleep U{1..5} ms, errorRate U[0, 1%]."""
     return realistic_topology(n, "multitier", seed, concurrent=True, sleep_ms=(1, 5),
                               error_rate=(0.0, 0.01))
+
+
+def config3p_topology(probability: int = 50, n: int = 10_000, seed: int = 42) -> Dict[str, Any]:
+    """Config 3's graph (same tree, sleeps and error rates) with `probability`
+    on every call: a dynamic walk over a 10k-position tree (VERDICT r3 item 3,
+    bench.py --config c3p)."""
+    return realistic_topology(n, "multitier", seed, concurrent=True, sleep_ms=(1, 5),
+                              error_rate=(0.0, 0.01), probability=probability)
 
 
 def config2_topology() -> Dict[str, Any]:

@@ -27,23 +27,32 @@ using namespace isim;
 namespace {
 
 struct Sink {
+  const Program *prog = nullptr;
   std::vector<uint64_t> calls, errs;                // per slot
-  std::vector<uint64_t> sum200, sum500;             // per row
+  std::vector<uint64_t> sum200, sum500;             // per row (HBM in the kernel, or its LDS sums)
+  std::vector<std::vector<uint64_t>> gbucket;       // per row: [2][33] the global-atomic buckets
   std::vector<uint32_t> dyn;                        // the LDS bucket tables (tree_dyn layout)
   bool out_of_table = false;
   void call(uint32_t slot) { calls[slot] += 1; }
-  void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
-    const uint32_t row = roww & 0xFFFFu, off = roww >> 16;
+  void resp_leaf(uint32_t slot, bool st) {
     if (st) errs[slot] += 1;
-    if (off != kTreeStaticRow) {  // as tree.hip TreeSink::resp, with the range check made an error
-      const uint32_t lo = dyn[off] & 0xFFu, w = dyn[off] >> 8, b = prom_bucket_ns(T);
-      if (b < lo || b >= lo + w) out_of_table = true;
-      else dyn[off + 1 + (st ? w : 0) + (b - lo)] += 1;
+  }
+  void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
+    const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
+    if (st) errs[slot] += 1;
+    if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // as tree.hip TreeSink::resp: a row in global memory
+      if (place == kTreeGlobalDyn) gbucket[idx][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;
+      (st ? sum500 : sum200)[idx] += T;
+      return;
     }
-    (st ? sum500 : sum200)[row] += T;
+    if (place != kTreeStaticRow) {  // an LDS bucket table, with the range check made an error
+      const uint32_t lo = dyn[place] & 0xFFu, w = dyn[place] >> 8, b = prom_bucket_ns(T);
+      if (b < lo || b >= lo + w) out_of_table = true;
+      else dyn[place + 1 + (st ? w : 0) + (b - lo)] += 1;
+    }
+    (st ? sum500 : sum200)[prog->sum_row[idx]] += T;
   }
 };
-
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -78,31 +87,41 @@ int main(int argc, char **argv) {
     std::printf("why %s\n", prog.tree_why.c_str());
     return 3;
   }
-  std::fprintf(stderr, "positions %zu frames %u\n", prog.tree_nodes.size(), prog.tree_frames);
+  std::fprintf(stderr, "positions %zu frames %u lds %u nodes_lds %u wg_per_cu %u lds_rows %u\n", prog.tree_nodes.size(),
+               prog.tree_frames, prog.tree_layout.bytes, prog.tree_layout.nodes_lds, prog.tree_layout.wg_per_cu,
+               prog.tree_layout.n_sum);
   const uint32_t S = (uint32_t)prog.n_slots, R = (uint32_t)prog.row_svc.size();
   Sink sk;
+  sk.prog = &prog;
   sk.calls.assign(S, 0);
   sk.errs.assign(S, 0);
   sk.sum200.assign(R, 0);
   sk.sum500.assign(R, 0);
+  sk.gbucket.assign(R, std::vector<uint64_t>(2 * ISIM_N_PROM, 0));
   sk.dyn.assign(prog.tree_dyn_words, 0);
   for (const TreeDynRow &d : prog.tree_dyn) sk.dyn[d.off] = d.b_lo | (d.width << 8);
   std::vector<uint64_t> root_hist(2 * ISIM_N_PROM, 0), root_sum(2, 0);
   const bool modeb = p.error_mode == ISIM_MODE_B;
   // one Lane per depth variant, reused trace after trace as a GPU lane is
-  // (tree.hip hands a lane its next trace as soon as one responds)
+  // (tree.hip hands a lane its next trace as soon as one responds); the
+  // spilling variant keeps its deep frames in a vector, one column (stride 1)
+  std::vector<uint32_t> spill((size_t)kTreeMaxFrames * kTreeSpillWords, 0);
   tw::Lane<4, true> b4;
   tw::Lane<8, true> b8;
   tw::Lane<16, true> b16;
+  tw::Lane<8, true, true, true> bs;
   tw::Lane<4, false> a4;
   tw::Lane<8, false> a8;
   tw::Lane<16, false> a16;
+  tw::Lane<8, false, true, true> as;
+  bs.sp = as.sp = spill.data();
+  const tw::CpuNodes nodes{prog.tree_nodes.data()};
   for (uint64_t i = 0; i < n; ++i) {
     uint32_t lat = 0, hops = 0, errh = 0;
     bool r500 = false;
     auto run = [&](auto &L) {
       L.start(begin + i);
-      while (!L.done) L.step(prog.tree_nodes.data(), prog.tree_ext.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
       lat = L.lat;
       hops = L.hopn;
       errh = L.errh;
@@ -110,12 +129,15 @@ int main(int argc, char **argv) {
     };
     // the register-stack depth the device compiles for this graph (tree.hip tree_kernel)
     const uint32_t fr = prog.tree_frames;
+    const bool spills = fr > kTreeRegFrames || std::getenv("ISIM_TW_SPILL") != nullptr;
     if (modeb) {
-      if (fr <= 4) run(b4);
+      if (spills) run(bs);
+      else if (fr <= 4) run(b4);
       else if (fr <= 8) run(b8);
       else run(b16);
     } else {
-      if (fr <= 4) run(a4);
+      if (spills) run(as);
+      else if (fr <= 4) run(a4);
       else if (fr <= 8) run(a8);
       else run(a16);
     }
@@ -150,15 +172,21 @@ int main(int argc, char **argv) {
   for (uint32_t r = 0; r < R; ++r) {
     row[r][2 * ISIM_N_PROM] = sk.sum200[r];
     row[r][2 * ISIM_N_PROM + 1] = sk.sum500[r];
+    for (uint32_t w = 0; w < 2 * ISIM_N_PROM; ++w) row[r][w] += sk.gbucket[r][w];
   }
   for (const TreeDynRow &d : prog.tree_dyn)
     for (uint32_t code = 0; code < 2; ++code)
       for (uint32_t j = 0; j < d.width; ++j) row[d.row][code * ISIM_N_PROM + d.b_lo + j] += sk.dyn[d.off + 1 + code * d.width + j];
-  for (uint32_t s = 0; s < S; ++s) {
-    const uint32_t w = prog.slot_tbkt[s], r = w & kDurRowMask, b = w >> 24;
-    if (b == kTreeDynBucket) continue;
-    row[r][b] += sk.calls[s] - sk.errs[s];
-    row[r][ISIM_N_PROM + b] += sk.errs[s];
+  for (uint32_t s = 0; s < S; ++s) {  // the kernel's flush: static buckets and leaf sums from the counters
+    const uint32_t w = prog.slot_tbkt[s], r = w & kTreeRowMask, b = w >> 24;
+    if (b != kTreeDynBucket) {
+      row[r][b] += sk.calls[s] - sk.errs[s];
+      row[r][ISIM_N_PROM + b] += sk.errs[s];
+    }
+    if (w & kTreeLeafSlot) {
+      row[r][2 * ISIM_N_PROM] += (uint64_t)prog.slot_tc[s] * (sk.calls[s] - sk.errs[s]);
+      row[r][2 * ISIM_N_PROM + 1] += (uint64_t)prog.slot_tc[s] * sk.errs[s];
+    }
   }
   for (uint32_t w = 0; w < 2 * ISIM_N_PROM; ++w) row[0][w] += root_hist[w];
   row[0][2 * ISIM_N_PROM] += root_sum[0];

@@ -19,7 +19,7 @@ from hypothesis import strategies as st
 
 import kat
 from conftest import ROOT, TOPOLOGIES
-from isim.generators import mesh_topology, realistic_topology
+from isim.generators import config3p_topology, mesh_topology, realistic_topology
 from isim.yamljson import obj_to_json, yaml_to_json
 from oracle import executor as oc
 from oracle import graph_ref as gr
@@ -156,3 +156,46 @@ def test_realistic_static(checker, tmp_path):
     j = obj_to_json(realistic_topology(300, "multitier", 5, concurrent=True, sleep_ms=(1, 5), error_rate=(0, 0.1)))
     for mode in (0, 1):
         assert compare(checker, tmp_path, j, mode, n=300)
+
+
+@pytest.mark.parametrize("prob", [30, 70])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_config3p(checker, tmp_path, prob, mode):
+    """Config 3's 10k-service graph with a probability on every call (bench
+    --config c3p): 10,000 positions, 19 nested calling invocations (frames
+    below the 8 register frames spill), most duration rows outside the LDS
+    budget (global-memory sums and buckets), sleeps before every concurrent
+    step (mode B: TF_XPRE), errorRate draws everywhere."""
+    j = obj_to_json(config3p_topology(prob))
+    assert compare(checker, tmp_path, j, mode, n=150, begin=(1 << 32) - 70)
+
+
+def test_concurrent_sleeps_and_pre(checker, tmp_path):
+    """A concurrent step with sleep sub-commands (TF_XCMAX: the step starts at
+    its longest sleep) and sleeps between call steps (mode B: TF_XPRE; mode A
+    folds them into the caller's tc), with probabilistic calls and aborts."""
+    doc = {"defaults": {"requestSize": "1 KB", "responseSize": 2000},
+           "services": [
+               {"name": "front", "isEntrypoint": True, "errorRate": 0.05,
+                "script": [{"sleep": "3ms"}, {"call": {"service": "mid", "probability": 60}},
+                           [{"call": "leaf"}, {"call": {"service": "mid", "size": 5}}, {"sleep": "6ms"}],
+                           {"sleep": "1ms"}, {"call": {"service": "leaf", "size": 20000}}, {"sleep": "2ms"}]},
+               {"name": "mid", "errorRate": 0.2, "responseSize": 7,
+                "script": [{"sleep": "4ms"}, {"call": {"service": "leaf", "probability": 50}},
+                           [{"sleep": "9ms"}, {"call": {"service": "leaf", "probability": 40}}]]},
+               {"name": "leaf", "errorRate": 0.1, "script": [{"sleep": "2ms"}]}]}
+    for mode in (0, 1):
+        assert compare(checker, tmp_path, json.dumps(doc), mode, n=3000)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_spill_variant(checker, tmp_path, mode, monkeypatch):
+    """The spilling register stack (frames at depth >= 8 in memory) on graphs
+    whose walks go deeper than 8 calling invocations: the same results as the
+    oracle (ISIM_TW_SPILL makes the checker use the spilling Lane)."""
+    monkeypatch.setenv("ISIM_TW_SPILL", "1")
+    deep = realistic_topology(3000, "multitier", 5, concurrent=True, sleep_ms=(1, 3), error_rate=(0.0, 0.05),
+                              probability=80)
+    assert compare(checker, tmp_path, obj_to_json(deep), mode, n=300)
+    assert compare(checker, tmp_path, with_defaults(obj_to_json(mesh_topology(1200, 11, fanout=2, seed=5, probability=70)),
+                                                    errorRate=0.05), mode, n=1000)
