@@ -15,6 +15,12 @@
  * over the SERVICE GRAPH (as isim_oracle.c's invoke() does), so this shares
  * no code or layout with the product's position arrays and level scans.
  *
+ * Probabilistic calls (mode A): before the simulation, a walk of each trace
+ * (as isim_oracle.c's invoke(): shouldSkipRequest with Intn(100) := draw %
+ * 100, hop ids counting EXECUTED invocations in preorder) fixes which calls
+ * execute and every executed invocation's hop id; a skipped call sends no
+ * request, holds nothing and takes no time.
+ *
  * Reference anchors (the simulated behaviour, not a Go transcription):
  *   Handler.ServeHTTP          isotope/service/pkg/srv/handler.go:37-79
  *   executeRequestCommand      executable.go:94-144  (request -> callee ServeHTTP)
@@ -127,6 +133,7 @@ typedef struct {
     const oparams *p;
     const odes *d;
     uint32_t *size;   /* [n_services] invocations in a call of the service (subtree size) */
+    uint32_t *ncalls; /* [n_services] call commands of the script (concurrent sub-commands included) */
     uint64_t *hold;   /* [n_services] total sleep */
     int32_t *nrep;
 } sctx;
@@ -137,20 +144,64 @@ static uint32_t subtree(sctx *c, int32_t s) {
     if (c->size[s]) return c->size[s];
     const ograph *g = c->g;
     uint64_t n = 1, hold = 0;
+    uint32_t nc = 0;
     for (int32_t i = 0; i < g->step_len[s]; ++i) {
         const ocmd *x = &g->cmds[g->step_off[s] + i];
         if (x->kind == K_SLEEP) hold += sl(x->sleep_ns);
-        else if (x->kind == K_CALL) n += subtree(c, g->site_callee[x->site]);
-        else
+        else if (x->kind == K_CALL) {
+            n += subtree(c, g->site_callee[x->site]);
+            ++nc;
+        } else
             for (int32_t j = 0; j < x->sub_len; ++j) {
                 const ocmd *y = &g->cmds[x->sub_off + j];
                 if (y->kind == K_SLEEP) hold += sl(y->sleep_ns);
-                else n += subtree(c, g->site_callee[y->site]);
+                else {
+                    n += subtree(c, g->site_callee[y->site]);
+                    ++nc;
+                }
             }
     }
+    c->ncalls[s] = nc;
     c->size[s] = (uint32_t)n;
     c->hold[s] = hold;
     return (uint32_t)n;
+}
+
+/* ---- the executed invocations of one trace (mode A: skips only) ---- */
+#define NO_HOP 0xFFFFFFFFu
+typedef struct {
+    const sctx *c;
+    uint64_t t;
+    uint32_t next;       /* next hop id = executed invocations so far */
+    uint32_t kid_next;
+    uint32_t *kid_base;  /* [nodes] per hop: its entries in kid */
+    uint32_t *kid;       /* per (hop, call command k): the callee's hop, NO_HOP when skipped */
+} pwalk;
+
+/* shouldSkipRequest (executable.go:84-90) with Intn(100) := draw % 100 (isim_oracle.c skip_call) */
+static int skip_call(uint64_t seed, uint64_t t, uint32_t hop, int32_t k, int32_t q) {
+    if (q == 0 || q >= 100) return 0;
+    return draw(seed, t, hop, 1u + ((uint32_t)k >> 2), k & 3) % 100u < (uint32_t)(100 - q);
+}
+
+static uint32_t pre_walk(pwalk *w, int32_t s) {
+    const ograph *g = w->c->g;
+    const uint32_t hop = w->next++;
+    const uint32_t base = w->kid_next;
+    w->kid_base[hop] = base;
+    w->kid_next += w->c->ncalls[s];
+    for (int32_t i = 0; i < g->step_len[s]; ++i) {
+        const ocmd *x = &g->cmds[g->step_off[s] + i];
+        const int32_t nsub = x->kind == K_CONC ? x->sub_len : 1;
+        for (int32_t j = 0; j < nsub; ++j) {
+            const ocmd *y = x->kind == K_CONC ? &g->cmds[x->sub_off + j] : x;
+            if (y->kind != K_CALL) continue;
+            w->kid[base + (uint32_t)y->k] = skip_call(w->c->p->seed, w->t, hop, y->k, g->site_prob[y->site])
+                                                ? NO_HOP
+                                                : pre_walk(w, g->site_callee[y->site]);
+        }
+    }
+    return hop;
 }
 
 /* ---- event heap ---- */
@@ -209,6 +260,7 @@ static ev hpop(heap *h) {
 typedef struct {
     sctx *c;
     const uint64_t *S, *A;  /* [nodes] start and arrival of this trace's invocations */
+    const uint32_t *kid_base, *kid;  /* the trace's executed calls (pwalk) */
     uint64_t t;
     uint64_t *st, *des;
     uint32_t err_hops;
@@ -221,7 +273,7 @@ static uint64_t finish(fstate *f, int32_t s, uint32_t hop, int *err) {
     uint64_t *st = f->st;
     st[ST_SVC + s] += 1;  /* RecordRequestReceived */
     uint64_t T = f->S[hop];
-    uint32_t next = hop + 1;
+    const uint32_t *kid = f->kid + f->kid_base[hop];
     int failed = 0;
     for (int32_t i = 0; i < g->step_len[s] && !failed; ++i) {
         const ocmd *x = &g->cmds[g->step_off[s] + i];
@@ -229,8 +281,8 @@ static uint64_t finish(fstate *f, int32_t s, uint32_t hop, int *err) {
             T += sl(x->sleep_ns);
         } else if (x->kind == K_CALL) {
             int e = 0;
-            const uint32_t h = next;
-            next += c->size[g->site_callee[x->site]];
+            const uint32_t h = kid[x->k];
+            if (h == NO_HOP) continue;  /* skipped: no request, no time */
             T = finish(f, g->site_callee[x->site], h, &e);  /* response at the callee's finish */
             st[ST_SVC + 2 * (uint64_t)g->n_services + (uint64_t)x->site] += 1;
             if (f->c->p->error_mode == 1 && e) failed = 1;
@@ -244,8 +296,8 @@ static uint64_t finish(fstate *f, int32_t s, uint32_t hop, int *err) {
                     end = T + sl(y->sleep_ns);
                 } else {
                     int e = 0;
-                    const uint32_t h = next;
-                    next += c->size[g->site_callee[y->site]];
+                    const uint32_t h = kid[y->k];
+                    if (h == NO_HOP) continue;
                     end = finish(f, g->site_callee[y->site], h, &e);
                     st[ST_SVC + 2 * (uint64_t)g->n_services + (uint64_t)y->site] += 1;
                     if (f->c->p->error_mode == 1 && e) cerr = 1;
@@ -294,6 +346,7 @@ typedef struct {
     istate *is;      /* [n_traces][nodes] */
     uint32_t nodes;
     uint64_t trace_begin;
+    const uint32_t *kid_base, *kid;  /* [n_traces][nodes]: the executed calls (pwalk) */
 } sim;
 
 static int advance(sim *m, uint64_t i, uint32_t hop);
@@ -306,17 +359,18 @@ static int notify(sim *m, uint64_t i, uint32_t hop, uint64_t fin) {
     return advance(m, i, hop);
 }
 
+/* 0: skipped (no request); 1: sent; -1: out of memory */
 static int push_call(sim *m, uint64_t i, istate *st, uint32_t hop, const ocmd *x) {
     const ograph *g = m->c->g;
     const int32_t cs = g->site_callee[x->site];
-    const uint32_t ch = st->next;
-    st->next += m->c->size[cs];
+    const uint32_t ch = m->kid[i * m->nodes + m->kid_base[i * m->nodes + hop] + (uint32_t)x->k];
+    if (ch == NO_HOP) return 0;
     istate *cst = &m->is[i * m->nodes + ch];
     cst->parent = hop;
     cst->svc = cs;
     ev ce = {st->T + g->site_hop[x->site], m->trace_begin + i, ch, cs};
     st->pending++;
-    return hpush(m->h, ce);
+    return hpush(m->h, ce) ? 1 : -1;
 }
 
 static int advance(sim *m, uint64_t i, uint32_t hop) {
@@ -330,8 +384,9 @@ static int advance(sim *m, uint64_t i, uint32_t hop) {
             st->T += sl(x->sleep_ns);
         } else if (x->kind == K_CALL) {
             st->runmax = st->T;
-            if (!push_call(m, i, st, hop, x)) return 0;
-            return 1;  /* waits for the callee */
+            const int r = push_call(m, i, st, hop, x);
+            if (r < 0) return 0;
+            if (r > 0) return 1;  /* waits for the callee */
         } else {
             uint64_t smax = 0;
             for (int32_t j = 0; j < x->sub_len; ++j) {
@@ -341,7 +396,7 @@ static int advance(sim *m, uint64_t i, uint32_t hop) {
             st->runmax = st->T + smax;
             for (int32_t j = 0; j < x->sub_len; ++j) {
                 const ocmd *y = &g->cmds[x->sub_off + j];
-                if (y->kind == K_CALL && !push_call(m, i, st, hop, y)) return 0;
+                if (y->kind == K_CALL && push_call(m, i, st, hop, y) < 0) return 0;
             }
             if (st->pending) return 1;  /* waits for all callees */
             st->T = st->runmax;
@@ -367,8 +422,9 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
     c.p = p;
     c.d = d;
     c.size = (uint32_t *)calloc((size_t)n, sizeof(uint32_t));
+    c.ncalls = (uint32_t *)calloc((size_t)n, sizeof(uint32_t));
     c.hold = (uint64_t *)calloc((size_t)n, sizeof(uint64_t));
-    if (!c.size || !c.hold) return 2;
+    if (!c.size || !c.ncalls || !c.hold) return 2;
     const uint32_t nodes = subtree(&c, p->entry);
     /* replica queues: busy-until per (service, replica) */
     uint64_t *qoff = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
@@ -388,12 +444,20 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
         if (!hpush(&h, e)) return 2;
     }
     istate *is = (istate *)calloc((size_t)n_traces * nodes, sizeof(istate));
-    if (!is) return 2;
+    /* each trace's executed calls and hop ids (every call command of an
+     * executed invocation is a distinct potential position: <= nodes entries) */
+    uint32_t *kid_base = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * nodes * sizeof(uint32_t));
+    uint32_t *kid = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * nodes * sizeof(uint32_t));
+    uint32_t *hops = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * sizeof(uint32_t));
+    if (!is || !kid_base || !kid || !hops) return 2;
     for (uint64_t i = 0; i < n_traces; ++i) {
         is[i * nodes].parent = NO_PARENT;
         is[i * nodes].svc = p->entry;
+        pwalk w = {&c, trace_begin + i, 0, 0, kid_base + i * nodes, kid + i * nodes};
+        (void)pre_walk(&w, p->entry);
+        hops[i] = w.next;
     }
-    sim m = {&c, &h, is, nodes, trace_begin};
+    sim m = {&c, &h, is, nodes, trace_begin, kid_base, kid};
     while (h.n) {
         const ev e = hpop(&h);
         const uint64_t i = e.t - trace_begin;
@@ -410,23 +474,22 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
         st->T = start;
         st->step = 0;
         st->pending = 0;
-        st->next = e.hop + 1;
         if (!advance(&m, i, e.hop)) return 2;
     }
     free(is);
     stats[5] = ~0ull;
     for (uint64_t i = 0; i < n_traces; ++i) {
-        fstate f = {&c, S + i * nodes, A + i * nodes, trace_begin + i, stats, des, 0};
+        fstate f = {&c, S + i * nodes, A + i * nodes, kid_base + i * nodes, kid + i * nodes, trace_begin + i, stats, des, 0};
         int e = 0;
         const uint64_t F = finish(&f, p->entry, 0, &e);
         const uint64_t L = F - arr[i];
         if (records) {
             records[2 * i] = L;
-            records[2 * i + 1] = (uint64_t)nodes | ((uint64_t)(((uint32_t)e << 31) | f.err_hops) << 32);
+            records[2 * i + 1] = (uint64_t)hops[i] | ((uint64_t)(((uint32_t)e << 31) | f.err_hops) << 32);
         }
         stats[0] += 1;
         stats[1] += L;
-        stats[2] += nodes;
+        stats[2] += hops[i];
         stats[3] += f.err_hops;
         stats[4] += (uint64_t)e;
         if (L < stats[5]) stats[5] = L;
@@ -436,12 +499,16 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
         stats[ST_LOG2 + e * N_LOG2 + l] += 1;
     }
     free(h.v);
+    free(hops);
+    free(kid);
+    free(kid_base);
     free(arr);
     free(A);
     free(S);
     free(busy);
     free(qoff);
     free(c.hold);
+    free(c.ncalls);
     free(c.size);
     return 0;
 }

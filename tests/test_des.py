@@ -172,6 +172,17 @@ def _canonical_doc():
     return json.loads(yaml_to_json(open(os.path.join(TOPOLOGIES, "canonical.yaml"), "rb").read()))
 
 
+def _prob_canonical():
+    doc = _canonical_doc()
+    for sv in doc["services"]:
+        for st in sv.get("script", []):
+            for c in (st if isinstance(st, list) else [st]):
+                if "call" in c:
+                    c["call"] = {"service": c["call"] if isinstance(c["call"], str) else c["call"]["service"],
+                                 "probability": 50}
+    return doc
+
+
 @pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
 @pytest.mark.parametrize("doc", [tree_topology(3, 3), tree_topology(4, 4),
                                  realistic_topology(300, concurrent=True, error_rate=(0.0, 0.3)),
@@ -196,6 +207,44 @@ def test_event_oracle_without_holds_is_the_static_walk(doc, mode):
     assert des[:, od.DES_ROW - 3].sum() == 0  # no waits
     # durations: the static walk's per-service table
     assert np.array_equal(des[:, :68], o["svc_dur"])
+
+
+@pytest.mark.parametrize("doc", [realistic_topology(300, concurrent=True, error_rate=(0.0, 0.3), probability=60),
+                                 realistic_topology(300, error_rate=(0.0, 0.3), probability=75),
+                                 mesh_topology(800, 4), _prob_canonical()],
+                         ids=["realistic300p60", "realistic300seq_p75", "mesh800", "canonical_p50"])
+def test_event_oracle_probabilistic_without_holds_is_the_walk(doc):
+    """Probabilistic calls (mode A): the event oracle's pre-walk fixes the
+    executed calls and hop ids (executable.go:84-90, semantics v1 §2.3); with
+    no holds nothing queues, so every trace must equal the walk oracle's
+    (latency, hops, status, err_hops) and the per-service durations its table."""
+    doc = json.loads(json.dumps(doc))
+    doc.setdefault("defaults", {})["errorRate"] = 0.2
+    h, sg, op = _oracle_case(doc)
+    assert not h.info.static_walk
+    n = 700
+    rs, ss = oc.run(sg, op, sg.entry(), (1 << 32) - 300, n)
+    rd, sd, des = od.run(sg, op, sg.entry(), (1 << 32) - 300, n, 1_000_000)
+    assert np.array_equal(rs, rd)
+    o = oc.split_stats(ss, len(sg.g.services), len(sg.sites))
+    assert np.array_equal(ss[:len(sd)], sd)
+    assert des[:, od.DES_ROW - 3].sum() == 0
+    assert np.array_equal(des[:, :68], o["svc_dur"])
+    assert 0 < int(ss[2]) < n * int(h.info.hops_upper)  # some calls were skipped
+
+
+@pytest.mark.parametrize("prob", [40, 80])
+def test_event_oracle_probabilistic_tree_spaced_arrivals(prob):
+    """A probabilistic tree with sleeps (holds) whose traces never overlap
+    (mean gap far above any latency): every service is invoked at most once
+    per trace, so no invocation ever waits and the latencies are the walk's."""
+    doc = realistic_topology(200, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.1), probability=prob)
+    h, sg, op = _oracle_case(doc)
+    n = 300
+    rs, _ = oc.run(sg, op, sg.entry(), 77, n)
+    rd, _, des = od.run(sg, op, sg.entry(), 77, n, 1 << 40)
+    assert np.array_equal(rs, rd)
+    assert des[:, od.DES_ROW - 3].sum() == 0
 
 
 @pytest.mark.parametrize("mean", [400_000, 3_000_000, 20_000_000])
