@@ -218,7 +218,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
     st.kind = 7;
     st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames,
                                   p.tree_frames > isim::kTreeRegFrames, p.tree_layout.nodes_lds != 0,
-                                  (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0);
+                                  (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
+                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"));
     st.lds_bytes = p.tree_layout.bytes;
     st.lds_counters = 1;
     // the workgroup size with the most resident waves per CU (registers and

@@ -212,13 +212,15 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters);
 // kind 7 variant (tree.hip, compiled once per mode and concurrency):
 // register-stack depth (4, 6, 8, 12, 16; `spill`: 8 registers + the rest in
 // global memory), nodes in LDS or global, the error-block cache.
-void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw);
-void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw);
-void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw);
-void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw);
-inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw) {
-  if (modeb) return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw) : tree_kernel_m1c0(frames, spill, nodes_lds, draw);
-  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw) : tree_kernel_m0c0(frames, spill, nodes_lds, draw);
+void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
+void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
+void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
+void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
+// occ2: the LDS layout fits two workgroups per CU (kernels built for 80 VGPRs)
+inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw, bool occ2) {
+  if (modeb)
+    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2) : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2);
+  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2) : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2);
 }
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

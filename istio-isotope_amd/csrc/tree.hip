@@ -143,13 +143,11 @@ struct TreeSink {
   }
 };
 
-// Waves per SIMD the register allocation must allow: 6 for stacks of up to 8
-// frames (80 VGPRs: two 768-thread workgroups per CU), 4 for deeper stacks.
-#ifndef TREE_WPE
-#define TREE_WPE 6
-#endif
-template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW>
-__global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
+// WPE: waves per SIMD the register allocation must allow — 6 (80 VGPRs: two
+// 768-thread workgroups per CU) when the LDS layout fits half the CU, else 4
+// (one 1024-thread workgroup per CU: up to 128 VGPRs, no spills).
+template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE>
+__global__ void __launch_bounds__(kWgThreads, WPE)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
   extern __shared__ __align__(16) unsigned char lds[];
@@ -239,8 +237,8 @@ __global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
         uint4 r;
         r.x = lat;
         r.y = 0u;
-        r.z = L.hopn;
-        r.w = (is500 ? 0x80000000u : 0u) | L.errh;
+        r.z = L.hops();
+        r.w = (is500 ? 0x80000000u : 0u) | L.errs();
         if (c.records) *reinterpret_cast<uint4 *>(c.records + idx) = r;
         const uint32_t nl = a_lat + lat;
         if (nl < a_lat) lds_add(&c.acc->sum_latency, 1ull << 32);
@@ -250,8 +248,8 @@ __global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
           if (n5 < a_lat500) lds_add(&c.acc->sum_latency500, 1ull << 32);
           a_lat500 = n5;
         }
-        a_hops += L.hopn;
-        a_err += L.errh;
+        a_hops += L.hops();
+        a_err += L.errs();
         a_max = lat > a_max ? lat : a_max;
         a_min = lat < a_min ? lat : a_min;
         active = false;
@@ -390,7 +388,7 @@ __global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
 }  // namespace dev
 
 // The variants of one (mode, concurrency) pair: this file is compiled once
-// per pair (Makefile: tree_m<MODEB>c<CONC>.o) so the 96 kernels build in
+// per pair (Makefile: tree_m<MODEB>c<CONC>.o) so the 144 kernels build in
 // parallel.  Register-stack depths: the smallest of 4, 6, 8, 12, 16 that
 // holds the graph's frames, else 8 registers + a global spill; nodes in LDS
 // when the layout holds them; the error-block cache only with error draws.
@@ -401,23 +399,28 @@ __global__ void __launch_bounds__(kWgThreads, FRAMES <= 8 ? TREE_WPE : 4)
 #define TREE_CONC 0
 #endif
 template <bool NLDS, bool DRAW>
-static void *tree_pick(uint32_t frames, bool spill) {
+static void *tree_pick(uint32_t frames, bool spill, bool occ2) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
-  if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW>;
-  if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW>;
-  if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW>;
-  if (frames <= 8) return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW>;
-  if (frames <= 12) return (void *)&isim_tree<M, 12, false, NLDS, C, DRAW>;
-  return (void *)&isim_tree<M, 16, false, NLDS, C, DRAW>;
+  if (occ2 && !spill && frames <= 8) {
+    if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, 6>;
+    if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW, 6>;
+    return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, 6>;
+  }
+  if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW, 4>;
+  if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, 4>;
+  if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW, 4>;
+  if (frames <= 8) return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, 4>;
+  if (frames <= 12) return (void *)&isim_tree<M, 12, false, NLDS, C, DRAW, 4>;
+  return (void *)&isim_tree<M, 16, false, NLDS, C, DRAW, 4>;
 }
 
 #define TREE_CAT2(a, b, c) a##b##c
 #define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
 void *TREE_CAT(tree_kernel_m, TREE_MODEB, TREE_CAT(c, TREE_CONC, ))(uint32_t frames, bool spill, bool nodes_lds,
-                                                                      bool draw) {
-  if (nodes_lds) return draw ? tree_pick<true, true>(frames, spill) : tree_pick<true, false>(frames, spill);
-  return draw ? tree_pick<false, true>(frames, spill) : tree_pick<false, false>(frames, spill);
+                                                                      bool draw, bool occ2) {
+  if (nodes_lds) return draw ? tree_pick<true, true>(frames, spill, occ2) : tree_pick<true, false>(frames, spill, occ2);
+  return draw ? tree_pick<false, true>(frames, spill, occ2) : tree_pick<false, false>(frames, spill, occ2);
 }
 
 }  // namespace isim

@@ -148,12 +148,19 @@ ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true>
 struct Lane {
   uint32_t t_lo = 0, t_hi = 0;
-  uint32_t p = 0, d = 0, end = 0, hopn = 0, errh = 0;
+  uint32_t p = 0, d = 0, end = 0;
+  uint32_t he = 0;  // executed invocations (hop ids handed out) | invocations that responded 500 << 16
   bool done = true;
   uint32_t lat = 0;
   bool root500 = false;
-  // current invocation (f_fl: FL_* | call block of f_res << KB_SHIFT)
-  uint32_t f_pos = 0, f_acc = 0, f_cmax = 0, f_hop = 0, f_fl = 0, f_res = 0;
+  // current invocation: f_hf = hop | fl << 16 (fl: FL_* | call block of f_res << KB_SHIFT), packed
+  // as its frame is (one register fewer; HF() shifts a flag into place)
+  uint32_t f_pos = 0, f_acc = 0, f_cmax = 0, f_hf = 0, f_res = 0;
+  static constexpr uint32_t HF(uint32_t fl) { return fl << 16; }
+  ISIM_TW uint32_t hops() const { return he & 0xFFFFu; }
+  ISIM_TW uint32_t errs() const { return he >> 16; }
+  ISIM_TW uint32_t f_kb() const { return (f_hf >> (16 + KB_SHIFT)) & KB_NONE; }
+  ISIM_TW void set_kb(uint32_t kb) { f_hf = (f_hf & ~HF(KB_NONE << KB_SHIFT)) | HF(kb << KB_SHIFT); }
   // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time
   uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1],
       s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
@@ -194,27 +201,26 @@ struct Lane {
     t_lo = (uint32_t)trace;
     t_hi = (uint32_t)(trace >> 32);
     done = false;
-    hopn = 0;
-    errh = 0;
+    he = 0;
     d = 0;
     ek_blk = 0xFFFFFFFFu;  // the error block belongs to the previous trace of the lane
     p = 0;
     end = 1;
-    f_fl = 0;
+    f_hf = 0;
   }
 
   ISIM_TW void fold(uint32_t c, bool st, bool conc) {
     if (CONC && conc) {
       f_cmax = c > f_cmax ? c : f_cmax;
-      if (MODEB && st) f_fl |= FL_CERR;
+      if (MODEB && st) f_hf |= HF(FL_CERR);
     } else {
       f_acc += c;
-      if (MODEB && st) f_fl |= FL_FAILED;
+      if (MODEB && st) f_hf |= HF(FL_FAILED);
     }
   }
 
   ISIM_TW void push() {
-    const uint32_t pe = f_pos | (end << 16), hf = f_hop | (f_fl << 16);
+    const uint32_t pe = f_pos | (end << 16), hf = f_hf;
     if (SPILL && d >= (uint32_t)FRAMES) {
       uint32_t *q = sp + (d - (uint32_t)FRAMES) * kTreeSpillWords * sp_stride;
       q[0] = pe;
@@ -259,8 +265,7 @@ TW_PRAGMA_UNROLL
     }
     f_pos = pe & 0xFFFFu;
     end = pe >> 16;
-    f_hop = hf & 0xFFFFu;
-    f_fl = hf >> 16;
+    f_hf = hf;
     f_res = r;
     f_acc = a;
     f_cmax = c;
@@ -273,12 +278,12 @@ TW_PRAGMA_UNROLL
   // script has failed (mode B: it runs no further step).
   ISIM_TW bool step_begin(const NodeW &n, const TreeStep *stp, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
     if (!(n.flags() & TF_STEP)) return true;
-    if (CONC && (fl & FL_INCONC)) {
+    if (CONC && (fl & HF(FL_INCONC))) {
       acc += cm;
-      if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
-      fl &= ~(FL_INCONC | FL_CERR);
+      if (MODEB && (fl & HF(FL_CERR))) fl |= HF(FL_FAILED);
+      fl &= ~HF(FL_INCONC | FL_CERR);
     }
-    if (MODEB && (fl & FL_FAILED)) return false;
+    if (MODEB && (fl & HF(FL_FAILED))) return false;
     if (n.flags() & (TF_XPRE | TF_XCMAX)) {
       const TreeStep x = stp[p];
       if (MODEB) acc += x.pre;  // TF_XPRE is never set in mode A (pre is 0 here then)
@@ -286,7 +291,7 @@ TW_PRAGMA_UNROLL
     } else {
       cm = 0;
     }
-    if (CONC && (n.flags() & TF_CONC)) fl |= FL_INCONC;
+    if (CONC && (n.flags() & TF_CONC)) fl |= HF(FL_INCONC);
     return true;
   }
 
@@ -298,16 +303,16 @@ TW_PRAGMA_UNROLL
   // close f_pos: its response folds into its caller (false: the entry responded)
   template <class Nodes, class Sink>
   ISIM_TW bool close(const Nodes &nodes, const TreeExt *ext, Sink &sink) {
-    uint32_t T = f_acc, fl = f_fl;
-    if (CONC && (fl & FL_INCONC)) {
+    uint32_t T = f_acc, fl = f_hf;
+    if (CONC && (fl & HF(FL_INCONC))) {
       T += f_cmax;
-      if (MODEB && (fl & FL_CERR)) fl |= FL_FAILED;
+      if (MODEB && (fl & HF(FL_CERR))) fl |= HF(FL_FAILED);
     }
     const TreeExt x = load_ext(ext, f_pos);
-    const bool failed = MODEB && (fl & FL_FAILED);
+    const bool failed = MODEB && (fl & HF(FL_FAILED));
     if (!failed) T += x.tc;
-    const bool st = failed || (fl & FL_OWN);
-    errh += st ? 1u : 0u;
+    const bool st = failed || (fl & HF(FL_OWN));
+    he += st ? 0x10000u : 0u;
     if (f_pos == 0) {
       done = true;
       lat = T;
@@ -316,7 +321,7 @@ TW_PRAGMA_UNROLL
     }
     sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
     const uint32_t c = x.H + T;
-    const bool cc = (fl & FL_CONC_CHILD) != 0;
+    const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
     pop();
     fold(c, st, cc);
     return true;
@@ -327,29 +332,30 @@ TW_PRAGMA_UNROLL
   ISIM_TW void process(const Nodes &nodes, const TreeExt *ext, const TreeStep *stp, Sink &sink, uint32_t k0,
                        uint32_t k1) {
     const NodeW n = nodes.load(p);
-    if (!step_begin(n, stp, f_acc, f_fl, f_cmax)) {  // mode B: the script stops, close at the subtree's end
+    if (!step_begin(n, stp, f_acc, f_hf, f_cmax)) {  // mode B: the script stops, close at the subtree's end
       p = end;
       return;
     }
     if (n.prob()) {  // shouldSkipRequest: word (k & 3) of Philox((t, caller hop, 1 + k/4, 0)) % 100 < 100 - p
       const uint32_t kb = (uint32_t)n.k() >> 2;
-      if (((f_fl >> KB_SHIFT) & KB_NONE) != kb) {  // a call block past the first four calls
-        f_res = residues(f_hop, kb, k0, k1);
-        f_fl = (f_fl & ~(KB_NONE << KB_SHIFT)) | (kb << KB_SHIFT);
+      if (f_kb() != kb) {  // a call block past the first four calls
+        f_res = residues(f_hf & 0xFFFFu, kb, k0, k1);
+        set_kb(kb);
       }
       if (skipped(n)) {
         p += n.size();
         return;
       }
     }
-    const uint32_t hop = hopn++;
+    const uint32_t hop = he & 0xFFFFu;
+    he += 1u;
     const uint32_t fl = n.flags();
     const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
     if (!entry) sink.call(n.slot());
     if (fl & TF_LEAF) {
       const TreeExt x = load_ext(ext, p);
       const bool own = own_error(hop, fl, x.thr, k0, k1);
-      errh += own ? 1u : 0u;
+      he += own ? 0x10000u : 0u;
       if (entry) {
         done = true;
         lat = x.tc;
@@ -367,10 +373,9 @@ TW_PRAGMA_UNROLL
     f_pos = p;
     f_acc = 0;
     f_cmax = 0;
-    f_hop = hop;
     const bool pk = (fl & TF_PROBK0) != 0;
     f_res = pk ? residues(hop, 0, k0, k1) : 0u;
-    f_fl = (own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT);
+    f_hf = hop | HF((own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT));
     end = p + n.size();
     p += 1;
   }
@@ -379,11 +384,11 @@ TW_PRAGMA_UNROLL
   template <class Nodes>
   ISIM_TW bool scan(const Nodes &nodes, const TreeStep *stp) {
     const NodeW n = nodes.load(p);
-    if (!n.prob() || (((f_fl >> KB_SHIFT) & KB_NONE) != ((uint32_t)n.k() >> 2)) || !skipped(n)) return false;
-    uint32_t acc = f_acc, fl = f_fl, cm = f_cmax;
+    if (!n.prob() || f_kb() != ((uint32_t)n.k() >> 2) || !skipped(n)) return false;
+    uint32_t acc = f_acc, fl = f_hf, cm = f_cmax;
     if (!step_begin(n, stp, acc, fl, cm)) return false;
     f_acc = acc;
-    f_fl = fl;
+    f_hf = fl;
     f_cmax = cm;
     p += n.size();
     return true;

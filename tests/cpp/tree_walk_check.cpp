@@ -123,8 +123,8 @@ int main(int argc, char **argv) {
       L.start(begin + i);
       while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
       lat = L.lat;
-      hops = L.hopn;
-      errh = L.errh;
+      hops = L.hops();
+      errh = L.errs();
       r500 = L.root500;
     };
     // the register-stack depth the device compiles for this graph (tree.hip tree_kernel)
