@@ -152,6 +152,8 @@ struct TreeLayout {
   uint32_t nodes_lds;   // 1: the nodes in LDS; 0: read from global memory
   uint32_t wg_per_cu;   // 2: the layout fits kTreeLdsHalf
   uint32_t n_sum;       // LDS sum rows
+  uint32_t cnt16;       // 1: one u32 per slot, calls | 500s << 16, each kept below 2^15 (a field reaching
+                        // 2^15 moves 2^15 to the stats at once); 0: [2][n_slots] u32
 };
 
 // Scalar kernel arguments (the program, records and stats pointers are

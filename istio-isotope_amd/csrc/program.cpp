@@ -2,6 +2,7 @@
 #include "program.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "gounits.h"
@@ -83,6 +84,8 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   const uint32_t P = (uint32_t)out.tree_nodes.size(), S = (uint32_t)out.n_slots;
   const uint32_t R = (uint32_t)out.row_svc.size();
   const uint32_t head = kLdsAccBytes + kHistWords * 4u;
+  // per-slot counters: guarded 16-bit pairs (4 B per slot; ISIM_TREE_CNT32 set: two u32, A/B measurements)
+  const uint32_t cb = std::getenv("ISIM_TREE_CNT32") ? 8u : 4u;
   // rows by heat (the entry's row, 0, is the end-to-end histogram: no LDS row)
   std::vector<uint32_t> order;
   for (uint32_t r = 1; r < R; ++r)
@@ -94,9 +97,11 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   };
   const Cand cands[4] = {{true, kTreeLdsHalf}, {true, kTreeLdsFull}, {false, kTreeLdsHalf}, {false, kTreeLdsFull}};
   int pick = -1;
+  // ISIM_TREE_NODES_GLOBAL set: only the layouts with the nodes in global memory (A/B measurements)
+  const int first = std::getenv("ISIM_TREE_NODES_GLOBAL") ? 2 : 0;
   for (int pass = 0; pass < 2 && pick < 0; ++pass) {
-    for (int i = 0; i < 4 && pick < 0; ++i) {
-      uint32_t fixed = ((head + 8u * S + 7u) & ~7u) + (cands[i].nodes ? 8u * P + 8u : 0u);
+    for (int i = first; i < 4 && pick < 0; ++i) {
+      uint32_t fixed = ((head + cb * S + 7u) & ~7u) + (cands[i].nodes ? 8u * P + 8u : 0u);
       if (fixed > cands[i].limit) continue;
       uint32_t all = fixed;
       for (uint32_t r : order) all += 8u + 4u * (row_bw[r] ? 1u + 2u * row_bw[r] : 0u);
@@ -110,7 +115,8 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   L.nodes_lds = c.nodes ? 1u : 0u;
   L.wg_per_cu = c.limit == kTreeLdsHalf ? 2u : 1u;
   L.off_cnt = head;
-  L.off_sums = (head + 8u * S + 7u) & ~7u;
+  L.cnt16 = cb == 4u ? 1u : 0u;
+  L.off_sums = (head + cb * S + 7u) & ~7u;
   uint32_t room = c.limit - L.off_sums - (c.nodes ? 8u * P + 8u : 0u);
   // rows into LDS while they fit: a sum word, and the bucket table when the bucket varies
   out.tree_row_place.assign(R, kTreeGlobalStatic);

@@ -51,6 +51,9 @@ __device__ __forceinline__ void lds_add(uint32_t *p, uint32_t v) {
 __device__ __forceinline__ void lds_add(unsigned long long *p, unsigned long long v) {
   __hip_atomic_fetch_add((lds_u64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t *p, uint32_t v) {
+  return __hip_atomic_fetch_add((lds_u32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Row of a duration-table word.  The empty asm hides the mask from the
 // AMDGPU backend (ROCm 7.2 LLVM): with the mask's known bits it formed a u24
@@ -81,12 +84,43 @@ struct GlobalNodes {
 };
 
 struct TreeSink {
-  uint32_t *cnt;                // LDS [2][n_slots]: executed calls, callee 500s
+  uint32_t *cnt;                // LDS: per slot calls | 500s << 16 (cnt16), else [2][n_slots] u32
   unsigned long long *sum200;   // LDS [n_sum]
   uint32_t *dyn;                // LDS bucket tables of the varying rows
   uint64_t *svc_tab;            // HBM duration table, or null (ISIM_FLAG_NO_SVC_DUR)
   const uint32_t *sum_row;      // per LDS sum index: its row (code-500 sums go to HBM)
   uint32_t n_slots;
+  bool cnt16;
+  unsigned long long *sites;    // stats: [2][n_slots] executed calls, callee 500s
+  const uint32_t *slot_tbkt, *slot_tc;
+  // A guarded 16-bit field reached 2^15: 2^15 of its events go to the stats
+  // now, with what the flush derives from them (static duration buckets,
+  // leaf-callee sums; for 500s, moved from code 200 to code 500)
+  __device__ __attribute__((noinline)) void move(uint32_t slot, bool err) {
+    constexpr unsigned long long K = 0x8000ull;
+    atomicAdd(sites + (err ? n_slots : 0u) + slot, K);
+    lds_add(cnt + slot, err ? 0x80000000u : 0xFFFF8000u);  // the field less 2^15 (no borrow: it is >= 2^15)
+    if (!svc_tab) return;
+    const uint32_t w = slot_tbkt[slot], bk = w >> 24;
+    unsigned long long *row = (unsigned long long *)(svc_tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS);
+    const unsigned long long tk = (w & kTreeLeafSlot) ? (unsigned long long)slot_tc[slot] * K : 0ull;
+    if (bk != kTreeDynBucket) {
+      atomicAdd(row + bk, err ? 0ull - K : K);
+      if (err) atomicAdd(row + ISIM_N_PROM + bk, K);
+    }
+    if (tk) {
+      atomicAdd(row + 2 * ISIM_N_PROM, err ? 0ull - tk : tk);
+      if (err) atomicAdd(row + 2 * ISIM_N_PROM + 1, tk);
+    }
+  }
+  __device__ __forceinline__ void count(uint32_t slot, bool err) {
+    if (cnt16) {
+      const uint32_t old = lds_add_rtn(cnt + slot, err ? 0x10000u : 1u);
+      if (((old >> (err ? 16 : 0)) & 0xFFFFu) == 0x7FFFu) move(slot, err);
+    } else {
+      lds_add(cnt + (err ? n_slots : 0u) + slot, 1u);
+    }
+  }
 #ifdef ISIM_TREE_DEBUG
   uint32_t n_pos, n_rows;
   unsigned long long *dbg;
@@ -103,14 +137,14 @@ struct TreeSink {
 #ifdef ISIM_TREE_DEBUG
     if (slot >= n_slots) { atomicOr(dbg, 16ull); return; }
 #endif
-    lds_add(cnt + slot, 1u);
+    count(slot, false);
   }
   // a leaf callee: its duration is static (bucket and sums follow from the counters at the flush)
   __device__ __forceinline__ void resp_leaf(uint32_t slot, bool st) {
 #ifdef TREE_NO_SINK
     return;
 #endif
-    if (st) lds_add(cnt + n_slots + slot, 1u);
+    if (st) count(slot, true);
   }
   __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
 #ifdef TREE_NO_SINK
@@ -119,7 +153,7 @@ struct TreeSink {
 #ifdef ISIM_TREE_DEBUG
     if (slot >= n_slots) { atomicOr(dbg, 32ull); return; }
 #endif
-    if (st) lds_add(cnt + n_slots + slot, 1u);
+    if (st) count(slot, true);
     if (!svc_tab) return;
     const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
     if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // a cold row: sums (and varying buckets) by global atomics
@@ -177,7 +211,8 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     dyn[d.off] = d.b_lo | (d.width << 8);
   }
   __syncthreads();
-  TreeSink sink{c.cnt, sum200, dyn, c.svc_tab, kp.sum_row, S};
+  TreeSink sink{c.cnt, sum200, dyn, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
+                reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
 #ifdef ISIM_TREE_DEBUG
   sink.n_pos = P;
   sink.n_rows = kp.n_rows;
@@ -327,13 +362,18 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
-  for (uint32_t i = threadIdx.x; i < 2u * S; i += blockDim.x)
-    if (c.cnt[i]) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)c.cnt[i]);
+  // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
+  auto calls_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] & 0xFFFFu) : c.cnt[s]; };
+  auto errs_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] >> 16) : c.cnt[S + s]; };
+  for (uint32_t i = threadIdx.x; i < 2u * S; i += blockDim.x) {
+    const uint32_t v = i < S ? calls_of(i) : errs_of(i - S);
+    if (v) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)v);
+  }
   if (c.svc_tab) {
     unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
     for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
       const uint32_t w = slot_tbkt[s], bk = w >> 24;
-      const uint32_t calls = c.cnt[s], errs = c.cnt[S + s];
+      const uint32_t calls = calls_of(s), errs = errs_of(s);
       if (calls == 0) continue;
       unsigned long long *row = tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS;
       if (bk != kTreeDynBucket) {

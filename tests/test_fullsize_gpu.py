@@ -236,3 +236,31 @@ def test_config4_bench_batch(gpu):
     # the full stats of one oracle-sized window through the same kernel (1 launch, svc_dur included)
     c.compare(begin + 3 * n // 2, 1 << 16)
     print(f"max_launch_traces={m}")
+
+
+def test_tree_guarded_counters_overflow(gpu):
+    """The lane tree walk keeps per-slot calls and 500s as two 16-bit fields of
+    one LDS word, each moved to the stats in steps of 2^15 when it reaches
+    2^15 (tree.hip TreeSink::move, with the duration buckets and leaf sums
+    derived from them).  A tiny dynamic graph at 2^25 traces per launch
+    makes every workgroup cross 2^15 many times at several sites, calls and
+    500s (errorRate 0.7), leaf and calling callees: the full stats must equal
+    the oracle's over the whole launch, and sampled record windows too."""
+    doc = {"defaults": {"requestSize": 64, "responseSize": 256},
+           "services": [
+               {"name": "front", "isEntrypoint": True, "errorRate": 0.1,
+                "script": [{"call": "mid"}, [{"call": {"service": "leaf", "probability": 90}}, {"call": "leaf"}]]},
+               {"name": "mid", "errorRate": 0.7, "script": [{"sleep": "1ms"}, {"call": {"service": "leaf",
+                                                                                    "probability": 60}}]},
+               {"name": "leaf", "errorRate": 0.7, "script": [{"sleep": "2ms"}]}]}
+    import json as _json
+    c = Case(_json.dumps(doc))
+    assert c.handler.launch_info(0)["kernel_kind"] == 7
+    n = 1 << 25
+    rec, f = _device_run(c, 3, n)
+    _, ost = c.cpu(3, n, records=False)
+    from oracle import executor as oc
+    from parity import assert_stats_equal
+    assert_stats_equal(f, oc.split_stats(ost, len(c.sg.g.services), len(c.sg.sites)))
+    _sampled_windows(c, rec, 3, n, windows=4)
+    assert int(f["site_calls"].max()) > 1 << 24
