@@ -438,14 +438,18 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
 #ifndef TREE_CONC
 #define TREE_CONC 0
 #endif
+// waves per SIMD of the two-workgroups-per-CU kernels (timing experiments: 8)
+#ifndef TREE_WPE2
+#define TREE_WPE2 6
+#endif
 template <bool NLDS, bool DRAW>
 static void *tree_pick(uint32_t frames, bool spill, bool occ2) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
   if (occ2 && !spill && frames <= 8) {
-    if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, 6>;
-    if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW, 6>;
-    return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, 6>;
+    if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, TREE_WPE2>;
+    if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW, TREE_WPE2>;
+    return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, TREE_WPE2>;
   }
   if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW, 4>;
   if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, 4>;

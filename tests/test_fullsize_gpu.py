@@ -264,3 +264,26 @@ def test_tree_guarded_counters_overflow(gpu):
     assert_stats_equal(f, oc.split_stats(ost, len(c.sg.g.services), len(c.sg.sites)))
     _sampled_windows(c, rec, 3, n, windows=4)
     assert int(f["site_calls"].max()) > 1 << 24
+
+
+@pytest.mark.parametrize("prob", [50])
+def test_config3p_bench_batch(gpu, prob):
+    """c3p exactly as bench.py times it: config 3's 10k
+    graph with probability `prob` on every call — a dynamic walk over a
+    10,000-position tree (frames beyond the register stack spill, most
+    duration rows by global atomics) on the lane tree walk, not kinds 2/3 —
+    BENCH_BATCH["c3p"] traces per launch, two launches into one stats
+    buffer; oracle windows at every launch edge and split, sampled windows,
+    and the full stats (per service, per site, svc_dur) of a window."""
+    j, _ = bench.build_graph("c3p", prob)
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    assert c.handler.launch_info(0)["kernel_kind"] == 7
+    n, L = bench.BENCH_BATCH["c3p"], 2
+    begin = (1 << 32) - n // 2
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    hops = rec["hops"].astype(np.float64)
+    assert 1 < hops.mean() < 10000 and hops.min() >= 1
+    _launch_edge_windows(c, rec, begin, n, L, width=128)
+    _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=9)
+    c.compare(begin + n - 2048, 4096)
