@@ -374,15 +374,19 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
       const uint32_t w = slot_tbkt[s], bk = w >> 24;
       const uint32_t calls = calls_of(s), errs = errs_of(s);
-      if (calls == 0) continue;
+      if (calls == 0 && errs == 0) continue;
+      // code-200 events = calls - 500s, in u64 wrap-around arithmetic: with the
+      // guarded 16-bit fields the two remainders are independent (the moved
+      // 2^15 steps already counted their share), so it may be "negative"
+      const unsigned long long ok = (unsigned long long)calls - (unsigned long long)errs;
       unsigned long long *row = tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS;
       if (bk != kTreeDynBucket) {
-        if (calls != errs) atomicAdd(row + bk, (unsigned long long)(calls - errs));
+        if (ok) atomicAdd(row + bk, ok);
         if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
       }
       if (w & kTreeLeafSlot) {  // a leaf callee lasts its latency every time
         const unsigned long long tc = kp.slot_tc[s];
-        if (calls != errs && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * (calls - errs));
+        if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
         if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
       }
     }
