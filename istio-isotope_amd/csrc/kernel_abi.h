@@ -140,6 +140,7 @@ constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations bel
 constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
 // LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
 // workgroups per CU, and the whole CU.
+constexpr uint32_t kTreeLutBytes = 512;  // the duration-bucket table by ceil(t / 1 ms), after the histograms
 constexpr uint32_t kTreeLdsHalf = 80u * 1024u;
 constexpr uint32_t kTreeLdsFull = 160u * 1024u;
 // Layout chosen by the host (program.cpp place_tree): LDS byte offsets.

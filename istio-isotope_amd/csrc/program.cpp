@@ -83,7 +83,7 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
                        const std::vector<char> &row_nonleaf) {
   const uint32_t P = (uint32_t)out.tree_nodes.size(), S = (uint32_t)out.n_slots;
   const uint32_t R = (uint32_t)out.row_svc.size();
-  const uint32_t head = kLdsAccBytes + kHistWords * 4u;
+  const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;  // + the duration-bucket LUT
   // per-slot counters: guarded 16-bit pairs (4 B per slot; ISIM_TREE_CNT32 set: two u32, A/B measurements)
   const uint32_t cb = std::getenv("ISIM_TREE_CNT32") ? 8u : 4u;
   // rows by heat (the entry's row, 0, is the end-to-end histogram: no LDS row)
@@ -99,8 +99,13 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   int pick = -1;
   // ISIM_TREE_NODES_GLOBAL set: only the layouts with the nodes in global memory (A/B measurements)
   const int first = std::getenv("ISIM_TREE_NODES_GLOBAL") ? 2 : 0;
+  // walks deeper than 8 calling invocations run kernels built for 4 waves per
+  // SIMD (tree.hip): one 1024-thread workgroup per CU whatever the layout, so
+  // the half-CU layouts would only leave LDS unused
+  const bool one_wg = out.tree_frames > 8;
   for (int pass = 0; pass < 2 && pick < 0; ++pass) {
     for (int i = first; i < 4 && pick < 0; ++i) {
+      if (one_wg && cands[i].limit == kTreeLdsHalf) continue;
       uint32_t fixed = ((head + cb * S + 7u) & ~7u) + (cands[i].nodes ? 8u * P + 8u : 0u);
       if (fixed > cands[i].limit) continue;
       uint32_t all = fixed;

@@ -66,6 +66,14 @@ __device__ __forceinline__ uint32_t dur_row(uint32_t w) {
   return r;
 }
 
+// The duration bucket of a u32 time (prometheus/handler.go:26-31, `le`) from
+// the workgroup's LDS copy of kBucketTable (walk_dev.h): one ds_read_u8
+// instead of an L1 gather, branch-free (entry 501 is the +Inf bucket).
+__device__ __forceinline__ uint32_t lut_bucket(const uint8_t *lut, uint32_t t) {
+  const uint32_t c = t < 500000001u ? t : 500000001u;
+  return ((const __attribute__((address_space(3))) uint8_t *)lut)[(c + 999999u) / 1000000u];
+}
+
 // Node accessors of tree_walk.h: LDS (ds_read_b64) or global memory
 // (global_load_dwordx2, L2-resident).
 struct LdsNodes {
@@ -85,6 +93,7 @@ struct GlobalNodes {
 
 struct TreeSink {
   uint32_t *cnt;                // LDS: per slot calls | 500s << 16 (cnt16), else [2][n_slots] u32
+  const uint8_t *lut;           // LDS duration-bucket table
   unsigned long long *sum200;   // LDS [n_sum]
   uint32_t *dyn;                // LDS bucket tables of the varying rows
   uint64_t *svc_tab;            // HBM duration table, or null (ISIM_FLAG_NO_SVC_DUR)
@@ -158,13 +167,13 @@ struct TreeSink {
     const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
     if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // a cold row: sums (and varying buckets) by global atomics
       unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(idx) * ISIM_SVC_DUR_WORDS);
-      if (place == kTreeGlobalDyn) atomicAdd(r + (st ? ISIM_N_PROM : 0u) + prom_bucket(T), 1ull);
+      if (place == kTreeGlobalDyn) atomicAdd(r + (st ? ISIM_N_PROM : 0u) + lut_bucket(lut, T), 1ull);
       atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
       return;
     }
     if (place != kTreeStaticRow) {  // the row's LDS bucket table: header b_lo | width << 8
       const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
-      uint32_t b = prom_bucket(T) - lo;
+      uint32_t b = lut_bucket(lut, T) - lo;
       b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
       lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
     }
@@ -197,9 +206,15 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   c.n_slots = S;
   unsigned long long *sum200 = reinterpret_cast<unsigned long long *>(lds + lay.off_sums);
   uint32_t *dyn = reinterpret_cast<uint32_t *>(lds + lay.off_dyn);
+  const uint8_t *lut = lds + kLdsAccBytes + kHistWords * 4u;
   // zero the accumulators (everything before the nodes), copy the nodes in
   uint32_t *z = reinterpret_cast<uint32_t *>(lds);
-  for (uint32_t i = threadIdx.x; i < lay.off_nodes / 4u; i += blockDim.x) z[i] = 0;
+  // (one write per word: the duration-bucket table's 128 words copied, the rest zeroed)
+  {
+    constexpr uint32_t l0 = (kLdsAccBytes + kHistWords * 4u) / 4u, l1 = l0 + kTreeLutBytes / 4u;
+    const uint32_t *tab = reinterpret_cast<const uint32_t *>(kBucketTable.b);
+    for (uint32_t i = threadIdx.x; i < lay.off_nodes / 4u; i += blockDim.x) z[i] = i >= l0 && i < l1 ? tab[i - l0] : 0u;
+  }
   if constexpr (NLDS) {
     const uint2 *src = reinterpret_cast<const uint2 *>(gnodes);
     uint2 *dst = reinterpret_cast<uint2 *>(lds + lay.off_nodes);
@@ -211,7 +226,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     dyn[d.off] = d.b_lo | (d.width << 8);
   }
   __syncthreads();
-  TreeSink sink{c.cnt, sum200, dyn, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
+  TreeSink sink{c.cnt, lut, sum200, dyn, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
                 reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
 #ifdef ISIM_TREE_DEBUG
   sink.n_pos = P;
@@ -293,7 +308,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       // the latency histograms: one LDS atomic per responding lane (their
       // buckets mostly differ, so a wave-aggregated add would loop per bucket)
       if (mine) {
-        lds_add(c.hist + (is500 ? ISIM_N_PROM : 0u) + prom_bucket(lat), 1u);
+        lds_add(c.hist + (is500 ? ISIM_N_PROM : 0u) + lut_bucket(lut, lat), 1u);
         const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
         lds_add(c.hist + 2 * ISIM_N_PROM + (is500 ? ISIM_N_LOG2 : 0u) + l2, 1u);
       }

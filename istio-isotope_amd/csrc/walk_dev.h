@@ -98,7 +98,7 @@ __device__ __forceinline__ void count(uint64_t *__restrict__ gstats, uint32_t *c
 // A 512-byte table of buckets by m = ceil(t / 1 ms) (0..500), built at
 // compile time; per-lane lookups hit L1 (the LDS of the lane tree walk is
 // full): 7 VALU per duration instead of a 32-compare chain.
-struct BucketTable {
+struct alignas(16) BucketTable {
   uint8_t b[512];
   constexpr BucketTable() : b() {
     const uint32_t e[32] = {7, 8, 9, 10, 11, 12, 14, 16, 18, 20, 25, 30, 35, 40, 45, 50,
