@@ -5,7 +5,7 @@
 // traces, and which Philox sites (a call block past the fourth call, an error
 // block, the skip residues of an open) the wave runs per iteration.  Build
 // (g++, from the repo root; -DTW_... selects tree_walk.h variants):
-//   C=istio-isotope_amd/csrc; g++ -O2 -std=c++17 -I$C tools/tree_wave_sim.cpp \
+//   C=istio-isotope_amd/csrc; g++ -O2 -std=c++17 -Iinclude -I$C tools/tree_wave_sim.cpp \
 //     $C/json.cpp $C/gounits.cpp $C/graph.cpp $C/program.cpp $C/marshal.cpp -o /tmp/tree_wave_sim
 //   /tmp/tree_wave_sim graph.json [waves]
 // ("Round 3 — macro steps": config 4 at 10.4 iterations per 64
@@ -29,6 +29,7 @@ namespace {
 struct NullSink {
   void call(uint32_t) {}
   void resp(uint32_t, uint32_t, uint32_t, bool) {}
+  void resp_leaf(uint32_t, bool) {}
 };
 }  // namespace
 
@@ -55,8 +56,9 @@ int main(int argc, char **argv) {
   p.flags = ISIM_FLAG_DYNAMIC;
   Program prog;
   if (compile_program(g, entry, p, prog, err) != ISIM_OK || prog.tree_nodes.empty()) return 3;
-  const TreeNode *nodes = prog.tree_nodes.data();
+  const tw::CpuNodes nodes{prog.tree_nodes.data()};
   const TreeExt *ext = prog.tree_ext.data();
+  const TreeStep *stp = prog.tree_step.data();
   NullSink sk;
   const int waves = argc > 2 ? atoi(argv[2]) : 100, per_wave = 1024;
   uint64_t next = 0, it = 0, execs = 0, lanes = 0, hops = 0, siteA = 0, siteB = 0, merged = 0;
@@ -68,7 +70,7 @@ int main(int argc, char **argv) {
       for (int l = 0; l < 64; ++l)
         if (act[l] && L[l].done) {
           act[l] = false;
-          hops += L[l].hopn;
+          hops += L[l].hops();
         }
       for (int l = 0; l < 64; ++l)
         if (!act[l] && issued < per_wave) {
@@ -82,12 +84,12 @@ int main(int argc, char **argv) {
       uint32_t opening = 0, nA = 0, nB = 0, maxBC = 0;
       for (int l = 0; l < 64; ++l) {
         if (!act[l] || L[l].done) continue;
-        const uint32_t d0 = L[l].d, eb = L[l].ek_blk, fp = L[l].f_pos, kb = L[l].f_fl >> tw::KB_SHIFT & tw::KB_NONE;
+        const uint32_t d0 = L[l].d, eb = L[l].ek_blk, fp = L[l].f_pos, kb = L[l].f_kb();
         const bool entry_step = L[l].p == 0;
-        L[l].step(nodes, ext, sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        L[l].step(nodes, ext, stp, sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
         const bool C = L[l].d > d0 || (entry_step && !L[l].done);  // drew its skip residues at an open
         const bool B = L[l].ek_blk != eb;                          // drew an error block
-        const bool A = !C && L[l].d == d0 && L[l].f_pos == fp && (L[l].f_fl >> tw::KB_SHIFT & tw::KB_NONE) != kb;
+        const bool A = !C && L[l].d == d0 && L[l].f_pos == fp && L[l].f_kb() != kb;
         opening += C;
         nA += A;
         nB += B;
