@@ -367,7 +367,7 @@ ISIM_API int isim_multi_get_id(isim_multi_id *id);
 ISIM_API int isim_multi_precheck(int device);
 /* This process is rank `rank` of n_ranks, on HIP device `device` (ncclCommInitRank; collective over the ranks).
  * Created non-blocking (ncclCommInitRankConfig, blocking = 0) when RCCL has it, and polled: if the
- * peers do not all arrive within ISIM_MULTI_TIMEOUT_S seconds (environment, default 600) the
+ * peers do not all arrive within ISIM_MULTI_TIMEOUT_S seconds (environment, default 120) the
  * communicator is aborted and ISIM_ECOMM returned.  Collectives and isim_serve_multi's wait are polled
  * the same way (hipStreamQuery + ncclCommGetAsyncError), so a rank whose peer aborted or never came
  * returns ISIM_ECOMM instead of waiting forever. */

@@ -123,11 +123,11 @@ __global__ void scatter_words(uint64_t *tab, const uint64_t *in, uint32_t rows, 
 // How long a rank waits for its peers (communicator creation, a collective)
 // before it aborts the communicator and returns ISIM_ECOMM: a peer that failed
 // locally before entering a collective never arrives, and over xGMI nothing
-// else tells the waiting rank.  ISIM_MULTI_TIMEOUT_S (seconds), default 600.
+// else tells the waiting rank.  ISIM_MULTI_TIMEOUT_S (seconds), default 120.
 double multi_timeout_s() {
   const char *e = std::getenv("ISIM_MULTI_TIMEOUT_S");
   const double v = e ? std::atof(e) : 0.0;
-  return v > 0 ? v : 600.0;
+  return v > 0 ? v : 120.0;
 }
 
 }  // namespace
