@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 8
+#define ISIM_ABI_VERSION 9
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -299,8 +299,10 @@ ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *st
  * call counters are those of the static walk; latencies and the per-service
  * durations include queueing.  Exact (bit-identical to the sequential
  * event-driven oracle) for the DES graph class of DESIGN.md §10.1: static
- * walks of at most 2^24 invocations and 65536 replicas per service
- * (isim_des_info_get returns ISIM_EINVAL with the reason otherwise).  Times
+ * walks of at most 2^24 invocations and 65536 replicas per service, and
+ * dynamic walks (probabilistic calls) in mode A whose lane-tree-walk tree was
+ * built (isim_des_info.items; isim_des_info_get returns ISIM_EINVAL with the
+ * reason otherwise).  Times
  * are kept per trace relative to its arrival: in 32-bit rows by default;
  * a batch with a latency of 2^31 ns (2.1 s) or more is then not accumulated
  * (ISIM_ST_DES_RETRY counts it) and must be rerun with ISIM_DES_FLAG_WIDE
@@ -324,6 +326,9 @@ typedef struct {
   int32_t cyclic;                /* 1: the call-step schedule is cyclic (fixed-point passes) */
   int32_t row_reads;             /* rows one trace's batch reads (queue + finish passes, one pass), 4 or 8 B each */
   int32_t row_writes;            /* rows it writes (the algorithmic bytes of bench.py's roofline) */
+  int32_t items;                 /* 1: a dynamic walk (probabilistic calls, mode A) on the item engine (DESIGN.md
+                                    §10.8): positions are the tree's POTENTIAL invocations, a batch simulates the
+                                    executed ones and synchronizes hip_stream twice (item count, bucket sizes) */
 } isim_des_info;
 
 ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);

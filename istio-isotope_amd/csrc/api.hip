@@ -75,6 +75,9 @@ struct DevState {
   uint32_t *d_des_fast = nullptr, *d_des_sort = nullptr, *d_des_arr = nullptr, *d_des_zero = nullptr;
   uint32_t *d_des_pipe = nullptr;
   void *d_des_ext = nullptr, *d_des_steps = nullptr;
+  // DES item engine (dynamic walks): per-position plan facts, BK rounds, the tree
+  void *d_des_ipos = nullptr, *d_des_nodes = nullptr, *d_des_text = nullptr, *d_des_tstep = nullptr;
+  uint32_t *d_des_sround = nullptr;
   isim::TreeExt *d_tree_ext = nullptr;  // kind 7: per position (the nodes are d_prog)
   isim::TreeStep *d_tree_step = nullptr;   // kind 7: per position, the rare step facts
   isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
@@ -90,7 +93,8 @@ void free_dev(DevState &d) {
                   d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
                   (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
                   (void *)d.d_des_pipe,
-                  d.d_des_ext, d.d_des_steps, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
+                  d.d_des_ext, d.d_des_steps, d.d_des_ipos, d.d_des_nodes, d.d_des_text, d.d_des_tstep,
+                  (void *)d.d_des_sround, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
                   (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill})
     if (q) (void)hipFree(q);
   d = DevState();
@@ -788,7 +792,7 @@ int des_ensure(const isim_handler *hc) {
   isim_handler *h = const_cast<isim_handler *>(hc);
   std::lock_guard<std::mutex> lk(h->des_mu);
   if (!h->des_built) {
-    h->des_rc = isim::build_des_plan(h->graph, h->prog, h->des, h->des_err);
+    h->des_rc = isim::build_des_plan(h->graph, h->prog, h->params.error_mode == ISIM_MODE_B, h->des, h->des_err);
     h->des_built = true;
   }
   return h->des_rc == ISIM_OK ? ISIM_OK : fail(h->des_rc, h->des_err);
@@ -820,6 +824,15 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
   std::vector<uint32_t> pipe(d.pipe_pos);
   pipe.insert(pipe.end(), d.pipe_dep.begin(), d.pipe_dep.end());
   if (!up((void **)&st->d_des_pipe, pipe.data(), pipe.size() * 4)) return fail(ISIM_EHIP, "DES plan upload failed");
+  if (d.items) {
+    const isim::Program &p = h->prog;
+    if (!up(&st->d_des_ipos, d.item_pos.data(), d.item_pos.size() * sizeof(isim::DesItemPos)) ||
+        !up((void **)&st->d_des_sround, d.step_round.data(), d.step_round.size() * 4) ||
+        !up(&st->d_des_nodes, p.tree_nodes.data(), p.tree_nodes.size() * sizeof(isim::TreeNode)) ||
+        !up(&st->d_des_text, p.tree_ext.data(), p.tree_ext.size() * sizeof(isim::TreeExt)) ||
+        !up(&st->d_des_tstep, p.tree_step.data(), p.tree_step.size() * sizeof(isim::TreeStep)))
+      return fail(ISIM_EHIP, "DES plan upload failed");
+  }
   return ISIM_OK;
 }
 
@@ -841,13 +854,15 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   isim::des_row_traffic(h->des, rr, rw);
   out->row_reads = (int32_t)rr;
   out->row_writes = (int32_t)rw;
+  out->items = h->des.items ? 1 : 0;
   return ISIM_OK;
 }
 
 int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
   if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
   if (const int drc = des_ensure(h)) return drc;
-  *bytes = isim::des_workspace_bytes(h->des, n_traces, stats_words(h), h->prog.row_svc.size());
+  *bytes = h->des.items ? isim::des_items_workspace_bytes(n_traces)
+                        : isim::des_workspace_bytes(h->des, n_traces, stats_words(h), h->prog.row_svc.size());
   return ISIM_OK;
 }
 
@@ -867,6 +882,36 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
   int rc = des_prepare(h, device, st);
   if (rc != ISIM_OK) return rc;
   const isim::DesPlan &d = h->des;
+  if (d.items) {
+    // a dynamic walk: the item engine (des_items.hip); 64-bit times throughout
+    if (!d_workspace || workspace_bytes < isim::des_items_workspace_bytes(n_traces))
+      return fail(ISIM_EINVAL, "DES workspace smaller than isim_des_workspace_bytes()");
+    isim::DesItemsLaunch L{};
+    L.plan = &d;
+    L.d_pos = st->d_des_pos;
+    L.d_item_pos = st->d_des_ipos;
+    L.d_steps = st->d_des_steps;
+    L.d_step_round = st->d_des_sround;
+    L.d_nodes = st->d_des_nodes;
+    L.d_ext = st->d_des_text;
+    L.d_tstep = st->d_des_tstep;
+    L.tree_frames = h->prog.tree_frames;
+    L.tree_flags = h->prog.tree_flags;
+    L.workspace = d_workspace;
+    L.d_stats = d_stats;
+    L.d_table = d_des_table;
+    L.d_records = d_records;
+    L.n_traces = n_traces;
+    L.trace_begin = trace_begin;
+    L.mean_ns = dp->mean_interarrival_ns;
+    L.seed = h->params.seed;
+    L.n_slots = (uint32_t)h->prog.n_slots;
+    std::string e;
+    const int irc = isim::des_items_launch(L, hip_stream, e);
+    if (irc == 2) return fail(ISIM_EINVAL, e);
+    if (irc) return fail(ISIM_EHIP, e);
+    return ISIM_OK;
+  }
   if (n_traces * (uint64_t)std::max<uint32_t>(1, d.max_sort_pos) > 0xFFFFFFFFull)
     return fail(ISIM_EINVAL, "n_traces x positions of one service above 2^32 per DES batch");
   // the queue scans' keys a_t - t * hold are signed 64-bit (des.hip down passes)
@@ -925,7 +970,8 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
   HIPCHK(hipSetDevice(device));
   const uint64_t words = stats_words(h);
   const uint64_t tab_words = (uint64_t)h->prog.row_svc.size() * ISIM_DES_ROW_WORDS;
-  const uint64_t ws_bytes = isim::des_workspace_bytes(h->des, n_traces, words, h->prog.row_svc.size());
+  const uint64_t ws_bytes = h->des.items ? isim::des_items_workspace_bytes(n_traces)
+                                         : isim::des_workspace_bytes(h->des, n_traces, words, h->prog.row_svc.size());
   uint64_t *d_stats = nullptr, *d_tab = nullptr;
   void *d_ws = nullptr;
   isim_trace_rec *d_rec = nullptr;
@@ -959,7 +1005,7 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
         break;
       }
       if (!retry) break;
-      if (p.flags & ISIM_DES_FLAG_WIDE) {
+      if ((p.flags & ISIM_DES_FLAG_WIDE) || h->des.items) {
         rc = fail(ISIM_EINVAL, "DES batch not accumulated with 64-bit rows: the cyclic schedule found no fixed point "
                                "within 256 passes (or arrivals beyond the sort keys)");
         break;

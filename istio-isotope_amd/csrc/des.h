@@ -91,8 +91,29 @@ struct DesStep {
 };
 static_assert(sizeof(DesStep) == 32, "DesStep must be 32 bytes");
 constexpr uint32_t kDesNone = 0xFFFFFFFFu;
+// step_round flag: a step begin whose callee-finish edges the cyclic schedule
+// cut (des_plan.cpp): it reads the previous pass's callee maxima (des_items.hip)
+constexpr uint32_t kDesStepCut = 0x80000000u;
+
+// Per position, for the item engine of dynamic walks (des_items.hip; 16 bytes, device layout).
+struct DesItemPos {
+  uint32_t qround;     // round of its queue (the service's, or its own for a zero-hold service)
+  uint32_t fgroup;     // finish group (DesPlan::fin_off index)
+  uint16_t kstep;      // its call step in the caller's script
+  uint16_t nsteps;     // call steps of its own script
+  uint32_t bk_first;   // nsteps >= 2: the DesStep id of its first call step (kDesNone otherwise)
+};
+static_assert(sizeof(DesItemPos) == 16, "DesItemPos must be 16 bytes");
 
 struct DesPlan {
+  // item engine (des_items.hip): a dynamic walk (probabilistic calls, mode A)
+  // over the tree of potential invocations; only executed invocations
+  // (ITEMS) are simulated
+  bool items = false;
+  std::vector<DesItemPos> item_pos;  // [n_pos]
+  std::vector<uint32_t> step_round;  // [steps]: the round of each BK op | kDesStepCut
+  uint32_t item_acc = 1;             // per item: callee finish maxima, one per call step (>= 1)
+  uint32_t item_bk = 0;              // per item: BK slots (the most call steps of a multi-step script; 0: none)
   std::vector<DesPos> pos;           // hop order (position 0 = the entry)
   std::vector<DesPosExt> ext;        // [n_pos]
   std::vector<uint32_t> child;       // children lists (positions, call-step order)
@@ -179,7 +200,26 @@ void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes);
 
 // Returns ISIM_OK or ISIM_EINVAL with the reason in `err` when the graph is
 // outside the DES class.
-int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err);
+int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan &out, std::string &err);
+
+// The item engine (des_items.hip): one batch of a dynamic walk's DES.  Device
+// per-trace workspace bytes; the per-item arrays are allocated on `stream`
+// (hipMallocAsync) once the batch's executed invocations are counted, which
+// synchronizes the stream once per batch.
+struct DesItemsLaunch {
+  const DesPlan *plan;
+  const void *d_pos, *d_item_pos, *d_steps;  // DesPos[n_pos], DesItemPos[n_pos], DesStep[]
+  const uint32_t *d_step_round;              // [steps]
+  const void *d_nodes, *d_ext, *d_tstep;     // the lane tree walk's TreeNode/TreeExt/TreeStep
+  uint32_t tree_frames, tree_flags;
+  void *workspace;
+  uint64_t *d_stats, *d_table;
+  isim_trace_rec *d_records;
+  uint64_t n_traces, trace_begin, mean_ns, seed;
+  uint32_t n_slots;
+};
+uint64_t des_items_workspace_bytes(uint64_t n);
+int des_items_launch(const DesItemsLaunch &L, void *stream, std::string &err);
 
 // -ln(w / 2^24), w = (u >> 8) + 1, in Q24 fixed point:
 // log1p(i/256) table, 16-bit linear interpolation.  Shared by host and device.

@@ -1,0 +1,751 @@
+// DES item engine: the exact per-replica worker-pool DES of
+// a DYNAMIC walk — probabilistic calls (shouldSkipRequest, isotope/service/
+// pkg/srv/executable.go:84-90), mode A — on the GPU.
+//
+// The static engine (des.hip) keeps one row per (position, trace): every
+// invocation executes in every trace.  Here a trace executes a few of the
+// tree's potential invocations (config 4's mesh: 5.7 of 3,280), so the unit
+// is the ITEM — one executed invocation — and the work is proportional to
+// the items, not the positions:
+//   1. arrivals    A_t = prefix sum of the exponential gaps (des.h Q24 log)
+//   2. pre-walk    the lane tree walk (tree_walk.h Lane, one trace per
+//                  thread) counts each trace's executed invocations, a scan
+//                  gives the item offsets, a second walk writes each item's
+//                  position, caller item and own error (hop id = item index
+//                  within the trace: executed invocations in preorder)
+//   3. buckets     the items sorted (stable radix sort) by their position's
+//                  queue round and by its finish group (des_plan.cpp's
+//                  schedule over the tree's positions)
+//   4. rounds      step begins (BK per item and call step), queues (the
+//                  round's items sorted by (service, replica, arrival) — two
+//                  stable radix sorts, ties in (trace, hop) order as the
+//                  oracle's event heap pops them — and one segmented
+//                  max-plus scan: S = max(a, S_prev + hold)), finishes
+//                  (deepest group first: F from the start or last BK and the
+//                  callees' maxima, which each callee folds into its caller's
+//                  per-step slot with a 64-bit atomic max)
+//   5. finalize    records and latency statistics per trace.
+// Reference anchors: as des.hip (handler.go:37-79, executable.go:94-179,
+// svc/service.go:30-31, prometheus/handler.go:87-106).  Parity: bit-exact
+// against oracle/des_oracle.c (its pre-walk, semantics v1 §2.3).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_scan_by_key.hpp>
+
+#include "des.h"
+#include "kernel_abi.h"
+#include "tree_walk.h"
+
+namespace isim {
+namespace dit {
+
+constexpr uint32_t kT = 256;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__constant__ int32_t c_ln[257] = {
+#include "des_ln_table.inc"
+};
+// service_request_duration_seconds edges (prometheus/handler.go:26-31), ns
+__constant__ uint64_t c_edges[32] = {
+    7000000ull,   8000000ull,   9000000ull,   10000000ull,  11000000ull,  12000000ull,  14000000ull,
+    16000000ull,  18000000ull,  20000000ull,  25000000ull,  30000000ull,  35000000ull,  40000000ull,
+    45000000ull,  50000000ull,  60000000ull,  70000000ull,  80000000ull,  90000000ull,  100000000ull,
+    120000000ull, 140000000ull, 160000000ull, 180000000ull, 200000000ull, 250000000ull, 300000000ull,
+    350000000ull, 400000000ull, 450000000ull, 500000000ull};
+
+__device__ __forceinline__ uint32_t prom_bucket(uint64_t t) {
+  uint32_t lo = 0, hi = 32;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (t <= c_edges[mid]) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// word 0 of Philox4x32-10 (t, w2, w3) under the handler's seed
+__device__ __forceinline__ uint32_t draw0(uint64_t t, uint32_t w2, uint32_t w3, uint32_t k0, uint32_t k1) {
+  uint32_t a = (uint32_t)t, b = (uint32_t)(t >> 32), c = w2, d = w3;
+  tw::philox10(a, b, c, d, k0, k1);
+  return a;
+}
+
+// -ln(w / 2^24) in Q24, w = (u >> 8) + 1 (des.h des_exp_q24_host)
+__device__ __forceinline__ uint64_t exp_q24(uint32_t u) {
+  const uint32_t w = (u >> 8) + 1u;
+  const int e = 31 - __builtin_clz(w);
+  const uint32_t f = (w << (24 - e)) & 0xFFFFFFu;
+  const uint32_t idx = f >> 16, rem = f & 0xFFFFu;
+  const int64_t lnm = c_ln[idx] + ((((int64_t)c_ln[idx + 1] - c_ln[idx]) * (int64_t)rem) >> 16);
+  return (uint64_t)(24 * kLn2Q24 - ((int64_t)e * kLn2Q24 + lnm));
+}
+
+struct K {
+  // plan
+  const DesPos *pos;
+  const DesItemPos *ip;
+  const DesStep *steps;
+  const uint32_t *step_round;
+  // tree (pre-walk)
+  const unsigned long long *nodes;
+  const TreeExt *ext;
+  const TreeStep *tstep;
+  uint32_t *spill;
+  // per trace
+  uint64_t *gap, *A, *cnt, *tend;  // cnt: hops; tend: inclusive item offsets
+  uint32_t *terr;                  // status_err
+  // per item
+  uint32_t *ipos, *ipar, *itr;
+  uint8_t *iown;
+  uint64_t *IA, *IS, *IF, *acc, *bk;
+  const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
+  uint32_t aw, bw;                 // acc / bk slots per item
+  uint64_t M;
+  // outputs
+  unsigned long long *stats, *table;
+  isim_trace_rec *records;
+  uint64_t n, trace_begin, mean_ns;
+  uint32_t k0, k1, n_slots;
+  uint32_t arr_bits;               // arrival bits of a queue key (64 - replica bits)
+  // cyclic schedules (des_plan.cpp): passes to a fixed point; a quiet pass
+  // records no statistics and flags any stored value it changes
+  uint32_t quiet;
+  uint32_t *changed;
+};
+
+__device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v) {
+  if (k.changed && *p != v) atomicOr(k.changed, 1u);
+  *p = v;
+}
+
+__device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * kT + threadIdx.x; }
+__device__ __forceinline__ uint64_t nthreads() { return (uint64_t)gridDim.x * kT; }
+__device__ __forceinline__ uint64_t item_off(const K &k, uint64_t t) { return t ? k.tend[t - 1] : 0; }
+
+// ---- 1. the exponential inter-arrival gaps (summed by a rocPRIM scan)
+__global__ void __launch_bounds__(kT) k_gaps(K k) {
+  for (uint64_t t = gid(); t < k.n; t += nthreads())
+    k.gap[t] = (k.mean_ns * exp_q24(draw0(k.trace_begin + t, 0u, 0x80000001u, k.k0, k.k1))) >> 24;
+}
+
+// ---- 2. the pre-walk
+struct GNodes {
+  const unsigned long long *__restrict__ p;
+  __device__ __forceinline__ tw::NodeW load(uint32_t i) const {
+    const unsigned long long v = p[i];
+    return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
+};
+struct CountSink {
+  __device__ __forceinline__ void call(uint32_t) {}
+  __device__ __forceinline__ void resp_leaf(uint32_t, bool) {}
+  __device__ __forceinline__ void resp(uint32_t, uint32_t, uint32_t, bool) {}
+};
+struct EmitSink : CountSink {
+  uint32_t *ipos, *ipar, *itr;
+  uint8_t *iown;
+  uint64_t base;
+  uint32_t t;
+  __device__ __forceinline__ void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
+    const uint64_t i = base + hop;
+    ipos[i] = p;
+    ipar[i] = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
+    itr[i] = t;
+    iown[i] = own ? 1 : 0;
+  }
+};
+
+template <int FR, bool SPILL, bool EMIT>
+__global__ void __launch_bounds__(kT) k_prewalk(K k) {
+  tw::Lane<FR, false, true, SPILL, true> L;
+  if constexpr (SPILL) {
+    L.sp = k.spill + gid();
+    L.sp_stride = (uint32_t)nthreads();
+  }
+  const GNodes nodes{k.nodes};
+  for (uint64_t t = gid(); t < k.n; t += nthreads()) {
+    L.start(k.trace_begin + t);
+    if constexpr (EMIT) {
+      EmitSink s;
+      s.ipos = k.ipos;
+      s.ipar = k.ipar;
+      s.itr = k.itr;
+      s.iown = k.iown;
+      s.base = item_off(k, t);
+      s.t = (uint32_t)t;
+      while (!L.done) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
+      k.terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
+    } else {
+      CountSink s;
+      while (!L.done) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
+      k.cnt[t] = L.hops();
+    }
+  }
+}
+
+// ---- 3. bucket keys: the position's queue round and finish group
+__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    const DesItemPos p = k.ip[k.ipos[i]];
+    qk[i] = p.qround;
+    fk[i] = p.fgroup;
+    ids[i] = (uint32_t)i;
+  }
+}
+
+// off[b] = first index of key b in the sorted keys (b = 0..nb)
+__global__ void __launch_bounds__(kT) k_bounds(const uint32_t *keys, uint64_t m, uint32_t nb, uint32_t *off) {
+  for (uint64_t i = gid(); i <= m; i += nthreads()) {
+    const uint32_t lo = i == 0 ? 0u : keys[i - 1] + 1u;  // keys (keys[i-1], keys[i]] start here
+    const uint32_t hi = i == m ? nb : keys[i];
+    for (uint32_t b = lo; b <= hi && b <= nb; ++b) off[b] = (uint32_t)i;
+  }
+}
+
+// ---- 4a. step begins of round r (calls after calls, des.h DesStep)
+__global__ void __launch_bounds__(kT) k_steps(K k, uint32_t r) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    const DesItemPos p = k.ip[k.ipos[i]];
+    if (p.nsteps < 2) continue;
+    for (uint32_t s = 0; s < p.nsteps; ++s) {
+      const uint32_t b = p.bk_first + s;
+      const uint32_t sr = k.step_round[b];
+      if ((sr & ~kDesStepCut) != r) continue;
+      const DesStep st = k.steps[b];
+      uint64_t v;
+      if (s == 0) {
+        v = k.IS[i];
+      } else {
+        v = k.bk[i * k.bw + (s - 1)] + st.smax;
+        // a cut step's callees finish later in the pass: their maxima of the previous one
+        const uint64_t c = ((sr & kDesStepCut) ? k.acc_prev : k.acc)[i * k.aw + (s - 1)];
+        v = c > v ? c : v;
+      }
+      store_tracked(k, k.bk + i * k.bw + s, v + st.add);
+    }
+  }
+}
+
+// ---- 4b. queues of round r: arrival and key per item (replica | arrival)
+__global__ void __launch_bounds__(kT) k_qkeys(K k, const uint32_t *ids, uint64_t m, uint64_t *key, uint32_t *val,
+                                              uint32_t *ovf) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t i = ids[j];
+    const uint32_t v = k.ipos[i];
+    const DesPos P = k.pos[v];
+    const uint32_t par = k.ipar[i];
+    const uint32_t t = k.itr[i];
+    uint64_t a;
+    if (par == kNone) {
+      a = k.A[t];
+    } else {
+      const uint32_t ks = k.ip[v].kstep;
+      a = (ks == 0 ? k.IS[par] : k.bk[(uint64_t)par * k.bw + ks]) + P.off;
+    }
+    k.IA[i] = a;
+    uint64_t rep = 0;
+    if (P.reps > 1) {
+      const uint32_t hop = (uint32_t)(i - item_off(k, t));
+      rep = draw0(k.trace_begin + t, hop, 0x80000002u, k.k0, k.k1) % P.reps;
+    }
+    if (k.arr_bits < 64 && (a >> k.arr_bits)) atomicOr(ovf, 1u);
+    key[j] = k.arr_bits < 64 ? (rep << k.arr_bits) | a : a;
+    val[j] = i;
+  }
+}
+
+// the service's duration-table row of each item, in the arrival order
+__global__ void __launch_bounds__(kT) k_rkeys(K k, const uint32_t *items, uint64_t m, uint32_t *rk, uint32_t *rv) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    rk[j] = k.pos[k.ipos[items[j]]].row;
+    rv[j] = (uint32_t)j;
+  }
+}
+
+// FIFO of one worker as a max-plus map x -> max(x + B, C) on "free at x"
+// (des.hip SegMP without the segment flag: rocPRIM's scan by key segments)
+struct MP {
+  uint64_t B, C;
+};
+struct MPThen {
+  __device__ __forceinline__ MP operator()(const MP &a, const MP &b) const {
+    const uint64_t c = a.C + b.B;
+    return MP{a.B + b.B, c > b.C ? c : b.C};
+  }
+};
+
+// the segment key (row | replica) and map (hold, a + hold) of each item in
+// (row, replica, arrival, trace, hop) order; sid: the item
+__global__ void __launch_bounds__(kT) k_pairs(K k, uint64_t m, const uint32_t *rkb, const uint32_t *rvb,
+                                              const uint64_t *key, const uint32_t *items, uint32_t *segk, MP *mp,
+                                              uint32_t *sid) {
+  const uint64_t amask = k.arr_bits < 64 ? (1ull << k.arr_bits) - 1 : ~0ull;
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t j1 = rvb[j];
+    const uint32_t i = items[j1];
+    const uint64_t kk = key[j1];
+    const uint32_t rep = k.arr_bits < 64 ? (uint32_t)(kk >> k.arr_bits) : 0u;
+    const uint64_t hold = k.pos[k.ipos[i]].hold;
+    segk[j] = (rkb[j] << 16) | rep;
+    mp[j] = MP{hold, (kk & amask) + hold};
+    sid[j] = i;
+  }
+}
+
+// start times; the queue figures per table row (runs of one row within a
+// thread's span are summed before the atomics)
+constexpr uint32_t kQSpan = 8;
+__global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
+                                             const MP *inc) {
+  for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+    uint32_t row = kNone;
+    unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
+    auto flush = [&]() {
+      if (row == kNone || !n) return;
+      unsigned long long *tr = k.table + (uint64_t)row * ISIM_DES_ROW_WORDS;
+      atomicAdd(tr + ISIM_DES_COUNT, n);
+      if (sw) atomicAdd(tr + ISIM_DES_SUM_WAIT, sw);
+      if (mw) atomicMax(tr + ISIM_DES_MAX_WAIT, mw);
+      if (sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, sh);
+    };
+    for (uint64_t j = j0; j < j0 + kQSpan && j < m; ++j) {
+      const uint32_t i = sid[j];
+      const uint64_t hold = k.pos[k.ipos[i]].hold;
+      const uint64_t S = inc[j].C - hold;
+      const uint64_t a = k.IA[i];
+      store_tracked(k, k.IS + i, S);
+      const uint32_t r = rkb[j];
+      if (r != row) {
+        if (!k.quiet) flush();
+        row = r;
+        n = sw = mw = sh = 0;
+      }
+      const uint64_t w = S - a;
+      n += 1;
+      sw += w;
+      mw = w > mw ? w : mw;
+      sh += hold;
+    }
+    if (!k.quiet) flush();
+  }
+}
+
+// ---- 4c. finishes of one group
+__global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t i = ids[j];
+    const uint32_t v = k.ipos[i];
+    const DesPos P = k.pos[v];
+    const DesItemPos p = k.ip[v];
+    uint64_t F;
+    if (P.flags & kDesFlagLeaf) {
+      F = k.IS[i] + P.floor;
+    } else {
+      const uint32_t last = p.nsteps >= 2 ? p.nsteps - 1u : 0u;
+      F = (p.nsteps >= 2 ? k.bk[(uint64_t)i * k.bw + last] : k.IS[i]) + P.floor;
+      const uint64_t c = k.acc[(uint64_t)i * k.aw + last];
+      F = (c > F ? c : F) + P.post;
+    }
+    store_tracked(k, k.IF + i, F);
+    const uint32_t par = k.ipar[i];
+    if (par != kNone) atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
+    if (k.quiet) continue;
+    const uint32_t own = k.iown[i];
+    const uint64_t dur = F - k.IA[i];
+    unsigned long long *tr = k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS;
+    atomicAdd(tr + own * ISIM_N_PROM + prom_bucket(dur), 1ull);
+    atomicAdd(tr + 2 * ISIM_N_PROM + own, (unsigned long long)dur);
+    if (par != kNone) {
+      atomicAdd(k.stats + ISIM_ST_SITES + P.slot, 1ull);
+      if (own) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P.slot, 1ull);
+    }
+  }
+}
+
+// ---- 5. records and the latency statistics
+__global__ void __launch_bounds__(kT) k_final(K k) {
+  __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
+  __shared__ unsigned long long red[6][kT / 64];
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kT) hp[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kT) hl[i] = 0;
+  __syncthreads();
+  unsigned long long sl = 0, sh = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
+  for (uint64_t t = gid(); t < k.n; t += nthreads()) {
+    const uint64_t root = item_off(k, t);
+    const uint64_t L = k.IF[root] - k.A[t];
+    const uint32_t hops = (uint32_t)(k.tend[t] - root);
+    const uint32_t s_e = k.terr[t];
+    const uint32_t st = s_e >> 31, e = s_e & 0x7FFFFFFFu;
+    if (k.records) {
+      isim_trace_rec r;
+      r.latency_ns = L;
+      r.hops = hops;
+      r.status_err = s_e;
+      k.records[t] = r;
+    }
+    sl += L;
+    sh += hops;
+    se += e;
+    n5 += st;
+    mn = L < mn ? L : mn;
+    mx = L > mx ? L : mx;
+    atomicAdd(&hp[st * ISIM_N_PROM + prom_bucket(L)], 1u);
+    atomicAdd(&hl[st * ISIM_N_LOG2 + (L ? 64u - (uint32_t)__builtin_clzll(L) : 0u)], 1u);
+  }
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    sl += __shfl_xor(sl, d, 64);
+    sh += __shfl_xor(sh, d, 64);
+    se += __shfl_xor(se, d, 64);
+    n5 += __shfl_xor(n5, d, 64);
+    const unsigned long long a = __shfl_xor(mn, d, 64), b = __shfl_xor(mx, d, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    const uint32_t w = threadIdx.x >> 6;
+    red[0][w] = sl;
+    red[1][w] = sh;
+    red[2][w] = se;
+    red[3][w] = n5;
+    red[4][w] = mn;
+    red[5][w] = mx;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kT)
+    if (hp[i]) atomicAdd(k.stats + ISIM_ST_PROM + i, (unsigned long long)hp[i]);
+  for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_LOG2; i += kT)
+    if (hl[i]) atomicAdd(k.stats + ISIM_ST_LOG2 + i, (unsigned long long)hl[i]);
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < kT / 64; ++w) {
+      for (uint32_t q = 0; q < 4; ++q) red[q][0] += red[q][w];
+      red[4][0] = red[4][w] < red[4][0] ? red[4][w] : red[4][0];
+      red[5][0] = red[5][w] > red[5][0] ? red[5][w] : red[5][0];
+    }
+    if (blockIdx.x == 0) atomicAdd(k.stats + ISIM_ST_N_TRACES, (unsigned long long)k.n);
+    atomicAdd(k.stats + ISIM_ST_SUM_LATENCY, red[0][0]);
+    atomicAdd(k.stats + ISIM_ST_SUM_HOPS, red[1][0]);
+    atomicAdd(k.stats + ISIM_ST_SUM_ERR_HOPS, red[2][0]);
+    atomicAdd(k.stats + ISIM_ST_N_500, red[3][0]);
+    if (red[4][0] != ~0ull) atomicMax(k.stats + ISIM_ST_NOT_MIN_LATENCY, ~red[4][0]);
+    atomicMax(k.stats + ISIM_ST_MAX_LATENCY, red[5][0]);
+  }
+}
+
+__global__ void k_flag_retry(unsigned long long *stats, const uint32_t *ovf) {
+  if (ovf[0] || ovf[1]) atomicAdd(stats + ISIM_ST_DES_RETRY, 1ull);
+}
+
+}  // namespace dit
+
+namespace {
+
+uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
+uint32_t grid_for(uint64_t m, uint32_t cap = 8192) {
+  const uint64_t g = (m + dit::kT - 1) / dit::kT;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+uint32_t bits_for(uint64_t v) {  // bits of the largest key v
+  uint32_t b = 0;
+  while (b < 64 && (v >> b)) ++b;
+  return std::max<uint32_t>(b, 1);
+}
+size_t scan_u64_bytes(uint64_t n) {
+  size_t b = 0;
+  (void)rocprim::inclusive_scan(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr, (size_t)n,
+                                rocprim::plus<uint64_t>());
+  return b;
+}
+constexpr uint32_t kPrewalkBlocks = 2048;  // pre-walk grid (one trace per thread per pass)
+constexpr uint32_t kMaxPasses = 256;       // fixed-point passes of a cyclic schedule (des.hip)
+
+}  // namespace
+
+// per trace: gaps, arrivals, hops, item ends (u64), status_err (u32), scan temp
+uint64_t des_items_workspace_bytes(uint64_t n) {
+  return 4 * al256(n * 8) + al256(n * 4) + al256(scan_u64_bytes(n)) + 256;
+}
+
+int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
+  using namespace dit;
+  hipStream_t s = (hipStream_t)stream_;
+  const DesPlan &pl = *L.plan;
+  const uint64_t n = L.n_traces;
+  char *ws = (char *)L.workspace;
+  auto take = [&](uint64_t bytes) {
+    char *p = ws;
+    ws += al256(bytes);
+    return (void *)p;
+  };
+  K k{};
+  k.pos = (const DesPos *)L.d_pos;
+  k.ip = (const DesItemPos *)L.d_item_pos;
+  k.steps = (const DesStep *)L.d_steps;
+  k.step_round = L.d_step_round;
+  k.nodes = (const unsigned long long *)L.d_nodes;
+  k.ext = (const TreeExt *)L.d_ext;
+  k.tstep = (const TreeStep *)L.d_tstep;
+  k.gap = (uint64_t *)take(n * 8);
+  k.A = (uint64_t *)take(n * 8);
+  k.cnt = (uint64_t *)take(n * 8);
+  k.tend = (uint64_t *)take(n * 8);
+  k.terr = (uint32_t *)take(n * 4);
+  const size_t scan_bytes = scan_u64_bytes(n);
+  void *scan_tmp = take(scan_bytes);
+  k.stats = (unsigned long long *)L.d_stats;
+  k.table = (unsigned long long *)L.d_table;
+  k.records = L.d_records;
+  k.n = n;
+  k.trace_begin = L.trace_begin;
+  k.mean_ns = L.mean_ns;
+  k.k0 = (uint32_t)L.seed;
+  k.k1 = (uint32_t)(L.seed >> 32);
+  k.n_slots = L.n_slots;
+  uint32_t max_reps = 1, max_row = 0;
+  for (const DesPos &q : pl.pos) {
+    max_reps = std::max(max_reps, q.reps);
+    max_row = std::max(max_row, q.row);
+  }
+  const uint32_t rep_bits = max_reps > 1 ? bits_for(max_reps - 1) : 0u;
+  k.arr_bits = 64 - rep_bits;
+  k.aw = pl.item_acc;
+  k.bw = pl.item_bk;
+  auto fail = [&](const char *what) {
+    err = std::string("DES items: ") + what;
+    return 1;
+  };
+  // 1. arrivals
+  hipLaunchKernelGGL(k_gaps, dim3(grid_for(n)), dim3(kT), 0, s, k);
+  size_t b = scan_bytes;
+  if (rocprim::inclusive_scan(scan_tmp, b, k.gap, k.A, (size_t)n, rocprim::plus<uint64_t>(), s) != hipSuccess)
+    return fail("arrival scan");
+  // 2. pre-walk: count, offsets, emit
+  const uint32_t fr = L.tree_frames;
+  const bool spill = fr > 16;
+  uint32_t *spill_buf = nullptr;
+  const uint64_t pw_threads = (uint64_t)kPrewalkBlocks * kT;
+  if (spill) {
+    const uint64_t words = (uint64_t)(fr - 8 + 1) * kTreeSpillWords * pw_threads;
+    if (hipMallocAsync((void **)&spill_buf, words * 4, s) != hipSuccess) return fail("spill allocation");
+  }
+  k.spill = spill_buf;
+  auto prewalk = [&](bool emit) {
+    if (spill) {
+      if (emit) hipLaunchKernelGGL((k_prewalk<8, true, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      else hipLaunchKernelGGL((k_prewalk<8, true, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+    } else if (fr > 8) {
+      if (emit) hipLaunchKernelGGL((k_prewalk<16, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      else hipLaunchKernelGGL((k_prewalk<16, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+    } else {
+      if (emit) hipLaunchKernelGGL((k_prewalk<8, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      else hipLaunchKernelGGL((k_prewalk<8, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+    }
+  };
+  prewalk(false);
+  b = scan_bytes;
+  if (rocprim::inclusive_scan(scan_tmp, b, k.cnt, k.tend, (size_t)n, rocprim::plus<uint64_t>(), s) != hipSuccess)
+    return fail("item offset scan");
+  uint64_t M = 0;
+  if (hipMemcpyAsync(&M, k.tend + (n - 1), 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail("item count read-back");
+  if (M >= 0xFFFFFFFFull) {
+    if (spill_buf) (void)hipFreeAsync(spill_buf, s);
+    err = "DES items: a batch of more than 2^32 - 1 executed invocations (use smaller batches)";
+    return 2;
+  }
+  k.M = M;
+  // the per-item arrays and the rounds' sort buffers, one allocation
+  const uint32_t R = pl.rounds();
+  const uint32_t G = (uint32_t)pl.fin_off.size() - 1;
+  size_t sort32_bytes = 0, sort64_bytes = 0, sbk_bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, sort32_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)M, 0, 32);
+  (void)rocprim::radix_sort_pairs(nullptr, sort64_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)M, 0, 64);
+  (void)rocprim::inclusive_scan_by_key(nullptr, sbk_bytes, (const uint32_t *)nullptr, (const MP *)nullptr,
+                                       (MP *)nullptr, (size_t)M, MPThen(), rocprim::equal_to<uint32_t>());
+  const size_t tmp_bytes = std::max(std::max(sort32_bytes, sort64_bytes), sbk_bytes);
+  const uint64_t parts[] = {
+      M * 4, M * 4, M * 4, M,                                  // ipos ipar itr iown
+      M * 8, M * 8, M * 8,                                     // IA IS IF
+      M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
+      pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
+      M * 4, M * 4, M * 4, M * 4, M * 4, M * 4,                // qk fk ids qk2 qids fids (fk2 = qk)
+      M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
+      M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
+      (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 12,        // qoff foff; ovf: key overflow, no fixed point, changed
+      tmp_bytes};
+  uint64_t total = 0;
+  for (uint64_t q : parts) total += al256(q ? q : 1);
+  char *base = nullptr;
+  if (hipMallocAsync((void **)&base, total, s) != hipSuccess) {
+    if (spill_buf) (void)hipFreeAsync(spill_buf, s);
+    return fail("item allocation");
+  }
+  char *at = base;
+  auto carve = [&](uint64_t bytes) {
+    char *p = at;
+    at += al256(bytes ? bytes : 1);
+    return (void *)p;
+  };
+  k.ipos = (uint32_t *)carve(parts[0]);
+  k.ipar = (uint32_t *)carve(parts[1]);
+  k.itr = (uint32_t *)carve(parts[2]);
+  k.iown = (uint8_t *)carve(parts[3]);
+  k.IA = (uint64_t *)carve(parts[4]);
+  k.IS = (uint64_t *)carve(parts[5]);
+  k.IF = (uint64_t *)carve(parts[6]);
+  k.acc = (uint64_t *)carve(parts[7]);
+  k.bk = (uint64_t *)carve(parts[8]);
+  uint64_t *acc_b = (uint64_t *)carve(parts[9]);
+  uint32_t *qk = (uint32_t *)carve(parts[10]), *fk = (uint32_t *)carve(parts[11]);
+  uint32_t *ids = (uint32_t *)carve(parts[12]), *qk2 = (uint32_t *)carve(parts[13]);
+  uint32_t *qids = (uint32_t *)carve(parts[14]), *fids = (uint32_t *)carve(parts[15]);
+  uint64_t *key_a = (uint64_t *)carve(parts[16]), *key_b = (uint64_t *)carve(parts[17]);
+  uint32_t *val_a = (uint32_t *)carve(parts[18]), *val_b = (uint32_t *)carve(parts[19]);
+  uint32_t *rk_a = (uint32_t *)carve(parts[20]), *rk_b = (uint32_t *)carve(parts[21]);
+  uint32_t *rv_a = (uint32_t *)carve(parts[22]), *rv_b = (uint32_t *)carve(parts[23]);
+  MP *mp_in = (MP *)carve(parts[24]), *mp_out = (MP *)carve(parts[25]);
+  uint32_t *sid = (uint32_t *)carve(parts[26]);
+  uint32_t *d_qoff = (uint32_t *)carve(parts[27]), *d_foff = (uint32_t *)carve(parts[28]);
+  uint32_t *ovf = (uint32_t *)carve(parts[29]);
+  void *tmp = carve(parts[30]);
+  int rc = 0;
+  std::vector<uint32_t> qoff(R + 1), foff(G + 1);
+  do {
+    if (hipMemsetAsync(ovf, 0, 12, s) != hipSuccess) {
+      rc = fail("memset");
+      break;
+    }
+    prewalk(true);
+    // 3. buckets
+    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids);
+    size_t tb = tmp_bytes;
+    if (rocprim::radix_sort_pairs(tmp, tb, qk, qk2, ids, qids, (size_t)M, 0, bits_for(R), s) != hipSuccess) {
+      rc = fail("round sort");
+      break;
+    }
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk2, M, R, d_qoff);
+    tb = tmp_bytes;
+    if (rocprim::radix_sort_pairs(tmp, tb, fk, qk, ids, fids, (size_t)M, 0, bits_for(G), s) != hipSuccess) {
+      rc = fail("finish-group sort");
+      break;
+    }
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk, M, G, d_foff);
+    if (hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(foff.data(), d_foff, (G + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = fail("bucket read-back");
+      break;
+    }
+    std::vector<char> has_steps(R, 0);
+    for (uint32_t sb : pl.step_round) has_steps[sb & ~kDesStepCut] = 1;
+    const uint32_t row_bits = bits_for(max_row);
+    // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
+    // every time: the iteration only raises values) until no stored value
+    // changes, then the pass that records the statistics (des.hip des_launch)
+    // callee maxima: zeroed per pass (a start can move down when the order of
+    // a queue changes, so maxima are never carried over); a cut step begin
+    // reads the previous pass's (the two buffers swap)
+    uint64_t *acc_a = k.acc;
+    auto pass = [&](K &kk) {
+    if (pl.cyclic) {
+      std::swap(acc_a, acc_b);
+      kk.acc = acc_a;
+      kk.acc_prev = acc_b;
+    }
+    if (hipMemsetAsync(kk.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
+      rc = fail("memset");
+      return;
+    }
+    for (uint32_t r = 0; r < R && !rc; ++r) {
+      if (has_steps[r]) hipLaunchKernelGGL(k_steps, dim3(grid_for(M)), dim3(kT), 0, s, kk, r);
+      const uint64_t m = qoff[r + 1] - qoff[r];
+      if (m) {
+        hipLaunchKernelGGL(k_qkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, key_a, val_a, ovf);
+        tb = tmp_bytes;
+        if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, 64, s) != hipSuccess) {
+          rc = fail("arrival sort");
+          break;
+        }
+        hipLaunchKernelGGL(k_rkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, val_b, m, rk_a, rv_a);
+        tb = tmp_bytes;
+        if (rocprim::radix_sort_pairs(tmp, tb, rk_a, rk_b, rv_a, rv_b, (size_t)m, 0, row_bits, s) != hipSuccess) {
+          rc = fail("service sort");
+          break;
+        }
+        hipLaunchKernelGGL(k_pairs, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, rk_b, rv_b, key_b, val_b, rk_a, mp_in,
+                           sid);
+        tb = tmp_bytes;
+        if (rocprim::inclusive_scan_by_key(tmp, tb, rk_a, mp_in, mp_out, (size_t)m, MPThen(),
+                                           rocprim::equal_to<uint32_t>(), s) != hipSuccess) {
+          rc = fail("queue scan");
+          break;
+        }
+        hipLaunchKernelGGL(k_qout, dim3(grid_for((m + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk, m, rk_b, sid,
+                           mp_out);
+      }
+      for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
+        const uint64_t mg = foff[gi + 1] - foff[gi];
+        if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for(mg)), dim3(kT), 0, s, kk, fids + foff[gi], mg);
+      }
+    }
+    };
+    if (pl.cyclic) {
+      if (hipMemsetAsync(k.IS, 0, M * 8, s) != hipSuccess || hipMemsetAsync(k.IF, 0, M * 8, s) != hipSuccess ||
+          (k.bw && hipMemsetAsync(k.bk, 0, M * 8 * k.bw, s) != hipSuccess) ||
+          hipMemsetAsync(acc_b, 0, M * 8 * k.aw, s) != hipSuccess ||
+          hipMemsetAsync(k.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
+        rc = fail("memset");
+        break;
+      }
+      K kq = k;
+      kq.quiet = 1;
+      kq.acc_prev = acc_b;
+      kq.changed = ovf + 2;
+      uint32_t p = 0;
+      for (; p < kMaxPasses && !rc; ++p) {
+        uint32_t changed = 1;
+        if (hipMemsetAsync(kq.changed, 0, 4, s) != hipSuccess) {
+          rc = fail("memset");
+          break;
+        }
+        pass(kq);
+        if (rc) break;
+        if (hipMemcpyAsync(&changed, kq.changed, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+          rc = fail("fixed-point read-back");
+          break;
+        }
+        if (!changed) break;
+      }
+      if (std::getenv("ISIM_DES_DEBUG")) std::fprintf(stderr, "isim des items: cyclic schedule, %u passes\n", p + 1);
+      if (!rc && p == kMaxPasses) {
+        static const uint32_t one = 1;
+        if (hipMemcpyAsync(ovf + 1, &one, 4, hipMemcpyHostToDevice, s) != hipSuccess) rc = fail("flag");
+      }
+      if (rc) break;
+    }
+    k.acc_prev = acc_b;
+    pass(k);
+    if (rc) break;
+    // 5. records and statistics
+    hipLaunchKernelGGL(k_final, dim3(grid_for(n, 1024)), dim3(kT), 0, s, k);
+    hipLaunchKernelGGL(k_flag_retry, dim3(1), dim3(1), 0, s, k.stats, ovf);
+    if (hipGetLastError() != hipSuccess) rc = fail("kernel launch");
+  } while (0);
+  (void)hipFreeAsync(base, s);
+  if (spill_buf) (void)hipFreeAsync(spill_buf, s);
+  return rc;
+}
+
+}  // namespace isim

@@ -98,26 +98,54 @@ void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes) {
   writes += (uint32_t)plan.steps.size();
 }
 
-int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::string &err) {
+int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan &out, std::string &err) {
   out = DesPlan();
-  if (!p.static_walk || p.stream_nodes == 0) {
-    err = "DES needs a static walk (no probabilistic calls, no mode-B aborts) of at most 2^24 invocations";
+  // the positions: a static walk's draw stream (every invocation executes in
+  // every trace), or — probabilistic calls in mode A — the lane tree walk's
+  // unrolled tree of POTENTIAL invocations (kernel_abi.h TreeNode): the item
+  // engine (des_items.hip) simulates the executed ones only
+  struct Src {
+    uint32_t slot, parent, thr;
+    bool always;
+  };
+  std::vector<Src> src;
+  if (p.static_walk && p.stream_nodes) {
+    std::vector<uint32_t> stack;
+    for (uint32_t i = 0; i < p.stream_nodes; ++i) {
+      const Node &nd = p.stream[i];
+      src.push_back({nd.meta & 0xFFFFFFu, stack.empty() ? kDesNoParent : stack.back(), nd.thr,
+                     (nd.meta & 0x80000000u) != 0});
+      stack.push_back(i);
+      for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
+    }
+  } else if (!p.static_walk && !p.tree_nodes.empty() && !modeb) {
+    out.items = true;
+    std::vector<std::pair<uint32_t, uint32_t>> stack;  // (position, end of its subtree)
+    for (uint32_t i = 0; i < (uint32_t)p.tree_nodes.size(); ++i) {
+      while (!stack.empty() && i >= stack.back().second) stack.pop_back();
+      const TreeNode &nd = p.tree_nodes[i];
+      src.push_back({i ? (uint32_t)nd.slot : kSlotRoot, stack.empty() ? kDesNoParent : stack.back().first,
+                     p.tree_ext[i].thr, (nd.flags & TF_ERR_ALWAYS) != 0});
+      stack.push_back({i, i + std::max<uint32_t>(1, nd.size)});
+    }
+  } else {
+    err = p.static_walk ? "DES needs a static walk of at most 2^24 invocations"
+          : modeb       ? "DES of a dynamic walk (probabilistic calls) needs mode A: no mode-B aborts"
+                        : "DES of a dynamic walk needs the lane tree walk's unrolled tree (" + p.tree_why + ")";
     return ISIM_EINVAL;
   }
   const int32_t n = (int32_t)g.services.size();
   std::vector<ScriptShape> shape(n);
   std::vector<char> shaped(n, 0);
-  const uint32_t np = p.stream_nodes;
+  const uint32_t np = (uint32_t)src.size();
   out.pos.resize(np);
   out.ext.assign(np, DesPosExt{kDesNone, kDesNone, 0, 0});
   std::vector<std::vector<uint32_t>> kids(np);
   std::vector<uint32_t> depth(np, 0), kstep(np, 0);  // kstep: the caller's call step of the position
   std::vector<int32_t> pos_svc(np, -1);
   std::vector<std::vector<uint32_t>> svc_pos(n);
-  std::vector<uint32_t> stack;
   for (uint32_t i = 0; i < np; ++i) {
-    const Node &nd = p.stream[i];
-    const uint32_t slot = nd.meta & 0xFFFFFFu;
+    const uint32_t slot = src[i].slot;
     const int32_t svc = slot == kSlotRoot ? p.entry : p.slot_callee[slot];
     if (!shaped[svc]) {
       shape[svc] = shape_of(g.services[svc]);
@@ -129,7 +157,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     }
     const ScriptShape &sh = shape[svc];
     DesPos &ps = out.pos[i];
-    ps.parent = stack.empty() ? kDesNoParent : stack.back();
+    ps.parent = src[i].parent;
     ps.row = (uint32_t)p.svc_row[svc];
     ps.slot = slot;
     ps.reps = (uint32_t)std::max<int32_t>(1, g.services[svc].num_replicas);
@@ -139,8 +167,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     // max(BK_last + floor, max_c(last step) F_c) + post
     ps.floor = sh.leaf() ? sh.pre : (sh.smax.size() == 1 ? sh.pre + sh.smax[0] : sh.smax.back());
     ps.post = sh.leaf() ? 0 : sh.gap.back();
-    ps.thr = nd.thr;
-    ps.flags = (nd.meta & 0x80000000u) ? kDesFlagAlways : 0u;
+    ps.thr = src[i].thr;
+    ps.flags = src[i].always ? kDesFlagAlways : 0u;
     if (sh.leaf()) ps.flags |= kDesFlagLeaf;
     pos_svc[i] = svc;
     svc_pos[svc].push_back(i);
@@ -153,8 +181,6 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       kids[par].push_back(i);
       depth[i] = depth[par] + 1;
     }
-    stack.push_back(i);
-    for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
   }
   for (uint32_t i = 0; i < np; ++i) {
     out.pos[i].child_off = (uint32_t)out.child.size();
@@ -239,7 +265,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       for (uint32_t j = 0; j < st.child_cnt; ++j) pred[Ab(b)].push_back({F(out.child[st.child_off + j]), 1});
     }
   }
-  std::vector<char> used(n_ops, 0);
+  std::vector<char> used(n_ops, 0), step_cut(nb, 0);
   for (uint32_t v = 0; v < np; ++v) used[Q(v)] = used[F(v)] = 1;
   for (uint32_t b = 0; b < nb; ++b) used[Ab(b)] = 1;
   // cycles (a service with a hold invoked both inside a caller's call step
@@ -298,6 +324,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       }
     }
     auto is_f = [&](uint32_t o) { return o >= nq && o < nq + np; };
+    step_cut.assign(nb, 0);
     auto is_a = [&](uint32_t o) { return o >= nq + np && o < nq + np + nb; };
     for (uint32_t o = 0; o < n_ops; ++o) {
       if (!used[o] || !is_a(o) || comp_size[comp[o]] < 2) continue;
@@ -308,7 +335,10 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
                                 return is_f(e.first) && comp[e.first] == comp[o];
                               }),
                pl.end());
-      if (pl.size() != before) out.cyclic = true;
+      if (pl.size() != before) {
+        out.cyclic = true;
+        step_cut[o - (nq + np)] = 1;
+      }
     }
   }
   // longest path in topological order (acyclic now): O(ops + edges).  A
@@ -386,7 +416,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
       fast[rnd[s]].push_back(v);
       // a leaf's finish needs only its start: the queue pass writes F (every
       // reader of F(v) runs in a later stage of Q(v)'s round or later)
-      if (out.pos[v].flags & kDesFlagLeaf) out.pos[v].flags |= kDesFlagFused;
+      if (!out.items && (out.pos[v].flags & kDesFlagLeaf)) out.pos[v].flags |= kDesFlagFused;
     }
   }
   // finish groups: by round, deepest first, most children first within a
@@ -452,7 +482,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   }
   // ---- pipelined queue segments
   auto pipeable = [&](uint32_t r) {
-    return out.arr_off[r + 1] == out.arr_off[r] && out.zero_off[r + 1] == out.zero_off[r] &&
+    return !out.items && out.arr_off[r + 1] == out.arr_off[r] && out.zero_off[r + 1] == out.zero_off[r] &&
            out.sorted_off[r + 1] == out.sorted_off[r] && out.fast_split[5 * r + 2] == out.fast_off[r + 1] &&
            out.fast_off[r + 1] > out.fast_off[r];
   };
@@ -497,7 +527,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   }
   // finishes without the start row (kDesFlagNoStart; ISIM_DES_NO_NOSTART
   // set: off, for A/B measurements)
-  if (!out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_NOSTART")) {
+  if (!out.items && !out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_NOSTART")) {
     for (uint32_t v = 0; v < np; ++v) {
       if ((out.pos[v].flags & kDesFlagFused) || kids[v].empty()) continue;
       const ScriptShape &sh = shape[pos_svc[v]];
@@ -511,7 +541,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
   // script (every arrival is start(caller) + off), no fixed-point passes, the
   // caller's first kDesDurKids non-fused callees (ISIM_DES_NO_PARENT_DUR set:
   // every position records its own, for A/B measurements)
-  if (!out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_PARENT_DUR")) {
+  if (!out.items && !out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_PARENT_DUR")) {
     for (uint32_t v = 0; v < np; ++v) {
       if (kids[v].size() > kDesUpChildLds) continue;
       uint32_t j = 0;
@@ -522,6 +552,27 @@ int build_des_plan(const ServiceGraph &g, const Program &p, DesPlan &out, std::s
     }
   }
   out.slot_mult = p.stream_mult;
+  if (out.items) {
+    // per position: its queue round, finish group, call step in its caller,
+    // and its own call steps' BK ids (des_items.hip)
+    out.item_pos.assign(np, DesItemPos{0, 0, 0, 0, kDesNone});
+    for (uint32_t v = 0; v < np; ++v) {
+      DesItemPos &ip = out.item_pos[v];
+      ip.qround = rnd[Q(v)];
+      ip.kstep = kstep[v];
+      const ScriptShape &sh = shape[pos_svc[v]];
+      ip.nsteps = (uint32_t)sh.smax.size();
+      out.item_acc = std::max<uint32_t>(out.item_acc, std::max<uint32_t>(1, ip.nsteps));
+      if (ip.nsteps >= 2) {
+        ip.bk_first = out.ext[v].bk_last - (ip.nsteps - 1);
+        out.item_bk = std::max<uint32_t>(out.item_bk, ip.nsteps);
+      }
+    }
+    for (uint32_t gi = 0; gi + 1 < out.fin_off.size(); ++gi)
+      for (uint32_t j = out.fin_off[gi]; j < out.fin_off[gi + 1]; ++j) out.item_pos[out.fin_pos[j]].fgroup = gi;
+    out.step_round.resize(nb);
+    for (uint32_t b = 0; b < nb; ++b) out.step_round[b] = rnd[Ab(b)] | (step_cut[b] ? kDesStepCut : 0u);
+  }
   return ISIM_OK;
 }
 

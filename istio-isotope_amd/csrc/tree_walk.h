@@ -129,7 +129,19 @@ ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 
 // Sink: call(slot) per executed call; resp_leaf(slot, status) per response
 // of a leaf callee (its duration is static); resp(slot, row word, T,
-// status) per response of a calling callee (the entry's is the trace result).
+// status) per response of a calling callee (the entry's is the trace result);
+// optionally exec(position, hop, caller hop, own error) per executed
+// invocation, entry included (caller hop kNoCaller) — the DES item engine's
+// pre-walk (des_items.hip) records the executed invocations with it.
+constexpr uint32_t kNoCaller = 0xFFFFFFFFu;
+template <class S, class = void>
+struct has_exec {
+  static constexpr bool value = false;
+};
+template <class S>
+struct has_exec<S, decltype((void)&S::exec)> {
+  static constexpr bool value = true;
+};
 //
 // One step() is a MACRO step: close the current invocation if the walk has
 // passed its subtree, then process position p (a call: skip it, run a leaf
@@ -356,6 +368,7 @@ TW_PRAGMA_UNROLL
       const TreeExt x = load_ext(ext, p);
       const bool own = own_error(hop, fl, x.thr, k0, k1);
       he += own ? 0x10000u : 0u;
+      if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : (f_hf & 0xFFFFu), own);
       if (entry) {
         done = true;
         lat = x.tc;
@@ -369,6 +382,7 @@ TW_PRAGMA_UNROLL
     }
     const bool own =
         (DRAW && (fl & TF_ERR_DRAW)) ? own_error(hop, fl, load_ext(ext, p).thr, k0, k1) : (fl & TF_ERR_ALWAYS) != 0;
+    if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : (f_hf & 0xFFFFu), own);
     if (!entry) push();
     f_pos = p;
     f_acc = 0;

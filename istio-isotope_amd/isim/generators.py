@@ -140,6 +140,21 @@ def mesh_topology(n_services: int = 100_000, layers: int = 8, fanout: int = 3,
             "services": services}
 
 
+def mesh_des_topology(n_services: int = 100_000, layers: int = 8, fanout: int = 3, probability: int = 30,
+                      sleep_us=(50, 250), seed: int = 7) -> Dict[str, Any]:
+    """Config 4's mesh with a sleep U{sleep_us} us at the start of every
+    script: the worker of each replica is held (DES v1), so services shared
+    by many callers queue under load; the three sequential probabilistic
+    calls are three call steps (the DES item engine's step begins,
+    DESIGN.md §10.8).  Sleeps in microseconds keep the static latency bound
+    of the 3,280-position tree below 2^32 ns (the lane tree walk's u32 time)."""
+    doc = mesh_topology(n_services, layers, fanout, probability, seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    for s in doc["services"]:
+        s["script"] = [{"sleep": f"{int(rng.integers(sleep_us[0], sleep_us[1] + 1))}us"}] + s.get("script", [])
+    return doc
+
+
 def config3_topology(n: int = 10_000, seed: int = 42) -> Dict[str, Any]:
     """BASELINE config 3: realistic multitier 10k, concurrent fan-out,
     sleep U{1..5} ms, errorRate U[0, 1%]."""

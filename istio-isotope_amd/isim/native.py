@@ -23,7 +23,7 @@ STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "E
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV",
                 10: "ECOMM"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 8  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 9  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
@@ -98,7 +98,7 @@ class MultiId(C.Structure):
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
                 ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32),
-                ("row_reads", C.c_int32), ("row_writes", C.c_int32)]
+                ("row_reads", C.c_int32), ("row_writes", C.c_int32), ("items", C.c_int32)]
 
 
 # every function declared in include/isim.h: name -> (restype, argtypes)

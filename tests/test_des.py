@@ -100,7 +100,10 @@ def _rejects(h, needle):
 
 def test_des_class():
     isim.DesHandler(_handler(config2_topology()), 1_000_000)  # sequential calls: step begins
-    _rejects(_handler(mesh_topology(800, 4)), "static walk")
+    # probabilistic calls: the item engine (mode A) over the tree's potential invocations
+    dm = isim.DesHandler(_handler(mesh_topology(800, 4)), 1_000_000)
+    assert dm.info.items == 1 and dm.info.n_positions == 40 and dm.info.n_fused == 0
+    _rejects(_handler(mesh_topology(800, 4), error_mode=isim.MODE_B), "mode A")
     doc = tree_topology(3, 3)
     doc["services"][-1]["numReplicas"] = 65
     isim.DesHandler(_handler(doc), 1_000_000)  # no sleeps: never queues, replicas do not matter
@@ -110,6 +113,7 @@ def test_des_class():
     _rejects(_handler(doc), "more than 65536 replicas")
     d = isim.DesHandler(_handler(realistic_topology(200, concurrent=True, sleep_ms=(1, 5))), 5_000_000)
     assert (d.info.n_positions, d.info.table_rows) == (200, 200)
+    assert d.info.items == 0
     assert d.info.cyclic == 0 and 0 < d.info.n_fused < 200  # the tree's leaves finish in their queue pass
     assert d.info.n_levels >= 2 and d.info.max_width >= 1
     assert d.workspace_bytes(1000) >= 200 * 1000 * 8 + 1000 * 12

@@ -1,0 +1,131 @@
+"""GPU parity of the DES item engine: dynamic walks —
+probabilistic calls (shouldSkipRequest, executable.go:84-90), mode A — under
+per-replica worker-pool contention, through the C ABI, against the
+sequential event-driven C oracle (oracle/des_oracle.c: its pre-walk fixes the
+executed calls and hop ids) — records, stats and the per-service DES table,
+bit-exact; and, for static graphs forced onto the item engine
+(ISIM_FLAG_DYNAMIC), against the level-synchronous static engine at sizes the
+oracle would take long on."""
+import json
+
+import numpy as np
+import pytest
+
+import isim
+from isim import native
+from isim.generators import mesh_des_topology, realistic_topology, tree_topology
+from isim.yamljson import obj_to_json
+
+from parity import assert_records_equal
+from test_des import _prob_canonical
+from test_des_gpu import DesCase, _sleepy_tree
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_prob(doc, p):
+    doc = json.loads(json.dumps(doc))
+    for sv in doc["services"]:
+        for st in sv.get("script", []):
+            for c in (st if isinstance(st, list) else [st]):
+                if "call" in c:
+                    name = c["call"] if isinstance(c["call"], str) else c["call"]["service"]
+                    c["call"] = {"service": name, "probability": p}
+    return doc
+
+
+def _sleepy(doc, pre="400us", post="100us"):
+    doc = json.loads(json.dumps(doc))
+    for s in doc["services"]:
+        s["script"] = [{"sleep": pre}] + s.get("script", []) + [{"sleep": post}]
+    return doc
+
+
+CASES = {
+    "real300p60": lambda: realistic_topology(300, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.3),
+                                             probability=60),
+    "real300seq_p75": lambda: realistic_topology(300, sleep_ms=(1, 5), error_rate=(0.0, 0.3), probability=75),
+    "mesh_des": lambda: mesh_des_topology(4000, 6, 3, 40),
+    "canonical_p50": lambda: _sleepy(_prob_canonical()),
+    "tree_reps_p70": lambda: _with_prob(_sleepy_tree(3, 4, reps_leaves=3), 70),
+    "seq_tree_p50": lambda: _with_prob(_sleepy(tree_topology(3, 3, sequential=True)), 50),
+}
+
+
+@pytest.mark.parametrize("mean", [300_000, 3_000_000])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_items_match_event_oracle(gpu, name, mean):
+    c = DesCase(CASES[name](), mean)
+    assert c.d.info.items == 1
+    recs, _, rows = c.compare(1000, 3000)
+    assert 0 < int(recs["hops"].sum()) < 3000 * int(c.h.info.hops_upper) or c.h.info.hops_upper == 1
+    c.compare((1 << 32) - 500, 1001)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 257])
+def test_items_ragged(gpu, n):
+    DesCase(CASES["real300p60"](), 1_000_000).compare(55, n)
+
+
+def test_items_contention(gpu):
+    # arrivals far faster than the services: long queues, every wait recorded
+    c = DesCase(CASES["mesh_des"](), 50_000)
+    _, _, rows = c.compare(0, 4000)
+    assert int(rows[:, isim.native.DES_ROW_WORDS - 2].max()) > 10_000_000  # some wait above 10 ms
+
+
+def _static_pair(doc, mean):
+    j = obj_to_json(doc)
+    g = isim.ServiceGraph.from_json(j)
+    hs = isim.Handler(g, None, isim.SimParams())
+    hd = isim.Handler(g, None, isim.SimParams(flags=native.FLAG_DYNAMIC))
+    ds, dd = isim.DesHandler(hs, mean), isim.DesHandler(hd, mean)
+    assert ds.info.items == 0 and dd.info.items == 1
+    return hs, hd, ds, dd
+
+
+@pytest.mark.parametrize("case", ["realistic", "tree_reps", "sequential"])
+def test_items_equal_static_engine(gpu, case):
+    if case == "realistic":
+        doc = realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.05))
+    elif case == "tree_reps":
+        doc = _sleepy_tree(3, 5, reps_leaves=4)
+    else:
+        doc = _sleepy(tree_topology(3, 4, sequential=True))
+    hs, hd, ds, dd = _static_pair(doc, 700_000)
+    n = 150_000
+    rs, ss, ts = ds.serve(12345, n, wide=True)
+    rd, sd, td = dd.serve(12345, n)
+    assert np.array_equal(rs, rd)
+    fs, fd = hs.fold(ss), hd.fold(sd)
+    for k in ("n_traces", "sum_latency", "sum_hops", "sum_err_hops", "n_500", "max_latency", "min_latency"):
+        assert fs[k] == fd[k], k
+    for k in ("lat_prom", "lat_log2", "svc_calls", "svc_errs", "site_calls"):
+        assert np.array_equal(np.asarray(fs[k], np.uint64), np.asarray(fd[k], np.uint64)), k
+    assert np.array_equal(ds.fold(ts), dd.fold(td))
+
+
+def test_items_device_entry_accumulates(gpu):
+    import torch
+    c = DesCase(CASES["real300p60"](), 1_000_000)
+    n = 5000
+    ws = torch.zeros(c.d.workspace_bytes(n) + 8, dtype=torch.uint8, device="cuda")
+    stats = torch.zeros(len(c.h.new_stats()), dtype=torch.int64, device="cuda")
+    table = torch.zeros(max(1, c.d.table_words), dtype=torch.int64, device="cuda")
+    rec = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for b in (0, n):
+        c.d.serve_device(b, n, rec.data_ptr(), stats.data_ptr(), table.data_ptr(), ws.data_ptr(), ws.numel(), s)
+    torch.cuda.synchronize()
+    _, st, tab = c.d.serve(0, 2 * n, device=0, records=False)
+    # two batches of n from time 0 each vs one of 2n: counts add up the same
+    got = stats.cpu().numpy().view(np.uint64)
+    assert int(got[native.ST_N_TRACES]) == 2 * n
+    assert int(got[native.ST_SUM_HOPS]) == int(c.h.fold(got)["sum_hops"])
+    tabn = table.cpu().numpy().view(np.uint64).reshape(-1, native.DES_ROW_WORDS)
+    assert int(tabn[:, native.DES_ROW_WORDS - 4].sum()) == int(got[native.ST_SUM_HOPS])
+    # the second batch's records are the oracle's for its trace ids
+    from oracle import des as od
+    orec, _, _ = od.run(c.sg, c.op, c.sg.entry(), n, n, c.mean, og=c.og)
+    r = rec.cpu().numpy().view(isim.REC_DTYPE)
+    assert_records_equal(r, orec)
