@@ -53,7 +53,13 @@ BENCH_BATCH = {
     # the pipelined queue pass's fill and drain (2^16 20.8,
     # 2^18 22.3, 2^20 23.9 M traces/s)
     "c5": 1 << 20,
+    # DES of dynamic walks on the item engine: config 3's
+    # graph at probability 50 (215 executed invocations per trace) and
+    # config 4's mesh with sleeps (a cyclic schedule: fixed-point passes)
+    "c5p": 1 << 18,
+    "c4d": 1 << 22,
 }
+DES_CONFIGS = ("c5", "c5p", "c4d")
 
 
 def parse():
@@ -64,7 +70,7 @@ def parse():
     # 2^24 traces (256 MB of records) per launch: the per-launch flush and
     # tail amortise (config 3: 2^22 335, 2^23 339, 2^24 340 M traces/s)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c4", "c5", "c5p", "c4d"])
     ap.add_argument("--prob", type=int, default=50, help="c3p: the probability on every call (1..99)")
     ap.add_argument("--no-wave-leg", action="store_true",
                     help="c3p: skip the wave-interpreter leg (kinds 2/3, ISIM_FLAG_WAVE_WALK) on the same graph")
@@ -72,8 +78,9 @@ def parse():
                     "fill the records (the library default) instead of walking every trace")
     ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
                     "64-bit only when a batch's latencies reach 2^31 ns)")
-    ap.add_argument("--mean-interarrival-ns", type=int, default=6_000_000,
-                    help="c5 (DES): mean gap of the open-loop Poisson arrivals")
+    ap.add_argument("--mean-interarrival-ns", type=int, default=0,
+                    help="DES (c5, c5p, c4d): mean gap of the open-loop Poisson arrivals (0: 6 ms for c5/c5p, "
+                         "150 us for c4d)")
     ap.add_argument("--mode", default="A", choices=["A", "B"])
     ap.add_argument("--no-mode-b", action="store_true", help="c3: skip the extra mode-B legs")
     ap.add_argument("--mode-b-steps", type=int, default=5, help="c3: timed steps of each extra mode-B leg")
@@ -84,11 +91,14 @@ def parse():
     ap.add_argument("--cpu-traces", type=int, default=0, help="cpu_baseline sample size (0 = auto)")
     args = ap.parse_args()
     args.des_auto_batch = False  # c5 with the default batch: shrink it to the device's free HBM
+    if not args.mean_interarrival_ns:
+        args.mean_interarrival_ns = 150_000 if args.config == "c4d" else 6_000_000
     return args
 
 
 def build_graph(config: str, prob: int = 50):
-    from isim.generators import config2_topology, config3_topology, config3p_topology, mesh_topology
+    from isim.generators import (config2_topology, config3_topology, config3p_topology, mesh_des_topology,
+                                 mesh_topology)
     from isim.yamljson import obj_to_json, yaml_to_json
     if config == "c1":
         j = yaml_to_json(open(os.path.join(ROOT, "tests", "golden", "topologies", "canonical.yaml"), "rb").read())
@@ -114,6 +124,18 @@ def build_graph(config: str, prob: int = 50):
                             "arrivals, one FIFO worker per replica held for the service's sleep (DES v1, DESIGN.md "
                             "§10), level-synchronous exact DES",
                 "services": 10000}
+    elif config == "c5p":
+        j = obj_to_json(config3p_topology(prob))
+        desc = {"workload": f"config 5 on a dynamic walk: config 3's 10k-service graph with probability {prob} on "
+                            "every call + per-replica worker-pool contention (DES v1), item engine over the "
+                            "executed invocations (DESIGN.md §10.9)",
+                "services": 10000, "probability": prob}
+    elif config == "c4d":
+        j = obj_to_json(mesh_des_topology())
+        desc = {"workload": "config 4's 100k-service mesh (fan-out 3 at probability 30, numReplicas) with a sleep "
+                            "U{50..250} us per script under per-replica worker-pool contention (DES v1): item "
+                            "engine, cyclic call-step schedule run to its fixed point (DESIGN.md §10.9)",
+                "services": 100000}
     else:
         j = obj_to_json(config3_topology())
         desc = {"workload": "create_realistic_topology.py multitier Barabasi 10k services, concurrent fan-out, "
@@ -277,11 +299,21 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     # 500 counts / finalize ~44 B, records 16 B
     R = 8 if wide[0] else 4
     rows = d.info.row_reads + d.info.row_writes
-    alg_bytes = B * (R * rows + npos // 4 + 44 + (0 if args.no_records else 16))
+    items = d.info.items == 1
+    hops = folded["sum_hops"] / total
+    if items:
+        # the item engine: per executed invocation the
+        # pre-walk writes 13 B, the two bucket sorts move 2 x 16 B, the queue
+        # pass ~96 B (keys, two stable sorts, the scan's maps in and out, the
+        # start), the finish ~48 B (start, arrival, callee maximum, finish);
+        # per trace the gaps, arrivals, offsets, hops ~44 B and the record
+        alg_bytes = int(B * (hops * (13 + 32 + 96 + 48) + 44 + (0 if args.no_records else 16)))
+    else:
+        alg_bytes = B * (R * rows + npos // 4 + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
     compulsory = B * 16 + h.info.stats_words * 8 + d.table_words * 8
     traffic = occupancy = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_summary_c5.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_summary_{args.config}.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
@@ -294,7 +326,7 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     W = isim.native
     mean_wait = float(rows[:, W.DES_SUM_WAIT].sum()) / max(1, int(rows[:, W.DES_COUNT].sum()))
     line = {
-        "metric": "simulated request traces/sec (node), config c5 (DES)",
+        "metric": f"simulated request traces/sec (node), config {args.config} (DES)",
         "value": value, "unit": "traces/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic",
@@ -303,13 +335,18 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
                        mean_interarrival_ns=args.mean_interarrival_ns,
                        parallelism=f"replicas x{world}", merge=merge_label, records=not args.no_records,
                        des_levels=d.info.n_levels, des_max_width=d.info.max_width,
-                       des_fused_leaves=d.info.n_fused, des_rows="u64" if wide[0] else "u32",
+                       des_fused_leaves=d.info.n_fused,
+                       des_engine="items (dynamic walk)" if items else "level-synchronous rows",
+                       des_rows="u64" if wide[0] or items else "u32", des_cyclic=bool(d.info.cyclic),
                        workspace_bytes=wsb),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "des_* (arrivals, down and up passes of all levels, finalize) per step",
+                     "kernel": ("des_items k_* + rocPRIM sorts/scans per step" if items else
+                                "des_* (arrivals, down and up passes of all levels, finalize) per step"),
                      "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes,
-                     "basis": "workspace: the level-synchronous rows the algorithm streams (DESIGN.md §10.4)"},
+                     "basis": ("per executed invocation ~189 B of item arrays and sort traffic per pass "
+                               "(DESIGN.md §10.9)" if items else
+                               "workspace: the level-synchronous rows the algorithm streams (DESIGN.md §10.4)")},
         # the same time against the bytes any implementation must
         # move — the 16-B record per trace and the statistics written once
         # (stats buffer + DES table) — beside the workspace fraction above
@@ -570,7 +607,7 @@ def main():
     if args.batch == DEFAULT_BATCH:
         args.batch = BENCH_BATCH[args.config]
         args.des_auto_batch = args.config == "c5"
-    if args.config == "c5":
+    if args.config in DES_CONFIGS:
         return main_des(args, h, json_text, desc, params, rank, world, dev, multi, merge_label)
     info = h.info
     launch = h.launch_info(torch.cuda.current_device())

@@ -327,7 +327,7 @@ typedef struct {
   int32_t row_reads;             /* rows one trace's batch reads (queue + finish passes, one pass), 4 or 8 B each */
   int32_t row_writes;            /* rows it writes (the algorithmic bytes of bench.py's roofline) */
   int32_t items;                 /* 1: a dynamic walk (probabilistic calls, mode A) on the item engine (DESIGN.md
-                                    §10.8): positions are the tree's POTENTIAL invocations, a batch simulates the
+                                    §10.9): positions are the tree's POTENTIAL invocations, a batch simulates the
                                     executed ones and synchronizes hip_stream twice (item count, bucket sizes) */
 } isim_des_info;
 

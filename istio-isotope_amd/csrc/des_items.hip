@@ -1,4 +1,4 @@
-// DES item engine (DESIGN.md §10.8): the exact per-replica worker-pool DES of
+// DES item engine (DESIGN.md §10.9): the exact per-replica worker-pool DES of
 // a DYNAMIC walk — probabilistic calls (shouldSkipRequest, isotope/service/
 // pkg/srv/executable.go:84-90), mode A — on the GPU.
 //

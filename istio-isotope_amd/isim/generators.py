@@ -146,7 +146,7 @@ def mesh_des_topology(n_services: int = 100_000, layers: int = 8, fanout: int = 
     script: the worker of each replica is held (DES v1), so services shared
     by many callers queue under load; the three sequential probabilistic
     calls are three call steps (the DES item engine's step begins,
-    DESIGN.md §10.8).  Sleeps in microseconds keep the static latency bound
+    DESIGN.md §10.9).  Sleeps in microseconds keep the static latency bound
     of the 3,280-position tree below 2^32 ns (the lane tree walk's u32 time)."""
     doc = mesh_topology(n_services, layers, fanout, probability, seed)
     rng = np.random.Generator(np.random.PCG64(seed + 1))

@@ -1,4 +1,4 @@
-"""GPU parity of the DES item engine (DESIGN.md §10.8): dynamic walks —
+"""GPU parity of the DES item engine (DESIGN.md §10.9): dynamic walks —
 probabilistic calls (shouldSkipRequest, executable.go:84-90), mode A — under
 per-replica worker-pool contention, through the C ABI, against the
 sequential event-driven C oracle (oracle/des_oracle.c: its pre-walk fixes the
