@@ -115,7 +115,6 @@ struct K {
   isim_trace_rec *records;
   uint64_t n, trace_begin, mean_ns;
   uint32_t k0, k1, n_slots;
-  uint32_t arr_bits;               // arrival bits of a queue key (64 - replica bits)
   // cyclic schedules (des_plan.cpp): passes to a fixed point; a quiet pass
   // records no statistics and flags any stored value it changes
   uint32_t quiet;
@@ -193,12 +192,27 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k) {
 }
 
 // ---- 3. bucket keys: the position's queue round and finish group
-__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids) {
-  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
-    const DesItemPos p = k.ip[k.ipos[i]];
-    qk[i] = p.qround;
-    fk[i] = p.fgroup;
-    ids[i] = (uint32_t)i;
+// and the items of multi-step scripts (step begins: any order), appended
+// one atomic per wave
+__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids, uint32_t *ms,
+                                                    uint32_t *n_ms) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t i0 = gid() - lane; i0 < k.M; i0 += nthreads()) {  // whole waves stay in the loop
+    const uint64_t i = i0 + lane;
+    bool multi = false;
+    if (i < k.M) {
+      const DesItemPos p = k.ip[k.ipos[i]];
+      qk[i] = p.qround;
+      fk[i] = p.fgroup;
+      ids[i] = (uint32_t)i;
+      multi = p.nsteps >= 2;
+    }
+    const unsigned long long mask = __ballot(multi);
+    if (!mask) continue;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(n_ms, (uint32_t)__popcll(mask));
+    base = __shfl(base, 0, 64);
+    if (multi) ms[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)i;
   }
 }
 
@@ -212,10 +226,10 @@ __global__ void __launch_bounds__(kT) k_bounds(const uint32_t *keys, uint64_t m,
 }
 
 // ---- 4a. step begins of round r (calls after calls, des.h DesStep)
-__global__ void __launch_bounds__(kT) k_steps(K k, uint32_t r) {
-  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+__global__ void __launch_bounds__(kT) k_steps(K k, uint32_t r, const uint32_t *ms, uint64_t m) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint64_t i = ms[j];
     const DesItemPos p = k.ip[k.ipos[i]];
-    if (p.nsteps < 2) continue;
     for (uint32_t s = 0; s < p.nsteps; ++s) {
       const uint32_t b = p.bk_first + s;
       const uint32_t sr = k.step_round[b];
@@ -235,9 +249,23 @@ __global__ void __launch_bounds__(kT) k_steps(K k, uint32_t r) {
   }
 }
 
-// ---- 4b. queues of round r: arrival and key per item (replica | arrival)
-__global__ void __launch_bounds__(kT) k_qkeys(K k, const uint32_t *ids, uint64_t m, uint64_t *key, uint32_t *val,
-                                              uint32_t *ovf) {
+// FIFO of one worker as a max-plus map x -> max(x + B, C) on "free at x"
+// (des.hip SegMP without the segment flag: rocPRIM's scan by key segments)
+struct MP {
+  uint64_t B, C;
+};
+struct MPThen {
+  __device__ __forceinline__ MP operator()(const MP &a, const MP &b) const {
+    const uint64_t c = a.C + b.B;
+    return MP{a.B + b.B, c > b.C ? c : b.C};
+  }
+};
+
+// ---- 4b. queues of round r: each item's arrival and replica, and the
+// round's arrival range (one 64-bit atomic min / max per wave)
+__global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t m, uint32_t *repb,
+                                             unsigned long long *mm) {
+  unsigned long long lo = ~0ull, hi = 0;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
     const uint32_t v = k.ipos[i];
@@ -252,13 +280,63 @@ __global__ void __launch_bounds__(kT) k_qkeys(K k, const uint32_t *ids, uint64_t
       a = (ks == 0 ? k.IS[par] : k.bk[(uint64_t)par * k.bw + ks]) + P.off;
     }
     k.IA[i] = a;
-    uint64_t rep = 0;
+    uint32_t rep = 0;
     if (P.reps > 1) {
       const uint32_t hop = (uint32_t)(i - item_off(k, t));
       rep = draw0(k.trace_begin + t, hop, 0x80000002u, k.k0, k.k1) % P.reps;
     }
-    if (k.arr_bits < 64 && (a >> k.arr_bits)) atomicOr(ovf, 1u);
-    key[j] = k.arr_bits < 64 ? (rep << k.arr_bits) | a : a;
+    repb[j] = rep;
+    lo = a < lo ? a : lo;
+    hi = a > hi ? a : hi;
+  }
+  for (uint32_t d = 32; d > 0; d >>= 1) {
+    const unsigned long long x = __shfl_xor(lo, d, 64), y = __shfl_xor(hi, d, 64);
+    lo = x < lo ? x : lo;
+    hi = y > hi ? y : hi;
+  }
+  if ((threadIdx.x & 63u) == 0 && lo <= hi) {
+    atomicMin(mm, lo);
+    atomicMax(mm + 1, hi);
+  }
+}
+
+// ONE sort key when the bits fit: row | replica | arrival - amin (the tie
+// order of equal keys is the item order: trace, hop)
+__global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
+                                              uint64_t amin, uint32_t rb, uint32_t ab, uint64_t *key, uint32_t *val) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t i = ids[j];
+    const uint64_t row = k.pos[k.ipos[i]].row;
+    key[j] = (((row << rb) | repb[j]) << ab) | (k.IA[i] - amin);
+    val[j] = i;
+  }
+}
+
+// the segment key (row | replica), row, map (hold, a + hold) and item of
+// each position of the sorted order
+__global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *key, const uint32_t *items,
+                                               uint32_t rb, uint32_t ab, uint32_t *segk, uint32_t *rowk, MP *mp,
+                                               uint32_t *sid) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint64_t kk = key[j];
+    const uint32_t i = items[j];
+    const uint64_t hold = k.pos[k.ipos[i]].hold;
+    segk[j] = (uint32_t)(kk >> ab);
+    rowk[j] = (uint32_t)(kk >> (ab + rb));
+    mp[j] = MP{hold, k.IA[i] + hold};
+    sid[j] = i;
+  }
+}
+
+// TWO stable sorts otherwise: replica | arrival - amin first, then the row
+__global__ void __launch_bounds__(kT) k_qkey2(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
+                                              uint64_t amin, uint32_t rb, uint64_t *key, uint32_t *val,
+                                              uint32_t *ovf) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t i = ids[j];
+    const uint64_t a = k.IA[i] - amin;
+    if (rb && (a >> (64 - rb))) atomicOr(ovf, 1u);
+    key[j] = rb ? ((uint64_t)repb[j] << (64 - rb)) | a : a;
     val[j] = i;
   }
 }
@@ -271,32 +349,16 @@ __global__ void __launch_bounds__(kT) k_rkeys(K k, const uint32_t *items, uint64
   }
 }
 
-// FIFO of one worker as a max-plus map x -> max(x + B, C) on "free at x"
-// (des.hip SegMP without the segment flag: rocPRIM's scan by key segments)
-struct MP {
-  uint64_t B, C;
-};
-struct MPThen {
-  __device__ __forceinline__ MP operator()(const MP &a, const MP &b) const {
-    const uint64_t c = a.C + b.B;
-    return MP{a.B + b.B, c > b.C ? c : b.C};
-  }
-};
-
-// the segment key (row | replica) and map (hold, a + hold) of each item in
-// (row, replica, arrival, trace, hop) order; sid: the item
-__global__ void __launch_bounds__(kT) k_pairs(K k, uint64_t m, const uint32_t *rkb, const uint32_t *rvb,
-                                              const uint64_t *key, const uint32_t *items, uint32_t *segk, MP *mp,
-                                              uint32_t *sid) {
-  const uint64_t amask = k.arr_bits < 64 ? (1ull << k.arr_bits) - 1 : ~0ull;
+__global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *rkb, const uint32_t *rvb,
+                                               const uint64_t *key, const uint32_t *items, uint32_t rb, uint32_t *segk,
+                                               MP *mp, uint32_t *sid) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t j1 = rvb[j];
     const uint32_t i = items[j1];
-    const uint64_t kk = key[j1];
-    const uint32_t rep = k.arr_bits < 64 ? (uint32_t)(kk >> k.arr_bits) : 0u;
+    const uint32_t rep = rb ? (uint32_t)(key[j1] >> (64 - rb)) : 0u;
     const uint64_t hold = k.pos[k.ipos[i]].hold;
     segk[j] = (rkb[j] << 16) | rep;
-    mp[j] = MP{hold, (kk & amask) + hold};
+    mp[j] = MP{hold, k.IA[i] + hold};
     sid[j] = i;
   }
 }
@@ -515,7 +577,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     max_row = std::max(max_row, q.row);
   }
   const uint32_t rep_bits = max_reps > 1 ? bits_for(max_reps - 1) : 0u;
-  k.arr_bits = 64 - rep_bits;
   k.aw = pl.item_acc;
   k.bw = pl.item_bk;
   auto fail = [&](const char *what) {
@@ -579,10 +640,13 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 8, M * 8, M * 8,                                     // IA IS IF
       M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
       pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
+      k.bw ? M * 4 : 4,                                        // multi-step items
       M * 4, M * 4, M * 4, M * 4, M * 4, M * 4,                // qk fk ids qk2 qids fids (fk2 = qk)
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
-      (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 12,        // qoff foff; ovf: key overflow, no fixed point, changed
+      (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 16,        // qoff foff; ovf: key overflow, no fixed point,
+                                                               // changed, multi-step items
+      16,                                                      // the round's arrival range
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
@@ -607,28 +671,30 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.acc = (uint64_t *)carve(parts[7]);
   k.bk = (uint64_t *)carve(parts[8]);
   uint64_t *acc_b = (uint64_t *)carve(parts[9]);
-  uint32_t *qk = (uint32_t *)carve(parts[10]), *fk = (uint32_t *)carve(parts[11]);
-  uint32_t *ids = (uint32_t *)carve(parts[12]), *qk2 = (uint32_t *)carve(parts[13]);
-  uint32_t *qids = (uint32_t *)carve(parts[14]), *fids = (uint32_t *)carve(parts[15]);
-  uint64_t *key_a = (uint64_t *)carve(parts[16]), *key_b = (uint64_t *)carve(parts[17]);
-  uint32_t *val_a = (uint32_t *)carve(parts[18]), *val_b = (uint32_t *)carve(parts[19]);
-  uint32_t *rk_a = (uint32_t *)carve(parts[20]), *rk_b = (uint32_t *)carve(parts[21]);
-  uint32_t *rv_a = (uint32_t *)carve(parts[22]), *rv_b = (uint32_t *)carve(parts[23]);
-  MP *mp_in = (MP *)carve(parts[24]), *mp_out = (MP *)carve(parts[25]);
-  uint32_t *sid = (uint32_t *)carve(parts[26]);
-  uint32_t *d_qoff = (uint32_t *)carve(parts[27]), *d_foff = (uint32_t *)carve(parts[28]);
-  uint32_t *ovf = (uint32_t *)carve(parts[29]);
-  void *tmp = carve(parts[30]);
+  uint32_t *ms_ids = (uint32_t *)carve(parts[10]);
+  uint32_t *qk = (uint32_t *)carve(parts[11]), *fk = (uint32_t *)carve(parts[12]);
+  uint32_t *ids = (uint32_t *)carve(parts[13]), *qk2 = (uint32_t *)carve(parts[14]);
+  uint32_t *qids = (uint32_t *)carve(parts[15]), *fids = (uint32_t *)carve(parts[16]);
+  uint64_t *key_a = (uint64_t *)carve(parts[17]), *key_b = (uint64_t *)carve(parts[18]);
+  uint32_t *val_a = (uint32_t *)carve(parts[19]), *val_b = (uint32_t *)carve(parts[20]);
+  uint32_t *rk_a = (uint32_t *)carve(parts[21]), *rk_b = (uint32_t *)carve(parts[22]);
+  uint32_t *rv_a = (uint32_t *)carve(parts[23]), *rv_b = (uint32_t *)carve(parts[24]);
+  MP *mp_in = (MP *)carve(parts[25]), *mp_out = (MP *)carve(parts[26]);
+  uint32_t *sid = (uint32_t *)carve(parts[27]);
+  uint32_t *d_qoff = (uint32_t *)carve(parts[28]), *d_foff = (uint32_t *)carve(parts[29]);
+  uint32_t *ovf = (uint32_t *)carve(parts[30]);
+  uint64_t *mm = (uint64_t *)carve(parts[31]);
+  void *tmp = carve(parts[32]);
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
-    if (hipMemsetAsync(ovf, 0, 12, s) != hipSuccess) {
+    if (hipMemsetAsync(ovf, 0, 16, s) != hipSuccess) {
       rc = fail("memset");
       break;
     }
     prewalk(true);
     // 3. buckets
-    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids);
+    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids, ms_ids, ovf + 3);
     size_t tb = tmp_bytes;
     if (rocprim::radix_sort_pairs(tmp, tb, qk, qk2, ids, qids, (size_t)M, 0, bits_for(R), s) != hipSuccess) {
       rc = fail("round sort");
@@ -641,7 +707,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       break;
     }
     hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk, M, G, d_foff);
-    if (hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    uint32_t n_ms = 0;
+    if (hipMemcpyAsync(&n_ms, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(foff.data(), d_foff, (G + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = fail("bucket read-back");
@@ -650,6 +718,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     std::vector<char> has_steps(R, 0);
     for (uint32_t sb : pl.step_round) has_steps[sb & ~kDesStepCut] = 1;
     const uint32_t row_bits = bits_for(max_row);
+    // A/B switch: always the two-sort queue path
+    const bool two_sorts = std::getenv("ISIM_DES_ITEMS_TWO_SORTS") != nullptr;
     // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
     // every time: the iteration only raises values) until no stored value
     // changes, then the pass that records the statistics (des.hip des_launch)
@@ -668,23 +738,49 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       return;
     }
     for (uint32_t r = 0; r < R && !rc; ++r) {
-      if (has_steps[r]) hipLaunchKernelGGL(k_steps, dim3(grid_for(M)), dim3(kT), 0, s, kk, r);
+      if (has_steps[r] && n_ms)
+        hipLaunchKernelGGL(k_steps, dim3(grid_for(n_ms)), dim3(kT), 0, s, kk, r, ms_ids, (uint64_t)n_ms);
       const uint64_t m = qoff[r + 1] - qoff[r];
       if (m) {
-        hipLaunchKernelGGL(k_qkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, key_a, val_a, ovf);
-        tb = tmp_bytes;
-        if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, 64, s) != hipSuccess) {
-          rc = fail("arrival sort");
+        if (hipMemsetAsync(mm, 0xFF, 8, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 8, s) != hipSuccess) {
+          rc = fail("memset");
           break;
         }
-        hipLaunchKernelGGL(k_rkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, val_b, m, rk_a, rv_a);
-        tb = tmp_bytes;
-        if (rocprim::radix_sort_pairs(tmp, tb, rk_a, rk_b, rv_a, rv_b, (size_t)m, 0, row_bits, s) != hipSuccess) {
-          rc = fail("service sort");
+        hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
+                           (unsigned long long *)mm);
+        uint64_t hmm[2] = {0, 0};
+        if (hipMemcpyAsync(hmm, mm, 16, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+          rc = fail("arrival range read-back");
           break;
         }
-        hipLaunchKernelGGL(k_pairs, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, rk_b, rv_b, key_b, val_b, rk_a, mp_in,
-                           sid);
+        const uint32_t ab = bits_for(hmm[1] - hmm[0]);
+        tb = tmp_bytes;
+        if (!two_sorts && row_bits + rep_bits + ab <= 64) {
+          hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
+                             ab, key_a, val_a);
+          if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, row_bits + rep_bits + ab,
+                                        s) != hipSuccess) {
+            rc = fail("queue sort");
+            break;
+          }
+          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b, rep_bits, ab, rk_a,
+                             rk_b, mp_in, sid);
+        } else {
+          hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
+                             key_a, val_a, ovf);
+          if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, 64, s) != hipSuccess) {
+            rc = fail("arrival sort");
+            break;
+          }
+          hipLaunchKernelGGL(k_rkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, val_b, m, rk_a, rv_a);
+          tb = tmp_bytes;
+          if (rocprim::radix_sort_pairs(tmp, tb, rk_a, rk_b, rv_a, rv_b, (size_t)m, 0, row_bits, s) != hipSuccess) {
+            rc = fail("service sort");
+            break;
+          }
+          hipLaunchKernelGGL(k_pairs2, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, rk_b, rv_b, key_b, val_b, rep_bits,
+                             rk_a, mp_in, sid);
+        }
         tb = tmp_bytes;
         if (rocprim::inclusive_scan_by_key(tmp, tb, rk_a, mp_in, mp_out, (size_t)m, MPThen(),
                                            rocprim::equal_to<uint32_t>(), s) != hipSuccess) {

@@ -129,3 +129,11 @@ def test_items_device_entry_accumulates(gpu):
     orec, _, _ = od.run(c.sg, c.op, c.sg.entry(), n, n, c.mean, og=c.og)
     r = rec.cpu().numpy().view(isim.REC_DTYPE)
     assert_records_equal(r, orec)
+
+
+@pytest.mark.parametrize("name", ["real300p60", "tree_reps_p70", "canonical_p50"])
+def test_items_two_sort_queue_path(gpu, name, monkeypatch):
+    # the fallback queue path (replica | arrival, then the row: two stable
+    # sorts), taken when row | replica | arrival does not fit one 64-bit key
+    monkeypatch.setenv("ISIM_DES_ITEMS_TWO_SORTS", "1")
+    DesCase(CASES[name](), 500_000).compare(31, 2500)
