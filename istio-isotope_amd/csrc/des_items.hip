@@ -108,6 +108,7 @@ struct K {
   uint8_t *iown;
   uint64_t *IA, *IS, *IF, *acc, *bk;
   const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
+  const uint64_t *row_hold;        // per duration-table row: the service's worker hold
   uint32_t aw, bw;                 // acc / bk slots per item
   uint64_t M;
   // outputs
@@ -192,60 +193,73 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k) {
 }
 
 // ---- 3. bucket keys: the position's queue round and finish group
-// and the items of multi-step scripts (step begins: any order), appended
-// one atomic per wave
-__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids, uint32_t *ms,
-                                                    uint32_t *n_ms) {
+// (finish groups keyed with the position below them, so a group's items come
+// position by position: k_fin sums runs), and the step-begin ops of the
+// multi-step items: (round, item << 16 | step), appended one atomic per wave
+__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids, uint32_t *sk,
+                                                    unsigned long long *sv, uint32_t *n_ops) {
   const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t i0 = gid() - lane; i0 < k.M; i0 += nthreads()) {  // whole waves stay in the loop
     const uint64_t i = i0 + lane;
-    bool multi = false;
+    uint32_t nst = 0;
+    DesItemPos p{};
     if (i < k.M) {
-      const DesItemPos p = k.ip[k.ipos[i]];
+      const uint32_t v = k.ipos[i];
+      p = k.ip[v];
       qk[i] = p.qround;
-      fk[i] = p.fgroup;
+      fk[i] = (p.fgroup << 16) | v;
       ids[i] = (uint32_t)i;
-      multi = p.nsteps >= 2;
+      nst = p.nsteps >= 2 ? p.nsteps : 0u;
     }
-    const unsigned long long mask = __ballot(multi);
-    if (!mask) continue;
+    // wave prefix sum of the op counts
+    uint32_t incl = nst;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += x;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (!total) continue;
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(n_ms, (uint32_t)__popcll(mask));
+    if (lane == 0) base = atomicAdd(n_ops, total);
     base = __shfl(base, 0, 64);
-    if (multi) ms[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    for (uint32_t s2 = 0; s2 < nst; ++s2) {
+      const uint32_t o = base + incl - nst + s2;
+      sk[o] = k.step_round[p.bk_first + s2] & ~kDesStepCut;
+      sv[o] = ((unsigned long long)i << 16) | s2;
+    }
   }
 }
 
-// off[b] = first index of key b in the sorted keys (b = 0..nb)
-__global__ void __launch_bounds__(kT) k_bounds(const uint32_t *keys, uint64_t m, uint32_t nb, uint32_t *off) {
+// off[b] = first index of key b in the sorted keys >> shift (b = 0..nb)
+__global__ void __launch_bounds__(kT) k_bounds(const uint32_t *keys, uint64_t m, uint32_t nb, uint32_t shift,
+                                               uint32_t *off) {
   for (uint64_t i = gid(); i <= m; i += nthreads()) {
-    const uint32_t lo = i == 0 ? 0u : keys[i - 1] + 1u;  // keys (keys[i-1], keys[i]] start here
-    const uint32_t hi = i == m ? nb : keys[i];
+    const uint32_t lo = i == 0 ? 0u : (keys[i - 1] >> shift) + 1u;  // keys (keys[i-1], keys[i]] start here
+    const uint32_t hi = i == m ? nb : (keys[i] >> shift);
     for (uint32_t b = lo; b <= hi && b <= nb; ++b) off[b] = (uint32_t)i;
   }
 }
 
 // ---- 4a. step begins of round r (calls after calls, des.h DesStep)
-__global__ void __launch_bounds__(kT) k_steps(K k, uint32_t r, const uint32_t *ms, uint64_t m) {
+__global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops, uint64_t m) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
-    const uint64_t i = ms[j];
+    const unsigned long long op = ops[j];
+    const uint64_t i = op >> 16;
+    const uint32_t s = (uint32_t)(op & 0xFFFFu);
     const DesItemPos p = k.ip[k.ipos[i]];
-    for (uint32_t s = 0; s < p.nsteps; ++s) {
-      const uint32_t b = p.bk_first + s;
-      const uint32_t sr = k.step_round[b];
-      if ((sr & ~kDesStepCut) != r) continue;
-      const DesStep st = k.steps[b];
-      uint64_t v;
-      if (s == 0) {
-        v = k.IS[i];
-      } else {
-        v = k.bk[i * k.bw + (s - 1)] + st.smax;
-        // a cut step's callees finish later in the pass: their maxima of the previous one
-        const uint64_t c = ((sr & kDesStepCut) ? k.acc_prev : k.acc)[i * k.aw + (s - 1)];
-        v = c > v ? c : v;
-      }
-      store_tracked(k, k.bk + i * k.bw + s, v + st.add);
+    const uint32_t b = p.bk_first + s;
+    const uint32_t sr = k.step_round[b];
+    const DesStep st = k.steps[b];
+    uint64_t v;
+    if (s == 0) {
+      v = k.IS[i];
+    } else {
+      v = k.bk[i * k.bw + (s - 1)] + st.smax;
+      // a cut step's callees finish later in the pass: their maxima of the previous one
+      const uint64_t c = ((sr & kDesStepCut) ? k.acc_prev : k.acc)[i * k.aw + (s - 1)];
+      v = c > v ? c : v;
     }
+    store_tracked(k, k.bk + i * k.bw + s, v + st.add);
   }
 }
 
@@ -315,16 +329,17 @@ __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t
 // the segment key (row | replica), row, map (hold, a + hold) and item of
 // each position of the sorted order
 __global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *key, const uint32_t *items,
-                                               uint32_t rb, uint32_t ab, uint32_t *segk, uint32_t *rowk, MP *mp,
-                                               uint32_t *sid) {
+                                               uint32_t rb, uint32_t ab, uint64_t amin, uint32_t *segk,
+                                               uint32_t *rowk, MP *mp, uint32_t *sid) {
+  const uint64_t amask = (1ull << ab) - 1ull;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint64_t kk = key[j];
-    const uint32_t i = items[j];
-    const uint64_t hold = k.pos[k.ipos[i]].hold;
+    const uint32_t row = (uint32_t)(kk >> (ab + rb));
+    const uint64_t hold = k.row_hold[row];
     segk[j] = (uint32_t)(kk >> ab);
-    rowk[j] = (uint32_t)(kk >> (ab + rb));
-    mp[j] = MP{hold, k.IA[i] + hold};
-    sid[j] = i;
+    rowk[j] = row;
+    mp[j] = MP{hold, (kk & amask) + amin + hold};
+    sid[j] = items[j];
   }
 }
 
@@ -356,7 +371,7 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
     const uint32_t j1 = rvb[j];
     const uint32_t i = items[j1];
     const uint32_t rep = rb ? (uint32_t)(key[j1] >> (64 - rb)) : 0u;
-    const uint64_t hold = k.pos[k.ipos[i]].hold;
+    const uint64_t hold = k.row_hold[rkb[j]];
     segk[j] = (rkb[j] << 16) | rep;
     mp[j] = MP{hold, k.IA[i] + hold};
     sid[j] = i;
@@ -367,7 +382,7 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 // thread's span are summed before the atomics)
 constexpr uint32_t kQSpan = 8;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
-                                             const MP *inc) {
+                                             const MP *in, const MP *inc) {
   for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
     uint32_t row = kNone;
     unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
@@ -381,11 +396,11 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
     };
     for (uint64_t j = j0; j < j0 + kQSpan && j < m; ++j) {
       const uint32_t i = sid[j];
-      const uint64_t hold = k.pos[k.ipos[i]].hold;
-      const uint64_t S = inc[j].C - hold;
-      const uint64_t a = k.IA[i];
-      store_tracked(k, k.IS + i, S);
       const uint32_t r = rkb[j];
+      const uint64_t hold = k.row_hold[r];
+      const uint64_t S = inc[j].C - hold;
+      const uint64_t a = in[j].C - hold;
+      store_tracked(k, k.IS + i, S);
       if (r != row) {
         if (!k.quiet) flush();
         row = r;
@@ -401,35 +416,69 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
   }
 }
 
-// ---- 4c. finishes of one group
+// ---- 4c. finishes of one group (its items position by position): per
+// item the finish and its callee maximum into the caller's slot; the
+// statistics summed over a thread's run of one position (and one bucket for
+// the histogram) before the atomics
 __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
-  for (uint64_t j = gid(); j < m; j += nthreads()) {
-    const uint32_t i = ids[j];
-    const uint32_t v = k.ipos[i];
-    const DesPos P = k.pos[v];
-    const DesItemPos p = k.ip[v];
-    uint64_t F;
-    if (P.flags & kDesFlagLeaf) {
-      F = k.IS[i] + P.floor;
-    } else {
-      const uint32_t last = p.nsteps >= 2 ? p.nsteps - 1u : 0u;
-      F = (p.nsteps >= 2 ? k.bk[(uint64_t)i * k.bw + last] : k.IS[i]) + P.floor;
-      const uint64_t c = k.acc[(uint64_t)i * k.aw + last];
-      F = (c > F ? c : F) + P.post;
+  for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+    uint32_t v_run = kNone, b_run = kNone;
+    DesPos P{};
+    DesItemPos p{};
+    unsigned long long n = 0, n5 = 0, d0 = 0, d1 = 0, nb = 0;
+    auto flush_bucket = [&]() {
+      if (!k.quiet && nb) atomicAdd(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS + b_run, nb);
+      nb = 0;
+    };
+    auto flush = [&]() {
+      flush_bucket();
+      if (k.quiet || v_run == kNone || !n) return;
+      unsigned long long *tr = k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS;
+      if (d0) atomicAdd(tr + 2 * ISIM_N_PROM, d0);
+      if (d1) atomicAdd(tr + 2 * ISIM_N_PROM + 1, d1);
+      if (P.parent != kDesNoParent) {
+        atomicAdd(k.stats + ISIM_ST_SITES + P.slot, n);
+        if (n5) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P.slot, n5);
+      }
+    };
+    for (uint64_t j = j0; j < j0 + kQSpan && j < m; ++j) {
+      const uint32_t i = ids[j];
+      const uint32_t v = k.ipos[i];
+      if (v != v_run) {
+        flush();
+        v_run = v;
+        P = k.pos[v];
+        p = k.ip[v];
+        n = n5 = d0 = d1 = 0;
+        b_run = kNone;
+      }
+      uint64_t F;
+      if (P.flags & kDesFlagLeaf) {
+        F = k.IS[i] + P.floor;
+      } else {
+        const uint32_t last = p.nsteps >= 2 ? p.nsteps - 1u : 0u;
+        F = (p.nsteps >= 2 ? k.bk[(uint64_t)i * k.bw + last] : k.IS[i]) + P.floor;
+        const uint64_t c = k.acc[(uint64_t)i * k.aw + last];
+        F = (c > F ? c : F) + P.post;
+      }
+      store_tracked(k, k.IF + i, F);
+      const uint32_t par = k.ipar[i];
+      if (par != kNone) atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
+      if (k.quiet) continue;
+      const uint32_t own = k.iown[i];
+      const uint64_t dur = F - k.IA[i];
+      const uint32_t b = own * ISIM_N_PROM + prom_bucket(dur);
+      if (b != b_run) {
+        flush_bucket();
+        b_run = b;
+      }
+      nb += 1;
+      n += 1;
+      n5 += own;
+      if (own) d1 += dur;
+      else d0 += dur;
     }
-    store_tracked(k, k.IF + i, F);
-    const uint32_t par = k.ipar[i];
-    if (par != kNone) atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
-    if (k.quiet) continue;
-    const uint32_t own = k.iown[i];
-    const uint64_t dur = F - k.IA[i];
-    unsigned long long *tr = k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS;
-    atomicAdd(tr + own * ISIM_N_PROM + prom_bucket(dur), 1ull);
-    atomicAdd(tr + 2 * ISIM_N_PROM + own, (unsigned long long)dur);
-    if (par != kNone) {
-      atomicAdd(k.stats + ISIM_ST_SITES + P.slot, 1ull);
-      if (own) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P.slot, 1ull);
-    }
+    flush();
   }
 }
 
@@ -634,19 +683,31 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
                                   (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)M, 0, 64);
   (void)rocprim::inclusive_scan_by_key(nullptr, sbk_bytes, (const uint32_t *)nullptr, (const MP *)nullptr,
                                        (MP *)nullptr, (size_t)M, MPThen(), rocprim::equal_to<uint32_t>());
-  const size_t tmp_bytes = std::max(std::max(sort32_bytes, sort64_bytes), sbk_bytes);
+  size_t sop_bytes = 0;
+  if (pl.item_bk)
+    (void)rocprim::radix_sort_pairs(nullptr, sop_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                    (size_t)(M * pl.item_bk), 0, 32);
+  const size_t tmp_bytes = std::max(std::max(std::max(sort32_bytes, sort64_bytes), sbk_bytes), sop_bytes);
+  // per duration-table row: the service's worker hold (the queue kernels read no item's position)
+  std::vector<uint64_t> row_hold(std::max<size_t>(1, max_row + 1), 0);
+  for (const DesPos &q : pl.pos) row_hold[q.row] = q.hold;
+  const size_t rows_n = row_hold.size();
+  if (bits_for(G) + 16 > 32) return fail("more than 65535 finish groups");
   const uint64_t parts[] = {
       M * 4, M * 4, M * 4, M,                                  // ipos ipar itr iown
       M * 8, M * 8, M * 8,                                     // IA IS IF
       M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
       pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
-      k.bw ? M * 4 : 4,                                        // multi-step items
+      k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops: rounds, (item, step)
       M * 4, M * 4, M * 4, M * 4, M * 4, M * 4,                // qk fk ids qk2 qids fids (fk2 = qk)
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 16,        // qoff foff; ovf: key overflow, no fixed point,
                                                                // changed, multi-step items
       16,                                                      // the round's arrival range
+      k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
+      (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
@@ -671,20 +732,25 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.acc = (uint64_t *)carve(parts[7]);
   k.bk = (uint64_t *)carve(parts[8]);
   uint64_t *acc_b = (uint64_t *)carve(parts[9]);
-  uint32_t *ms_ids = (uint32_t *)carve(parts[10]);
-  uint32_t *qk = (uint32_t *)carve(parts[11]), *fk = (uint32_t *)carve(parts[12]);
-  uint32_t *ids = (uint32_t *)carve(parts[13]), *qk2 = (uint32_t *)carve(parts[14]);
-  uint32_t *qids = (uint32_t *)carve(parts[15]), *fids = (uint32_t *)carve(parts[16]);
-  uint64_t *key_a = (uint64_t *)carve(parts[17]), *key_b = (uint64_t *)carve(parts[18]);
-  uint32_t *val_a = (uint32_t *)carve(parts[19]), *val_b = (uint32_t *)carve(parts[20]);
-  uint32_t *rk_a = (uint32_t *)carve(parts[21]), *rk_b = (uint32_t *)carve(parts[22]);
-  uint32_t *rv_a = (uint32_t *)carve(parts[23]), *rv_b = (uint32_t *)carve(parts[24]);
-  MP *mp_in = (MP *)carve(parts[25]), *mp_out = (MP *)carve(parts[26]);
-  uint32_t *sid = (uint32_t *)carve(parts[27]);
-  uint32_t *d_qoff = (uint32_t *)carve(parts[28]), *d_foff = (uint32_t *)carve(parts[29]);
-  uint32_t *ovf = (uint32_t *)carve(parts[30]);
-  uint64_t *mm = (uint64_t *)carve(parts[31]);
-  void *tmp = carve(parts[32]);
+  uint32_t *op_k = (uint32_t *)carve(parts[10]);
+  unsigned long long *op_v = (unsigned long long *)carve(parts[11]);
+  uint32_t *qk = (uint32_t *)carve(parts[12]), *fk = (uint32_t *)carve(parts[13]);
+  uint32_t *ids = (uint32_t *)carve(parts[14]), *qk2 = (uint32_t *)carve(parts[15]);
+  uint32_t *qids = (uint32_t *)carve(parts[16]), *fids = (uint32_t *)carve(parts[17]);
+  uint64_t *key_a = (uint64_t *)carve(parts[18]), *key_b = (uint64_t *)carve(parts[19]);
+  uint32_t *val_a = (uint32_t *)carve(parts[20]), *val_b = (uint32_t *)carve(parts[21]);
+  uint32_t *rk_a = (uint32_t *)carve(parts[22]), *rk_b = (uint32_t *)carve(parts[23]);
+  uint32_t *rv_a = (uint32_t *)carve(parts[24]), *rv_b = (uint32_t *)carve(parts[25]);
+  MP *mp_in = (MP *)carve(parts[26]), *mp_out = (MP *)carve(parts[27]);
+  uint32_t *sid = (uint32_t *)carve(parts[28]);
+  uint32_t *d_qoff = (uint32_t *)carve(parts[29]), *d_foff = (uint32_t *)carve(parts[30]);
+  uint32_t *ovf = (uint32_t *)carve(parts[31]);
+  uint64_t *mm = (uint64_t *)carve(parts[32]);
+  uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
+  unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
+  uint32_t *d_soff = (uint32_t *)carve(parts[35]);
+  uint64_t *d_row_hold = (uint64_t *)carve(parts[36]);
+  void *tmp = carve(parts[37]);
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -694,29 +760,48 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     }
     prewalk(true);
     // 3. buckets
-    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids, ms_ids, ovf + 3);
+    if (hipMemcpyAsync(d_row_hold, row_hold.data(), rows_n * 8, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = fail("hold table upload");
+      break;
+    }
+    k.row_hold = d_row_hold;
+    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids, op_k, op_v, ovf + 3);
     size_t tb = tmp_bytes;
     if (rocprim::radix_sort_pairs(tmp, tb, qk, qk2, ids, qids, (size_t)M, 0, bits_for(R), s) != hipSuccess) {
       rc = fail("round sort");
       break;
     }
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk2, M, R, d_qoff);
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk2, M, R, 0u, d_qoff);
     tb = tmp_bytes;
-    if (rocprim::radix_sort_pairs(tmp, tb, fk, qk, ids, fids, (size_t)M, 0, bits_for(G), s) != hipSuccess) {
+    if (rocprim::radix_sort_pairs(tmp, tb, fk, qk, ids, fids, (size_t)M, 0, bits_for(G) + 16, s) != hipSuccess) {
       rc = fail("finish-group sort");
       break;
     }
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk, M, G, d_foff);
-    uint32_t n_ms = 0;
-    if (hipMemcpyAsync(&n_ms, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk, M, G, 16u, d_foff);
+    uint32_t n_ops = 0;
+    if (hipMemcpyAsync(&n_ops, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+      rc = fail("step-op count read-back");
+      break;
+    }
+    std::vector<uint32_t> soff(R + 1, 0);
+    if (n_ops) {
+      tb = tmp_bytes;
+      if (rocprim::radix_sort_pairs(tmp, tb, op_k, op_k2, op_v, op_v2, (size_t)n_ops, 0, bits_for(R), s) != hipSuccess) {
+        rc = fail("step-op sort");
+        break;
+      }
+      hipLaunchKernelGGL(k_bounds, dim3(grid_for(n_ops + 1)), dim3(kT), 0, s, op_k2, (uint64_t)n_ops, R, 0u, d_soff);
+      if (hipMemcpyAsync(soff.data(), d_soff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+        rc = fail("step-op offsets read-back");
+        break;
+      }
+    }
+    if (hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(foff.data(), d_foff, (G + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = fail("bucket read-back");
       break;
     }
-    std::vector<char> has_steps(R, 0);
-    for (uint32_t sb : pl.step_round) has_steps[sb & ~kDesStepCut] = 1;
     const uint32_t row_bits = bits_for(max_row);
     // A/B switch: always the two-sort queue path
     const bool two_sorts = std::getenv("ISIM_DES_ITEMS_TWO_SORTS") != nullptr;
@@ -738,8 +823,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       return;
     }
     for (uint32_t r = 0; r < R && !rc; ++r) {
-      if (has_steps[r] && n_ms)
-        hipLaunchKernelGGL(k_steps, dim3(grid_for(n_ms)), dim3(kT), 0, s, kk, r, ms_ids, (uint64_t)n_ms);
+      if (soff[r + 1] > soff[r])
+        hipLaunchKernelGGL(k_steps, dim3(grid_for(soff[r + 1] - soff[r])), dim3(kT), 0, s, kk, op_v2 + soff[r],
+                           (uint64_t)(soff[r + 1] - soff[r]));
       const uint64_t m = qoff[r + 1] - qoff[r];
       if (m) {
         if (hipMemsetAsync(mm, 0xFF, 8, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 8, s) != hipSuccess) {
@@ -763,8 +849,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
             rc = fail("queue sort");
             break;
           }
-          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b, rep_bits, ab, rk_a,
-                             rk_b, mp_in, sid);
+          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b, rep_bits, ab, hmm[0],
+                             rk_a, rk_b, mp_in, sid);
         } else {
           hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
                              key_a, val_a, ovf);
@@ -788,11 +874,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           break;
         }
         hipLaunchKernelGGL(k_qout, dim3(grid_for((m + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk, m, rk_b, sid,
-                           mp_out);
+                           mp_in, mp_out);
       }
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
         const uint64_t mg = foff[gi + 1] - foff[gi];
-        if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for(mg)), dim3(kT), 0, s, kk, fids + foff[gi], mg);
+        if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for((mg + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk,
+                                   fids + foff[gi], mg);
       }
     }
     };

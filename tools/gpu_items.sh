@@ -18,9 +18,13 @@ for c in ${CFGS:-c5p c4d}; do
     > $O/bench_$c.log 2>&1 || { echo "bench $c failed"; tail -20 $O/bench_$c.log; exit 2; }
   grep '^{' $O/bench_$c.log | tail -1
   if [ "${PROF:-1}" = 1 ]; then
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o run \
+    # the kernel trace itself is large (thousands of launches per step): only the stats come back
+    P=/tmp/items_prof_$c
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $P -o run \
       --output-format csv -- python3 $R/bench.py --config $c --steps 2 --warmup 1 --no-cpu > $O/prof_$c.log 2>&1) \
       || { echo "profile $c failed"; tail -20 $O/prof_$c.log; exit 3; }
+    find $P -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats_$c.csv \;
+    head -25 $O/kernel_stats_$c.csv | cut -d, -f1-8
   fi
 done
 echo items done
