@@ -122,8 +122,16 @@ struct K {
   uint32_t *changed;
 };
 
+// a quiet pass flags a change with ONE atomic per wave, and none once the
+// flag is set (millions of lanes changing values in the first passes would
+// otherwise serialise on the flag's address)
 __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v) {
-  if (k.changed && *p != v) atomicOr(k.changed, 1u);
+  if (k.changed) {
+    const bool diff = *p != v;
+    if (__ballot(diff) && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)__ballot(diff)) - 1u &&
+        __hip_atomic_load(k.changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      atomicOr(k.changed, 1u);
+  }
   *p = v;
 }
 
@@ -308,9 +316,23 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
     lo = x < lo ? x : lo;
     hi = y > hi ? y : hi;
   }
-  if ((threadIdx.x & 63u) == 0 && lo <= hi) {
-    atomicMin(mm, lo);
-    atomicMax(mm + 1, hi);
+  // one min / max per workgroup, and only when it improves on the current
+  // range (thousands of workgroups on one address otherwise serialise)
+  __shared__ unsigned long long s_lo[kT / 64], s_hi[kT / 64];
+  if ((threadIdx.x & 63u) == 0) {
+    s_lo[threadIdx.x >> 6] = lo;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < kT / 64; ++w) {
+      lo = s_lo[w] < lo ? s_lo[w] : lo;
+      hi = s_hi[w] > hi ? s_hi[w] : hi;
+    }
+    if (lo <= hi) {
+      if (lo < __hip_atomic_load(mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(mm, lo);
+      if (hi > __hip_atomic_load(mm + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(mm + 1, hi);
+    }
   }
 }
 
@@ -380,7 +402,7 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 
 // start times; the queue figures per table row (runs of one row within a
 // thread's span are summed before the atomics)
-constexpr uint32_t kQSpan = 8;
+constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
                                              const MP *in, const MP *inc) {
   for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
