@@ -733,6 +733,17 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
+  // keep the freed item arrays in the device's pool between batches (the
+  // default release threshold 0 hands them back at every synchronisation,
+  // and the next batch maps them again)
+  {
+    int dev = 0;
+    hipMemPool_t pool;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  }
   char *base = nullptr;
   if (hipMallocAsync((void **)&base, total, s) != hipSuccess) {
     if (spill_buf) (void)hipFreeAsync(spill_buf, s);

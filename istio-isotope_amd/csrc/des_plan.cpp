@@ -130,7 +130,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
     }
   } else {
     err = p.static_walk ? "DES needs a static walk of at most 2^24 invocations"
-          : modeb       ? "DES of a dynamic walk (probabilistic calls) needs mode A: no mode-B aborts"
+          : modeb       ? "DES in mode B needs a static walk (no probabilistic calls, no call step after one that "
+                          "can fail); dynamic walks run on the item engine in mode A only"
                         : "DES of a dynamic walk needs the lane tree walk's unrolled tree (" + p.tree_why + ")";
     return ISIM_EINVAL;
   }
