@@ -104,8 +104,13 @@ struct K {
   uint64_t *gap, *A, *cnt, *tend;  // cnt: hops; tend: inclusive item offsets
   uint32_t *terr;                  // status_err
   // per item
-  uint32_t *ipos, *ipar, *itr;
+  uint32_t *ipos, *ipar, *itr, *ihop;
   uint8_t *iown;
+  uint32_t *troot;                 // per trace: its entry item (items are renumbered position-major)
+  // the pre-walk's items in trace order, before the renumbering: position,
+  // and caller item | (trace | own error << 31) << 32
+  uint32_t *epos;
+  unsigned long long *erec;
   uint64_t *IA, *IS, *IF, *acc, *bk;
   const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
   const uint64_t *row_hold;        // per duration-table row: the service's worker hold
@@ -159,16 +164,15 @@ struct CountSink {
   __device__ __forceinline__ void resp(uint32_t, uint32_t, uint32_t, bool) {}
 };
 struct EmitSink : CountSink {
-  uint32_t *ipos, *ipar, *itr;
-  uint8_t *iown;
+  uint32_t *epos;
+  unsigned long long *erec;
   uint64_t base;
   uint32_t t;
   __device__ __forceinline__ void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
     const uint64_t i = base + hop;
-    ipos[i] = p;
-    ipar[i] = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
-    itr[i] = t;
-    iown[i] = own ? 1 : 0;
+    epos[i] = p;
+    const uint32_t par = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
+    erec[i] = (unsigned long long)par | (unsigned long long)(t | (own ? 0x80000000u : 0u)) << 32;
   }
 };
 
@@ -184,10 +188,8 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k) {
     L.start(k.trace_begin + t);
     if constexpr (EMIT) {
       EmitSink s;
-      s.ipos = k.ipos;
-      s.ipar = k.ipar;
-      s.itr = k.itr;
-      s.iown = k.iown;
+      s.epos = k.epos;
+      s.erec = k.erec;
       s.base = item_off(k, t);
       s.t = (uint32_t)t;
       while (!L.done) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
@@ -198,6 +200,35 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k) {
       k.cnt[t] = L.hops();
     }
   }
+}
+
+// ---- 2b. renumbering: items in (position, trace) order (a stable radix
+// sort of the trace-ordered items by position) so that the passes, which
+// visit a position's items together (queues by service, finishes by
+// position), read the per-item arrays nearly in sequence
+__global__ void __launch_bounds__(kT) k_perm_keys(K k, uint32_t *key, uint32_t *val) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    key[i] = k.epos[i];
+    val[i] = (uint32_t)i;
+  }
+}
+// inv[old] = new
+__global__ void __launch_bounds__(kT) k_perm_inv(K k, const uint32_t *perm, uint32_t *inv) {
+  for (uint64_t j = gid(); j < k.M; j += nthreads()) inv[perm[j]] = (uint32_t)j;
+}
+__global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm, const uint32_t *inv) {
+  for (uint64_t j = gid(); j < k.M; j += nthreads()) {
+    const uint32_t i = perm[j];
+    const unsigned long long r = k.erec[i];
+    const uint32_t par = (uint32_t)r, t = (uint32_t)(r >> 32) & 0x7FFFFFFFu;
+    k.itr[j] = t;
+    k.iown[j] = (uint8_t)(r >> 63);
+    k.ihop[j] = (uint32_t)(i - item_off(k, t));
+    k.ipar[j] = par == kNone ? kNone : inv[par];
+  }
+}
+__global__ void __launch_bounds__(kT) k_roots(K k, const uint32_t *inv) {
+  for (uint64_t t = gid(); t < k.n; t += nthreads()) k.troot[t] = inv[item_off(k, t)];
 }
 
 // ---- 3. bucket keys: the position's queue round and finish group
@@ -304,7 +335,7 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
     k.IA[i] = a;
     uint32_t rep = 0;
     if (P.reps > 1) {
-      const uint32_t hop = (uint32_t)(i - item_off(k, t));
+      const uint32_t hop = k.ihop[i];
       rep = draw0(k.trace_begin + t, hop, 0x80000002u, k.k0, k.k1) % P.reps;
     }
     repb[j] = rep;
@@ -405,7 +436,11 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
                                              const MP *in, const MP *inc) {
-  for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+  // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
+  // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
+  // / position, so its runs still sum before the atomics
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t j0 = (gid() - lane) * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
     uint32_t row = kNone;
     unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
     auto flush = [&]() {
@@ -416,7 +451,7 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
       if (mw) atomicMax(tr + ISIM_DES_MAX_WAIT, mw);
       if (sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, sh);
     };
-    for (uint64_t j = j0; j < j0 + kQSpan && j < m; ++j) {
+    for (uint64_t j = j0 + lane; j < j0 + 64 * kQSpan && j < m; j += 64) {
       const uint32_t i = sid[j];
       const uint32_t r = rkb[j];
       const uint64_t hold = k.row_hold[r];
@@ -443,7 +478,11 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
 // statistics summed over a thread's run of one position (and one bucket for
 // the histogram) before the atomics
 __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
-  for (uint64_t j0 = gid() * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+  // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
+  // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
+  // / position, so its runs still sum before the atomics
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t j0 = (gid() - lane) * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
     uint32_t v_run = kNone, b_run = kNone;
     DesPos P{};
     DesItemPos p{};
@@ -463,7 +502,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
         if (n5) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P.slot, n5);
       }
     };
-    for (uint64_t j = j0; j < j0 + kQSpan && j < m; ++j) {
+    for (uint64_t j = j0 + lane; j < j0 + 64 * kQSpan && j < m; j += 64) {
       const uint32_t i = ids[j];
       const uint32_t v = k.ipos[i];
       if (v != v_run) {
@@ -513,9 +552,9 @@ __global__ void __launch_bounds__(kT) k_final(K k) {
   __syncthreads();
   unsigned long long sl = 0, sh = 0, se = 0, n5 = 0, mn = ~0ull, mx = 0;
   for (uint64_t t = gid(); t < k.n; t += nthreads()) {
-    const uint64_t root = item_off(k, t);
+    const uint64_t root = k.troot[t];
     const uint64_t L = k.IF[root] - k.A[t];
-    const uint32_t hops = (uint32_t)(k.tend[t] - root);
+    const uint32_t hops = (uint32_t)(k.tend[t] - item_off(k, t));
     const uint32_t s_e = k.terr[t];
     const uint32_t st = s_e >> 31, e = s_e & 0x7FFFFFFFu;
     if (k.records) {
@@ -730,6 +769,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       16,                                                      // the round's arrival range
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
+      M * 4, n * 4, M * 4, M * 8, 8, 8, M * 4,                 // ihop troot; epos erec (2 spare); inverse
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
@@ -783,7 +823,14 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
   uint32_t *d_soff = (uint32_t *)carve(parts[35]);
   uint64_t *d_row_hold = (uint64_t *)carve(parts[36]);
-  void *tmp = carve(parts[37]);
+  k.ihop = (uint32_t *)carve(parts[37]);
+  k.troot = (uint32_t *)carve(parts[38]);
+  k.epos = (uint32_t *)carve(parts[39]);
+  k.erec = (unsigned long long *)carve(parts[40]);
+  (void)carve(parts[41]);
+  (void)carve(parts[42]);
+  uint32_t *inv = (uint32_t *)carve(parts[43]);
+  void *tmp = carve(parts[44]);
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -792,6 +839,18 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       break;
     }
     prewalk(true);
+    // 2b. renumber position-major: ipos = the sorted keys, the rest gathered
+    hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, ids);
+    {
+      size_t tb0 = tmp_bytes;
+      if (rocprim::radix_sort_pairs(tmp, tb0, qk, k.ipos, ids, qids, (size_t)M, 0, 16, s) != hipSuccess) {
+        rc = fail("position sort");
+        break;
+      }
+    }
+    hipLaunchKernelGGL(k_perm_inv, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
+    hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
+    hipLaunchKernelGGL(k_roots, dim3(grid_for(n)), dim3(kT), 0, s, k, inv);
     // 3. buckets
     if (hipMemcpyAsync(d_row_hold, row_hold.data(), rows_n * 8, hipMemcpyHostToDevice, s) != hipSuccess) {
       rc = fail("hold table upload");
