@@ -176,28 +176,67 @@ struct EmitSink : CountSink {
   }
 };
 
+// One trace per lane; a lane whose trace has responded takes the next trace
+// id of its wave's batch of 64, the wave claiming batches from a global
+// counter as it runs dry (the kind-7 kernel's refill, tree.hip): the waves
+// stay full instead of waiting for their longest trace.
 template <int FR, bool SPILL, bool EMIT>
-__global__ void __launch_bounds__(kT) k_prewalk(K k) {
+__global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
   tw::Lane<FR, false, true, SPILL, true> L;
   if constexpr (SPILL) {
     L.sp = k.spill + gid();
     L.sp_stride = (uint32_t)nthreads();
   }
   const GNodes nodes{k.nodes};
-  for (uint64_t t = gid(); t < k.n; t += nthreads()) {
-    L.start(k.trace_begin + t);
-    if constexpr (EMIT) {
-      EmitSink s;
-      s.epos = k.epos;
-      s.erec = k.erec;
-      s.base = item_off(k, t);
-      s.t = (uint32_t)t;
-      while (!L.done) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
-      k.terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
-    } else {
-      CountSink s;
-      while (!L.done) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
-      k.cnt[t] = L.hops();
+  const uint32_t lane = threadIdx.x & 63u;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint64_t nxt = 0, lim = 0;
+  bool dry = false, active = false;
+  uint32_t t = 0;
+  EmitSink s;
+  s.epos = k.epos;
+  s.erec = k.erec;
+  s.base = 0;
+  s.t = 0;
+  CountSink cs;
+  while (true) {
+    if (active && L.done) {
+      if constexpr (EMIT) k.terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
+      else k.cnt[t] = L.hops();
+      active = false;
+    }
+    unsigned long long idle = __ballot(!active);
+    while (idle && !dry) {
+      if (nxt >= lim) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(work, 1ull);
+        b = __shfl(b, 0, 64);
+        if (b * 64 >= k.n) {
+          dry = true;
+          break;
+        }
+        nxt = b * 64;
+        lim = nxt + 64 < k.n ? nxt + 64 : k.n;
+      }
+      const uint32_t rank = (uint32_t)__popcll(idle & lt);
+      const bool take = ((idle >> lane) & 1ull) && rank < lim - nxt;
+      if (take) {
+        t = (uint32_t)(nxt + rank);
+        active = true;
+        L.start(k.trace_begin + t);
+        if constexpr (EMIT) {
+          s.base = item_off(k, t);
+          s.t = t;
+        }
+      }
+      const unsigned long long took = __ballot(take);
+      nxt += (uint64_t)__popcll(took);
+      idle &= ~took;
+    }
+    if (!__ballot(active)) break;
+    if (active && !L.done) {
+      if constexpr (EMIT) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
+      else L.step(nodes, k.ext, k.tstep, cs, k.k0, k.k1);
     }
   }
 }
@@ -435,7 +474,12 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 // thread's span are summed before the atomics)
 constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
-                                             const MP *in, const MP *inc) {
+                                             const MP *in, const MP *inc, unsigned long long *mm) {
+  // the next round's arrival range starts empty (its k_qarr runs after this kernel)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
+    atomicExch(mm, ~0ull);
+    atomicExch(mm + 1, 0ull);
+  }
   // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
   // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
   // / position, so its runs still sum before the atomics
@@ -636,14 +680,14 @@ size_t scan_u64_bytes(uint64_t n) {
                                 rocprim::plus<uint64_t>());
   return b;
 }
-constexpr uint32_t kPrewalkBlocks = 2048;  // pre-walk grid (one trace per thread per pass)
+constexpr uint32_t kPrewalkBlocks = 2048;  // pre-walk grid (waves refill from a global batch counter)
 constexpr uint32_t kMaxPasses = 256;       // fixed-point passes of a cyclic schedule (des.hip)
 
 }  // namespace
 
 // per trace: gaps, arrivals, hops, item ends (u64), status_err (u32), scan temp
 uint64_t des_items_workspace_bytes(uint64_t n) {
-  return 4 * al256(n * 8) + al256(n * 4) + al256(scan_u64_bytes(n)) + 256;
+  return 4 * al256(n * 8) + al256(n * 4) + al256(16) + al256(scan_u64_bytes(n)) + 256;
 }
 
 int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
@@ -670,6 +714,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.cnt = (uint64_t *)take(n * 8);
   k.tend = (uint64_t *)take(n * 8);
   k.terr = (uint32_t *)take(n * 4);
+  // the refill counters of the two pre-walks
+  unsigned long long *work = (unsigned long long *)take(16);
   const size_t scan_bytes = scan_u64_bytes(n);
   void *scan_tmp = take(scan_bytes);
   k.stats = (unsigned long long *)L.d_stats;
@@ -709,17 +755,19 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   }
   k.spill = spill_buf;
   auto prewalk = [&](bool emit) {
+    unsigned long long *w = work + (emit ? 1 : 0);
     if (spill) {
-      if (emit) hipLaunchKernelGGL((k_prewalk<8, true, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
-      else hipLaunchKernelGGL((k_prewalk<8, true, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      if (emit) hipLaunchKernelGGL((k_prewalk<8, true, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      else hipLaunchKernelGGL((k_prewalk<8, true, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
     } else if (fr > 8) {
-      if (emit) hipLaunchKernelGGL((k_prewalk<16, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
-      else hipLaunchKernelGGL((k_prewalk<16, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      if (emit) hipLaunchKernelGGL((k_prewalk<16, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      else hipLaunchKernelGGL((k_prewalk<16, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
     } else {
-      if (emit) hipLaunchKernelGGL((k_prewalk<8, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
-      else hipLaunchKernelGGL((k_prewalk<8, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k);
+      if (emit) hipLaunchKernelGGL((k_prewalk<8, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      else hipLaunchKernelGGL((k_prewalk<8, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
     }
   };
+  if (hipMemsetAsync(work, 0, 16, s) != hipSuccess) return fail("memset");
   prewalk(false);
   b = scan_bytes;
   if (rocprim::inclusive_scan(scan_tmp, b, k.cnt, k.tend, (size_t)n, rocprim::plus<uint64_t>(), s) != hipSuccess)
@@ -834,7 +882,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
-    if (hipMemsetAsync(ovf, 0, 16, s) != hipSuccess) {
+    static const uint64_t mm_empty[2] = {~0ull, 0ull};
+    if (hipMemsetAsync(ovf, 0, 16, s) != hipSuccess ||
+        hipMemcpyAsync(mm, mm_empty, 16, hipMemcpyHostToDevice, s) != hipSuccess) {
       rc = fail("memset");
       break;
     }
@@ -920,10 +970,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
                            (uint64_t)(soff[r + 1] - soff[r]));
       const uint64_t m = qoff[r + 1] - qoff[r];
       if (m) {
-        if (hipMemsetAsync(mm, 0xFF, 8, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 8, s) != hipSuccess) {
-          rc = fail("memset");
-          break;
-        }
         hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
                            (unsigned long long *)mm);
         uint64_t hmm[2] = {0, 0};
@@ -966,7 +1012,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           break;
         }
         hipLaunchKernelGGL(k_qout, dim3(grid_for((m + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk, m, rk_b, sid,
-                           mp_in, mp_out);
+                           mp_in, mp_out, (unsigned long long *)mm);
       }
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
         const uint64_t mg = foff[gi + 1] - foff[gi];
