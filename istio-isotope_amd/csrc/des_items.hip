@@ -108,8 +108,8 @@ struct K {
   uint8_t *iown;
   uint32_t *troot;                 // per trace: its entry item (items are renumbered position-major)
   // the pre-walk's items in trace order, before the renumbering: position,
-  // and caller item | (trace | own error << 31) << 32
-  uint32_t *epos;
+  // and caller item | (trace | own error << 31) << 32; duration without contention
+  uint32_t *epos, *eT;
   unsigned long long *erec;
   uint64_t *IA, *IS, *IF, *acc, *bk;
   const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
@@ -125,6 +125,7 @@ struct K {
   // records no statistics and flags any stored value it changes
   uint32_t quiet;
   uint32_t *changed;
+  uint32_t first;                  // the first quiet pass: acc_prev holds contention-free relative maxima
 };
 
 // a quiet pass flags a change with ONE atomic per wave, and none once the
@@ -164,7 +165,7 @@ struct CountSink {
   __device__ __forceinline__ void resp(uint32_t, uint32_t, uint32_t, bool) {}
 };
 struct EmitSink : CountSink {
-  uint32_t *epos;
+  uint32_t *epos, *eT;
   unsigned long long *erec;
   uint64_t base;
   uint32_t t;
@@ -174,6 +175,7 @@ struct EmitSink : CountSink {
     const uint32_t par = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
     erec[i] = (unsigned long long)par | (unsigned long long)(t | (own ? 0x80000000u : 0u)) << 32;
   }
+  __device__ __forceinline__ void dur(uint32_t hop, uint32_t T) { eT[base + hop] = T; }
 };
 
 // One trace per lane; a lane whose trace has responded takes the next trace
@@ -195,6 +197,7 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
   uint32_t t = 0;
   EmitSink s;
   s.epos = k.epos;
+  s.eT = k.eT;
   s.erec = k.erec;
   s.base = 0;
   s.t = 0;
@@ -266,6 +269,26 @@ __global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm, co
     k.ipar[j] = par == kNone ? kNone : inv[par];
   }
 }
+// cyclic schedules: the first quiet pass starts its cut step begins from the
+// contention-free callee durations instead of zero (a lower bound of every
+// callee's finish: F(c) >= begin(step) + H(c) + T(c)), so the passes only
+// have to settle the queueing, not the whole chain of cut links.  Per
+// (caller, call step): max over its callees of H + T, relative to the
+// step's begin
+__global__ void __launch_bounds__(kT) k_relmax(K k, const uint32_t *perm, unsigned long long *rel) {
+  for (uint64_t j = gid(); j < k.M; j += nthreads()) {
+    const uint32_t par = k.ipar[j];
+    if (par == kNone) continue;
+    const uint32_t v = k.ipos[j];
+    const DesItemPos p = k.ip[v];
+    const DesItemPos pp = k.ip[k.ipos[par]];
+    if (pp.nsteps < 2) continue;  // no step begins: nothing reads it
+    // off = H, except in the first call step: pre + H relative to the start (the step begins at start + pre)
+    const uint64_t h = k.pos[v].off - (p.kstep == 0 ? k.steps[pp.bk_first].add : 0ull);
+    atomicMax(rel + (uint64_t)par * k.aw + p.kstep, (unsigned long long)(h + k.eT[perm[j]]));
+  }
+}
+
 __global__ void __launch_bounds__(kT) k_roots(K k, const uint32_t *inv) {
   for (uint64_t t = gid(); t < k.n; t += nthreads()) k.troot[t] = inv[item_off(k, t)];
 }
@@ -333,8 +356,12 @@ __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops
       v = k.IS[i];
     } else {
       v = k.bk[i * k.bw + (s - 1)] + st.smax;
-      // a cut step's callees finish later in the pass: their maxima of the previous one
-      const uint64_t c = ((sr & kDesStepCut) ? k.acc_prev : k.acc)[i * k.aw + (s - 1)];
+      // a cut step's callees finish later in the pass: their maxima of the
+      // previous one (the first pass: the contention-free lower bound)
+      uint64_t c;
+      if (!(sr & kDesStepCut)) c = k.acc[i * k.aw + (s - 1)];
+      else if (k.first) c = k.bk[i * k.bw + (s - 1)] + k.acc_prev[i * k.aw + (s - 1)];
+      else c = k.acc_prev[i * k.aw + (s - 1)];
       v = c > v ? c : v;
     }
     store_tracked(k, k.bk + i * k.bw + s, v + st.add);
@@ -817,7 +844,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       16,                                                      // the round's arrival range
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
-      M * 4, n * 4, M * 4, M * 8, 8, 8, M * 4,                 // ihop troot; epos erec (2 spare); inverse
+      M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
@@ -875,7 +902,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.troot = (uint32_t *)carve(parts[38]);
   k.epos = (uint32_t *)carve(parts[39]);
   k.erec = (unsigned long long *)carve(parts[40]);
-  (void)carve(parts[41]);
+  k.eT = (uint32_t *)carve(parts[41]);
   (void)carve(parts[42]);
   uint32_t *inv = (uint32_t *)carve(parts[43]);
   void *tmp = carve(parts[44]);
@@ -901,6 +928,13 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     hipLaunchKernelGGL(k_perm_inv, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
     hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
     hipLaunchKernelGGL(k_roots, dim3(grid_for(n)), dim3(kT), 0, s, k, inv);
+    if (pl.cyclic) {  // the first pass's cut step begins: contention-free callee maxima (k_relmax)
+      if (hipMemsetAsync(k.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
+        rc = fail("memset");
+        break;
+      }
+      hipLaunchKernelGGL(k_relmax, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, (unsigned long long *)k.acc);
+    }
     // 3. buckets
     if (hipMemcpyAsync(d_row_hold, row_hold.data(), rows_n * 8, hipMemcpyHostToDevice, s) != hipSuccess) {
       rc = fail("hold table upload");
@@ -1024,8 +1058,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     if (pl.cyclic) {
       if (hipMemsetAsync(k.IS, 0, M * 8, s) != hipSuccess || hipMemsetAsync(k.IF, 0, M * 8, s) != hipSuccess ||
           (k.bw && hipMemsetAsync(k.bk, 0, M * 8 * k.bw, s) != hipSuccess) ||
-          hipMemsetAsync(acc_b, 0, M * 8 * k.aw, s) != hipSuccess ||
-          hipMemsetAsync(k.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
+          hipMemsetAsync(acc_b, 0, M * 8 * k.aw, s) != hipSuccess) {
         rc = fail("memset");
         break;
       }
@@ -1040,6 +1073,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           rc = fail("memset");
           break;
         }
+        kq.first = p == 0 ? 1u : 0u;
         pass(kq);
         if (rc) break;
         if (hipMemcpyAsync(&changed, kq.changed, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -59,6 +59,7 @@ struct Sink {
   void call(uint32_t) {}
   void resp_leaf(uint32_t, bool) {}
   void resp(uint32_t, uint32_t, uint32_t, bool) {}
+  void dur(uint32_t, uint32_t) {}
   void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
     if (items->size() <= base + hop) items->resize(base + hop + 1);
     (*items)[base + hop] = Item{p, caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller), t,
