@@ -54,10 +54,12 @@ BENCH_BATCH = {
     # 2^18 22.3, 2^20 23.9 M traces/s)
     "c5": 1 << 20,
     # DES of dynamic walks on the item engine: config 3's
-    # graph at probability 50 (215 executed invocations per trace) and
-    # config 4's mesh with sleeps (a cyclic schedule: fixed-point passes)
-    "c5p": 1 << 18,
-    "c4d": 1 << 22,
+    # graph at probability 50 (215 executed invocations per trace; 2^18 /
+    # 2^19 / 2^20 traces per step 7.4 / 8.3 / 8.4 M traces/s, ~190 B per item)
+    # and config 4's mesh with sleeps (a cyclic schedule: fixed-point passes;
+    # 2^21 / 2^22 / 2^23: 4.3 / 6.2 / 7.4 M traces/s)
+    "c5p": 1 << 20,
+    "c4d": 1 << 23,
 }
 DES_CONFIGS = ("c5", "c5p", "c4d")
 
