@@ -58,7 +58,10 @@ BENCH_BATCH = {
     # 2^19 / 2^20 traces per step 7.4 / 8.3 / 8.4 M traces/s, ~190 B per item)
     # and config 4's mesh with sleeps (a cyclic schedule: fixed-point passes;
     # 2^21 / 2^22 / 2^23: 4.3 / 6.2 / 7.4 M traces/s)
-    "c5p": 1 << 20,
+    # (2^19: 21 GB of item arrays; a step right after another process freed
+    # ~170 GB — config 5's workspace — ran 4x slower at 2^20 while the driver
+    # still held that memory)
+    "c5p": 1 << 19,
     "c4d": 1 << 23,
 }
 DES_CONFIGS = ("c5", "c5p", "c4d")
