@@ -62,6 +62,23 @@ __constant__ uint64_t c_edges[32] = {
     120000000ull, 140000000ull, 160000000ull, 180000000ull, 200000000ull, 250000000ull, 300000000ull,
     350000000ull, 400000000ull, 450000000ull, 500000000ull};
 
+// The same bucket from a workgroup's LDS table by ceil(t / 1 ms) (every edge
+// is a whole number of milliseconds; entry 501 is +Inf): one ds_read_u8
+// instead of five dependent constant loads per item.
+constexpr uint32_t kLutEntries = 502;
+__device__ __forceinline__ void lut_init(uint8_t *lut) {
+  for (uint32_t i = threadIdx.x; i < kLutEntries; i += blockDim.x) {
+    uint32_t b = 0;
+    while (b < 32 && (uint64_t)i * 1000000ull > c_edges[b]) ++b;
+    lut[i] = (uint8_t)b;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ uint32_t lut_bucket(const uint8_t *lut, uint64_t t) {
+  const uint64_t c = t < 500000001ull ? t : 500000001ull;
+  return lut[(uint32_t)((c + 999999ull) / 1000000ull)];
+}
+
 __device__ __forceinline__ uint32_t prom_bucket(uint64_t t) {
   uint32_t lo = 0, hi = 32;
   while (lo < hi) {
@@ -549,6 +566,8 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
 // statistics summed over a thread's run of one position (and one bucket for
 // the histogram) before the atomics
 __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
+  __shared__ uint8_t lut[kLutEntries];
+  if (!k.quiet) lut_init(lut);
   // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
   // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
   // / position, so its runs still sum before the atomics
@@ -599,7 +618,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       if (k.quiet) continue;
       const uint32_t own = k.iown[i];
       const uint64_t dur = F - k.IA[i];
-      const uint32_t b = own * ISIM_N_PROM + prom_bucket(dur);
+      const uint32_t b = own * ISIM_N_PROM + lut_bucket(lut, dur);
       if (b != b_run) {
         flush_bucket();
         b_run = b;
