@@ -143,6 +143,7 @@ struct K {
   uint32_t quiet;
   uint32_t *changed;
   uint32_t first;                  // the first quiet pass: acc_prev holds contention-free relative maxima
+  uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
 };
 
 // a quiet pass flags a change with ONE atomic per wave, and none once the
@@ -567,18 +568,34 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
 // the histogram) before the atomics
 __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
   __shared__ uint8_t lut[kLutEntries];
+  // the duration histogram of the chunk's first row (a chunk of 4,096 sorted
+  // items is mostly one position): LDS atomics, one global add per bucket
+  __shared__ uint32_t hist[2 * ISIM_N_PROM];
+  __shared__ uint32_t s_row;
   if (!k.quiet) lut_init(lut);
-  // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
-  // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
-  // / position, so its runs still sum before the atomics
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t j0 = (gid() - lane) * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+  // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
+  // count: its barriers), a wave 64 x kQSpan of them, lane l the items
+  // l, l + 64, ...: coalesced loads, and a lane's items mostly share a
+  // position, so its runs sum before the atomics
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  constexpr uint64_t kChunk = (uint64_t)kT * kQSpan;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < m; c0 += (uint64_t)gridDim.x * kChunk) {
+    if (!k.quiet) {
+      for (uint32_t x = threadIdx.x; x < 2 * ISIM_N_PROM; x += kT) hist[x] = 0;
+      if (threadIdx.x == 0) s_row = k.pos[k.ipos[ids[c0]]].row;
+      __syncthreads();
+    }
+    const uint32_t hrow = k.quiet ? kNone : s_row;
+    const uint64_t j0 = c0 + (uint64_t)wave * 64 * kQSpan;
     uint32_t v_run = kNone, b_run = kNone;
     DesPos P{};
     DesItemPos p{};
     unsigned long long n = 0, n5 = 0, d0 = 0, d1 = 0, nb = 0;
     auto flush_bucket = [&]() {
-      if (!k.quiet && nb) atomicAdd(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS + b_run, nb);
+      if (!k.quiet && nb) {
+        if (P.row == hrow) atomicAdd(&hist[b_run], (uint32_t)nb);
+        else atomicAdd(k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS + b_run, nb);
+      }
       nb = 0;
     };
     auto flush = [&]() {
@@ -614,7 +631,8 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       }
       store_tracked(k, k.IF + i, F);
       const uint32_t par = k.ipar[i];
-      if (par != kNone) atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
+      if (par != kNone && !k.no_acc)
+        atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
       if (k.quiet) continue;
       const uint32_t own = k.iown[i];
       const uint64_t dur = F - k.IA[i];
@@ -630,6 +648,12 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       else d0 += dur;
     }
     flush();
+    if (!k.quiet) {
+      __syncthreads();
+      for (uint32_t x = threadIdx.x; x < 2 * ISIM_N_PROM; x += kT)
+        if (hist[x]) atomicAdd(k.table + (uint64_t)hrow * ISIM_DES_ROW_WORDS + x, (unsigned long long)hist[x]);
+      __syncthreads();  // hist and s_row are reset for the next chunk
+    }
   }
 }
 
@@ -773,6 +797,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.k0 = (uint32_t)L.seed;
   k.k1 = (uint32_t)(L.seed >> 32);
   k.n_slots = L.n_slots;
+  k.no_acc = std::getenv("ISIM_DES_ITEMS_NO_ACC") != nullptr;
   uint32_t max_reps = 1, max_row = 0;
   for (const DesPos &q : pl.pos) {
     max_reps = std::max(max_reps, q.reps);
@@ -1070,7 +1095,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
         const uint64_t mg = foff[gi + 1] - foff[gi];
         if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for((mg + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk,
-                                   fids + foff[gi], mg);
+                                   fids + foff[gi], mg);  // grid_for(ceil(mg / kQSpan)) blocks of kT: >= the chunks
       }
     }
     };
