@@ -114,6 +114,11 @@ struct DesPlan {
   std::vector<uint32_t> step_round;  // [steps]: the round of each BK op | kDesStepCut
   uint32_t item_acc = 1;             // per item: callee finish maxima, one per call step (>= 1)
   uint32_t item_bk = 0;              // per item: BK slots (the most call steps of a multi-step script; 0: none)
+  // per round: every position queued in it needs no sort — its service has
+  // no other position and one replica and its arrivals come in trace order
+  // (the static engine's fast-path condition), or no hold (start = arrival):
+  // the round scans its items in their (position, trace) order directly
+  std::vector<uint8_t> round_nosort;
   std::vector<DesPos> pos;           // hop order (position 0 = the entry)
   std::vector<DesPosExt> ext;        // [n_pos]
   std::vector<uint32_t> child;       // children lists (positions, call-step order)

@@ -480,6 +480,24 @@ __global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *
   }
 }
 
+// a round whose positions need no sort (DesPlan::round_nosort): its items in
+// their (position, trace) order are each position's FIFO already; the
+// segment key is the position (two positions of one zero-hold service stay
+// two segments)
+__global__ void __launch_bounds__(kT) k_pairs0(K k, const uint32_t *ids, uint64_t m, uint32_t *segk, uint32_t *rowk,
+                                               MP *mp, uint32_t *sid) {
+  for (uint64_t j = gid(); j < m; j += nthreads()) {
+    const uint32_t i = ids[j];
+    const uint32_t v = k.ipos[i];
+    const uint32_t row = k.pos[v].row;
+    const uint64_t hold = k.row_hold[row];
+    segk[j] = v;
+    rowk[j] = row;
+    mp[j] = MP{hold, k.IA[i] + hold};
+    sid[j] = i;
+  }
+}
+
 // TWO stable sorts otherwise: replica | arrival - amin first, then the row
 __global__ void __launch_bounds__(kT) k_qkey2(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
                                               uint64_t amin, uint32_t rb, uint64_t *key, uint32_t *val,
@@ -1050,14 +1068,19 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       if (m) {
         hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
                            (unsigned long long *)mm);
+        const bool nosort = pl.round_nosort[r] && !two_sorts;
         uint64_t hmm[2] = {0, 0};
-        if (hipMemcpyAsync(hmm, mm, 16, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        if (!nosort && (hipMemcpyAsync(hmm, mm, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                        hipStreamSynchronize(s) != hipSuccess)) {
           rc = fail("arrival range read-back");
           break;
         }
         const uint32_t ab = bits_for(hmm[1] - hmm[0]);
         tb = tmp_bytes;
-        if (!two_sorts && row_bits + rep_bits + ab <= 64) {
+        if (nosort) {
+          hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b, mp_in,
+                             sid);
+        } else if (!two_sorts && row_bits + rep_bits + ab <= 64) {
           hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
                              ab, key_a, val_a);
           if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, row_bits + rep_bits + ab,

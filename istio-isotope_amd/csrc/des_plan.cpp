@@ -571,6 +571,13 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
     }
     for (uint32_t gi = 0; gi + 1 < out.fin_off.size(); ++gi)
       for (uint32_t j = out.fin_off[gi]; j < out.fin_off[gi + 1]; ++j) out.item_pos[out.fin_pos[j]].fgroup = gi;
+    out.round_nosort.assign(R, 1);
+    for (uint32_t v = 0; v < np; ++v) {
+      const DesPos &q = out.pos[v];
+      const bool free = q.hold == 0 ||
+                        (svc_pos[pos_svc[v]].size() == 1 && q.reps == 1 && arr_sorted[v]);
+      if (!free) out.round_nosort[rnd[Q(v)]] = 0;
+    }
     out.step_round.resize(nb);
     for (uint32_t b = 0; b < nb; ++b) out.step_round[b] = rnd[Ab(b)] | (step_cut[b] ? kDesStepCut : 0u);
   }
