@@ -538,20 +538,40 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
                                              const MP *in, const MP *inc, unsigned long long *mm) {
+  // the chunk's first row's queue figures in LDS (a chunk of 4,096 items is
+  // mostly one row: one global atomic per figure and chunk, not per lane run)
+  __shared__ unsigned long long s_n, s_sw, s_mw, s_sh;
+  __shared__ uint32_t s_row;
   // the next round's arrival range starts empty (its k_qarr runs after this kernel)
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
     atomicExch(mm, ~0ull);
     atomicExch(mm + 1, 0ull);
   }
-  // a wave takes 64 x kQSpan consecutive sorted items, lane l the items
-  // l, l + 64, ...: coalesced loads, and a lane's items mostly share a row
-  // / position, so its runs still sum before the atomics
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t j0 = (gid() - lane) * kQSpan; j0 < m; j0 += nthreads() * kQSpan) {
+  // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
+  // count: its barriers), a wave 64 x kQSpan, lane l the items l, l + 64, ...
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  constexpr uint64_t kChunk = (uint64_t)kT * kQSpan;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < m; c0 += (uint64_t)gridDim.x * kChunk) {
+    if (!k.quiet) {
+      if (threadIdx.x == 0) {
+        s_n = s_sw = s_mw = s_sh = 0;
+        s_row = rkb[c0];
+      }
+      __syncthreads();
+    }
+    const uint32_t hrow = k.quiet ? kNone : s_row;
+    const uint64_t j0 = c0 + (uint64_t)wave * 64 * kQSpan;
     uint32_t row = kNone;
     unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
     auto flush = [&]() {
       if (row == kNone || !n) return;
+      if (row == hrow) {
+        atomicAdd(&s_n, n);
+        if (sw) atomicAdd(&s_sw, sw);
+        if (mw) atomicMax(&s_mw, mw);
+        if (sh) atomicAdd(&s_sh, sh);
+        return;
+      }
       unsigned long long *tr = k.table + (uint64_t)row * ISIM_DES_ROW_WORDS;
       atomicAdd(tr + ISIM_DES_COUNT, n);
       if (sw) atomicAdd(tr + ISIM_DES_SUM_WAIT, sw);
@@ -576,7 +596,18 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
       mw = w > mw ? w : mw;
       sh += hold;
     }
-    if (!k.quiet) flush();
+    if (!k.quiet) {
+      flush();
+      __syncthreads();
+      if (threadIdx.x == 0 && s_n) {
+        unsigned long long *tr = k.table + (uint64_t)hrow * ISIM_DES_ROW_WORDS;
+        atomicAdd(tr + ISIM_DES_COUNT, s_n);
+        if (s_sw) atomicAdd(tr + ISIM_DES_SUM_WAIT, s_sw);
+        if (s_mw) atomicMax(tr + ISIM_DES_MAX_WAIT, s_mw);
+        if (s_sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, s_sh);
+      }
+      __syncthreads();  // the LDS figures are reset for the next chunk
+    }
   }
 }
 
@@ -589,7 +620,9 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
   // the duration histogram of the chunk's first row (a chunk of 4,096 sorted
   // items is mostly one position): LDS atomics, one global add per bucket
   __shared__ uint32_t hist[2 * ISIM_N_PROM];
-  __shared__ uint32_t s_row;
+  __shared__ uint32_t s_row, s_pos;
+  // and the chunk's first position's duration sums and site counts
+  __shared__ unsigned long long f_d0, f_d1, f_n, f_n5;
   if (!k.quiet) lut_init(lut);
   // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
   // count: its barriers), a wave 64 x kQSpan of them, lane l the items
@@ -600,10 +633,14 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
   for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < m; c0 += (uint64_t)gridDim.x * kChunk) {
     if (!k.quiet) {
       for (uint32_t x = threadIdx.x; x < 2 * ISIM_N_PROM; x += kT) hist[x] = 0;
-      if (threadIdx.x == 0) s_row = k.pos[k.ipos[ids[c0]]].row;
+      if (threadIdx.x == 0) {
+        s_pos = k.ipos[ids[c0]];
+        s_row = k.pos[s_pos].row;
+        f_d0 = f_d1 = f_n = f_n5 = 0;
+      }
       __syncthreads();
     }
-    const uint32_t hrow = k.quiet ? kNone : s_row;
+    const uint32_t hrow = k.quiet ? kNone : s_row, hpos = k.quiet ? kNone : s_pos;
     const uint64_t j0 = c0 + (uint64_t)wave * 64 * kQSpan;
     uint32_t v_run = kNone, b_run = kNone;
     DesPos P{};
@@ -619,6 +656,13 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
     auto flush = [&]() {
       flush_bucket();
       if (k.quiet || v_run == kNone || !n) return;
+      if (v_run == hpos) {
+        atomicAdd(&f_n, n);
+        if (n5) atomicAdd(&f_n5, n5);
+        if (d0) atomicAdd(&f_d0, d0);
+        if (d1) atomicAdd(&f_d1, d1);
+        return;
+      }
       unsigned long long *tr = k.table + (uint64_t)P.row * ISIM_DES_ROW_WORDS;
       if (d0) atomicAdd(tr + 2 * ISIM_N_PROM, d0);
       if (d1) atomicAdd(tr + 2 * ISIM_N_PROM + 1, d1);
@@ -670,7 +714,17 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       __syncthreads();
       for (uint32_t x = threadIdx.x; x < 2 * ISIM_N_PROM; x += kT)
         if (hist[x]) atomicAdd(k.table + (uint64_t)hrow * ISIM_DES_ROW_WORDS + x, (unsigned long long)hist[x]);
-      __syncthreads();  // hist and s_row are reset for the next chunk
+      if (threadIdx.x == 0 && f_n) {
+        unsigned long long *tr = k.table + (uint64_t)hrow * ISIM_DES_ROW_WORDS;
+        if (f_d0) atomicAdd(tr + 2 * ISIM_N_PROM, f_d0);
+        if (f_d1) atomicAdd(tr + 2 * ISIM_N_PROM + 1, f_d1);
+        const DesPos P0 = k.pos[hpos];
+        if (P0.parent != kDesNoParent) {
+          atomicAdd(k.stats + ISIM_ST_SITES + P0.slot, f_n);
+          if (f_n5) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P0.slot, f_n5);
+        }
+      }
+      __syncthreads();  // the LDS figures are reset for the next chunk
     }
   }
 }
