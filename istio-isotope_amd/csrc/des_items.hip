@@ -202,7 +202,10 @@ struct EmitSink : CountSink {
 // stay full instead of waiting for their longest trace.
 template <int FR, bool SPILL, bool EMIT>
 __global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
-  tw::Lane<FR, false, true, SPILL, true> L;
+  // no error draws in the walk (DRAW = false): in mode A an invocation's own
+  // error changes no skip, so the walks only need the skip residues; the
+  // errors are drawn per item afterwards (k_own), fully parallel
+  tw::Lane<FR, false, true, SPILL, false> L;
   if constexpr (SPILL) {
     L.sp = k.spill + gid();
     L.sp_stride = (uint32_t)nthreads();
@@ -222,8 +225,7 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
   CountSink cs;
   while (true) {
     if (active && L.done) {
-      if constexpr (EMIT) k.terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
-      else k.cnt[t] = L.hops();
+      if constexpr (!EMIT) k.cnt[t] = L.hops();
       active = false;
     }
     unsigned long long idle = __ballot(!active);
@@ -260,6 +262,31 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
       else L.step(nodes, k.ext, k.tstep, cs, k.k0, k.k1);
     }
   }
+}
+
+// ---- 2a. own errors (RecordRequestReceived's status in mode A): word
+// (hop & 3) of Philox (t, hop >> 2, 0, 0) against the callee's threshold, as
+// the walk draws it (tree_walk.h own_error); the trace's 500 count by atomics
+// (errors are rare), its entry status below
+__global__ void __launch_bounds__(kT) k_own(K k) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    const unsigned long long r = k.erec[i];
+    const uint32_t t = (uint32_t)(r >> 32) & 0x7FFFFFFFu;
+    const uint32_t hop = (uint32_t)(i - item_off(k, t));
+    const DesPos P = k.pos[k.epos[i]];
+    bool own = (P.flags & kDesFlagAlways) != 0;
+    if (!own && P.thr) {
+      uint32_t a = (uint32_t)(k.trace_begin + t), b = (uint32_t)((k.trace_begin + t) >> 32), c = hop >> 2, d = 0;
+      tw::philox10(a, b, c, d, k.k0, k.k1);
+      own = tw::word4(hop & 3u, a, b, c, d) < P.thr;
+    }
+    k.erec[i] = (r & ~(1ull << 63)) | ((unsigned long long)own << 63);
+    if (own) atomicAdd(k.terr + t, 1u);
+  }
+}
+__global__ void __launch_bounds__(kT) k_root500(K k) {
+  for (uint64_t t = gid(); t < k.n; t += nthreads())
+    if (k.erec[item_off(k, t)] >> 63) k.terr[t] |= 0x80000000u;
 }
 
 // ---- 2b. renumbering: items in (position, trace) order (a stable radix
@@ -1032,6 +1059,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       break;
     }
     prewalk(true);
+    if (hipMemsetAsync(k.terr, 0, n * 4, s) != hipSuccess) {
+      rc = fail("memset");
+      break;
+    }
+    hipLaunchKernelGGL(k_own, dim3(grid_for(M)), dim3(kT), 0, s, k);
+    hipLaunchKernelGGL(k_root500, dim3(grid_for(n)), dim3(kT), 0, s, k);
     // 2b. renumber position-major: ipos = the sorted keys, the rest gathered
     hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, ids);
     {
