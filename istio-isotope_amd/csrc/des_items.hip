@@ -144,6 +144,7 @@ struct K {
   uint32_t *changed;
   uint32_t first;                  // the first quiet pass: acc_prev holds contention-free relative maxima
   uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
+  uint32_t count_changes;          // ISIM_DES_DEBUG: changed[1] counts the values a quiet pass changed
 };
 
 // a quiet pass flags a change with ONE atomic per wave, and none once the
@@ -152,9 +153,12 @@ struct K {
 __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v) {
   if (k.changed) {
     const bool diff = *p != v;
-    if (__ballot(diff) && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)__ballot(diff)) - 1u &&
-        __hip_atomic_load(k.changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-      atomicOr(k.changed, 1u);
+    const unsigned long long m = __ballot(diff);
+    if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1u) {
+      // ISIM_DES_DEBUG: count the changed values (one atomic per wave)
+      if (k.count_changes) atomicAdd(k.changed + 1, (uint32_t)__popcll(m));
+      if (__hip_atomic_load(k.changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(k.changed, 1u);
+    }
   }
   *p = v;
 }
@@ -897,6 +901,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.k1 = (uint32_t)(L.seed >> 32);
   k.n_slots = L.n_slots;
   k.no_acc = std::getenv("ISIM_DES_ITEMS_NO_ACC") != nullptr;
+  const bool debug = std::getenv("ISIM_DES_DEBUG") != nullptr;
+  k.count_changes = debug ? 1u : 0u;
   uint32_t max_reps = 1, max_row = 0;
   for (const DesPos &q : pl.pos) {
     max_reps = std::max(max_reps, q.reps);
@@ -984,7 +990,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 16,        // qoff foff; ovf: key overflow, no fixed point,
                                                                // changed, multi-step items
-      16,                                                      // the round's arrival range
+      32,                                                      // the round's arrival range; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
       M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
@@ -1037,6 +1043,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *d_qoff = (uint32_t *)carve(parts[29]), *d_foff = (uint32_t *)carve(parts[30]);
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
   uint64_t *mm = (uint64_t *)carve(parts[32]);
+  uint32_t *chg = (uint32_t *)mm + 4;  // [0] a quiet pass changed a value, [1] how many (debug); after mm's 2 words
   uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
   unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
   uint32_t *d_soff = (uint32_t *)carve(parts[35]);
@@ -1219,23 +1226,24 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       K kq = k;
       kq.quiet = 1;
       kq.acc_prev = acc_b;
-      kq.changed = ovf + 2;
+      kq.changed = chg;
       uint32_t p = 0;
       for (; p < kMaxPasses && !rc; ++p) {
-        uint32_t changed = 1;
-        if (hipMemsetAsync(kq.changed, 0, 4, s) != hipSuccess) {
+        uint32_t changed[2] = {1, 0};
+        if (hipMemsetAsync(kq.changed, 0, 8, s) != hipSuccess) {
           rc = fail("memset");
           break;
         }
         kq.first = p == 0 ? 1u : 0u;
         pass(kq);
         if (rc) break;
-        if (hipMemcpyAsync(&changed, kq.changed, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        if (hipMemcpyAsync(changed, kq.changed, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
           rc = fail("fixed-point read-back");
           break;
         }
-        if (!changed) break;
+        if (debug) std::fprintf(stderr, "isim des items: pass %u changed %u values\n", p + 1, changed[1]);
+        if (!changed[0]) break;
       }
       if (std::getenv("ISIM_DES_DEBUG")) std::fprintf(stderr, "isim des items: cyclic schedule, %u passes\n", p + 1);
       if (!rc && p == kMaxPasses) {
