@@ -8,22 +8,30 @@
 // is the ITEM — one executed invocation — and the work is proportional to
 // the items, not the positions:
 //   1. arrivals    A_t = prefix sum of the exponential gaps (des.h Q24 log)
-//   2. pre-walk    the lane tree walk (tree_walk.h Lane, one trace per
-//                  thread) counts each trace's executed invocations, a scan
-//                  gives the item offsets, a second walk writes each item's
-//                  position, caller item and own error (hop id = item index
-//                  within the trace: executed invocations in preorder)
+//   2. pre-walk    the lane tree walk (tree_walk.h Lane, one trace per lane,
+//                  waves refilling from a batch counter, no error draws)
+//                  counts each trace's executed invocations, a scan gives
+//                  the item offsets, a second walk writes each item's
+//                  position, caller and contention-free duration (hop id =
+//                  item index within the trace: executed invocations in
+//                  preorder); the own errors are drawn per item afterwards;
+//                  then the items are RENUMBERED position-major (a stable
+//                  radix sort by position), so every later pass reads them
+//                  nearly in sequence
 //   3. buckets     the items sorted (stable radix sort) by their position's
-//                  queue round and by its finish group (des_plan.cpp's
-//                  schedule over the tree's positions)
-//   4. rounds      step begins (BK per item and call step), queues (the
-//                  round's items sorted by (service, replica, arrival) — two
-//                  stable radix sorts, ties in (trace, hop) order as the
-//                  oracle's event heap pops them — and one segmented
-//                  max-plus scan: S = max(a, S_prev + hold)), finishes
-//                  (deepest group first: F from the start or last BK and the
-//                  callees' maxima, which each callee folds into its caller's
-//                  per-step slot with a 64-bit atomic max)
+//                  queue round and by (finish group, position) (des_plan.cpp's
+//                  schedule over the tree's positions); step-begin ops by round
+//   4. rounds      step begins (BK per item and call step), queues (a round
+//                  whose positions arrive in trace order with one replica is
+//                  already in FIFO order; otherwise ONE stable radix sort by
+//                  row | replica | arrival — two when the bits do not fit —,
+//                  ties in (trace, hop) order as the oracle's event heap pops
+//                  them — then one segmented max-plus scan: S = max(a,
+//                  S_prev + hold)), finishes (deepest group first: F from the
+//                  start or last BK and the callees' maxima, which each callee
+//                  folds into its caller's per-step slot with a 64-bit atomic
+//                  max); statistics summed in LDS per 4,096-item chunk; a
+//                  cyclic schedule runs quiet passes to its fixed point first
 //   5. finalize    records and latency statistics per trace.
 // Reference anchors: as des.hip (handler.go:37-79, executable.go:94-179,
 // svc/service.go:30-31, prometheus/handler.go:87-106).  Parity: bit-exact
