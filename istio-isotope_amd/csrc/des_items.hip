@@ -438,9 +438,18 @@ struct MPThen {
 };
 
 // ---- 4b. queues of round r: each item's arrival and replica, and the
-// round's arrival range (one 64-bit atomic min / max per wave)
+// round's arrival range (mm[0..1]: one 64-bit atomic min / max per
+// workgroup); in a quiet pass of a cyclic schedule mm[2] flags an arrival
+// that differs from the previous pass's (none: the round's queues are as
+// they were and the pass skips them).  The range words alternate between two
+// slots by launch; this launch empties the other slot for the next one.
 __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t m, uint32_t *repb,
-                                             unsigned long long *mm) {
+                                             unsigned long long *mm, unsigned long long *mm_next) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
+    atomicExch(mm_next, ~0ull);
+    atomicExch(mm_next + 1, 0ull);
+    atomicExch(mm_next + 2, 0ull);
+  }
   unsigned long long lo = ~0ull, hi = 0;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
@@ -454,6 +463,12 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
     } else {
       const uint32_t ks = k.ip[v].kstep;
       a = (ks == 0 ? k.IS[par] : k.bk[(uint64_t)par * k.bw + ks]) + P.off;
+    }
+    if (k.changed) {
+      const unsigned long long dm = __ballot(k.IA[i] != a);
+      if (dm && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)dm) - 1u &&
+          __hip_atomic_load(mm + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull)
+        atomicOr(mm + 2, 1ull);
     }
     k.IA[i] = a;
     uint32_t rep = 0;
@@ -576,16 +591,11 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 // thread's span are summed before the atomics)
 constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
-                                             const MP *in, const MP *inc, unsigned long long *mm) {
+                                             const MP *in, const MP *inc) {
   // the chunk's first row's queue figures in LDS (a chunk of 4,096 items is
   // mostly one row: one global atomic per figure and chunk, not per lane run)
   __shared__ unsigned long long s_n, s_sw, s_mw, s_sh;
   __shared__ uint32_t s_row;
-  // the next round's arrival range starts empty (its k_qarr runs after this kernel)
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
-    atomicExch(mm, ~0ull);
-    atomicExch(mm + 1, 0ull);
-  }
   // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
   // count: its barriers), a wave 64 x kQSpan, lane l the items l, l + 64, ...
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -998,7 +1008,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 16,        // qoff foff; ovf: key overflow, no fixed point,
                                                                // changed, multi-step items
-      32,                                                      // the round's arrival range; change flag, count
+      96,                                                      // two arrival-range slots; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
       M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
@@ -1051,7 +1061,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *d_qoff = (uint32_t *)carve(parts[29]), *d_foff = (uint32_t *)carve(parts[30]);
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
   uint64_t *mm = (uint64_t *)carve(parts[32]);
-  uint32_t *chg = (uint32_t *)mm + 4;  // [0] a quiet pass changed a value, [1] how many (debug); after mm's 2 words
+  uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] how many (debug)
   uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
   unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
   uint32_t *d_soff = (uint32_t *)carve(parts[35]);
@@ -1067,9 +1077,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
-    static const uint64_t mm_empty[2] = {~0ull, 0ull};
+    static const uint64_t mm_empty[8] = {~0ull, 0ull, 0ull, 0ull, ~0ull, 0ull, 0ull, 0ull};
     if (hipMemsetAsync(ovf, 0, 16, s) != hipSuccess ||
-        hipMemcpyAsync(mm, mm_empty, 16, hipMemcpyHostToDevice, s) != hipSuccess) {
+        hipMemcpyAsync(mm, mm_empty, 64, hipMemcpyHostToDevice, s) != hipSuccess) {
       rc = fail("memset");
       break;
     }
@@ -1145,6 +1155,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     const uint32_t row_bits = bits_for(max_row);
     // A/B switch: always the two-sort queue path
     const bool two_sorts = std::getenv("ISIM_DES_ITEMS_TWO_SORTS") != nullptr;
+    // A/B switch: never skip an unchanged round
+    const bool no_skip = std::getenv("ISIM_DES_ITEMS_NO_SKIP") != nullptr;
     // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
     // every time: the iteration only raises values) until no stored value
     // changes, then the pass that records the statistics (des.hip des_launch)
@@ -1152,6 +1164,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     // a queue changes, so maxima are never carried over); a cut step begin
     // reads the previous pass's (the two buffers swap)
     uint64_t *acc_a = k.acc;
+    uint32_t qn = 0;       // k_qarr launches: the arrival-range slot alternates
+    uint64_t skipped = 0;  // queue rounds a quiet pass skipped (ISIM_DES_DEBUG)
     auto pass = [&](K &kk) {
     if (pl.cyclic) {
       std::swap(acc_a, acc_b);
@@ -1168,14 +1182,25 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
                            (uint64_t)(soff[r + 1] - soff[r]));
       const uint64_t m = qoff[r + 1] - qoff[r];
       if (m) {
+        uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
+        ++qn;
         hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
-                           (unsigned long long *)mm);
+                           (unsigned long long *)slot, (unsigned long long *)slot_next);
         const bool nosort = pl.round_nosort[r] && !two_sorts;
-        uint64_t hmm[2] = {0, 0};
-        if (!nosort && (hipMemcpyAsync(hmm, mm, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                        hipStreamSynchronize(s) != hipSuccess)) {
+        // a quiet pass after the first: a round whose arrivals all equal the
+        // previous pass's keeps its starts (its queues are skipped)
+        // (sort rounds only: they read the range back anyway; a sort-free
+        // round would pay a stream synchronisation for the check)
+        const bool may_skip = kk.quiet && !kk.first && !nosort && !no_skip;
+        uint64_t hmm[3] = {0, 0, 1};
+        if ((!nosort || may_skip) && (hipMemcpyAsync(hmm, slot, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                                      hipStreamSynchronize(s) != hipSuccess)) {
           rc = fail("arrival range read-back");
           break;
+        }
+        if (may_skip && !hmm[2]) {
+          ++skipped;
+          goto finishes;
         }
         const uint32_t ab = bits_for(hmm[1] - hmm[0]);
         tb = tmp_bytes;
@@ -1215,8 +1240,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           break;
         }
         hipLaunchKernelGGL(k_qout, dim3(grid_for((m + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk, m, rk_b, sid,
-                           mp_in, mp_out, (unsigned long long *)mm);
+                           mp_in, mp_out);
       }
+    finishes:
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
         const uint64_t mg = foff[gi + 1] - foff[gi];
         if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for((mg + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk,
@@ -1253,7 +1279,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         if (debug) std::fprintf(stderr, "isim des items: pass %u changed %u values\n", p + 1, changed[1]);
         if (!changed[0]) break;
       }
-      if (std::getenv("ISIM_DES_DEBUG")) std::fprintf(stderr, "isim des items: cyclic schedule, %u passes\n", p + 1);
+      if (debug)
+        std::fprintf(stderr, "isim des items: cyclic schedule, %u passes, %llu unchanged queue rounds skipped\n", p + 1,
+                     (unsigned long long)skipped);
       if (!rc && p == kMaxPasses) {
         static const uint32_t one = 1;
         if (hipMemcpyAsync(ovf + 1, &one, 4, hipMemcpyHostToDevice, s) != hipSuccess) rc = fail("flag");
