@@ -897,6 +897,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.d_tstep = st->d_des_tstep;
     L.tree_frames = h->prog.tree_frames;
     L.tree_flags = h->prog.tree_flags;
+    L.n_nodes = (uint32_t)h->prog.tree_nodes.size();
     L.workspace = d_workspace;
     L.d_stats = d_stats;
     L.d_table = d_des_table;

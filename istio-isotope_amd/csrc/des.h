@@ -216,7 +216,7 @@ struct DesItemsLaunch {
   const void *d_pos, *d_item_pos, *d_steps;  // DesPos[n_pos], DesItemPos[n_pos], DesStep[]
   const uint32_t *d_step_round;              // [steps]
   const void *d_nodes, *d_ext, *d_tstep;     // the lane tree walk's TreeNode/TreeExt/TreeStep
-  uint32_t tree_frames, tree_flags;
+  uint32_t tree_frames, tree_flags, n_nodes;
   void *workspace;
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;

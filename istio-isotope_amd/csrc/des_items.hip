@@ -122,6 +122,7 @@ struct K {
   const uint32_t *step_round;
   // tree (pre-walk)
   const unsigned long long *nodes;
+  uint32_t n_nodes;
   const TreeExt *ext;
   const TreeStep *tstep;
   uint32_t *spill;
@@ -212,17 +213,26 @@ struct EmitSink : CountSink {
 // id of its wave's batch of 64, the wave claiming batches from a global
 // counter as it runs dry (the kind-7 kernel's refill, tree.hip): the waves
 // stay full instead of waiting for their longest trace.
-template <int FR, bool SPILL, bool EMIT>
-__global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
+// the tree's nodes in LDS when they fit (one ds_read_b64 per visit instead of
+// an L2 round trip; kind 7's LdsNodes)
+struct LNodes {
+  const __attribute__((address_space(3))) unsigned long long *p;
+  __device__ __forceinline__ tw::NodeW load(uint32_t i) const {
+    const unsigned long long v = p[i];
+    return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
+  }
+};
+
+template <int FR, bool SPILL, bool EMIT, class Nodes>
+__device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *work, const Nodes &nodes) {
   // no error draws in the walk (DRAW = false): in mode A an invocation's own
   // error changes no skip, so the walks only need the skip residues; the
   // errors are drawn per item afterwards (k_own), fully parallel
   tw::Lane<FR, false, true, SPILL, false> L;
   if constexpr (SPILL) {
-    L.sp = k.spill + gid();
-    L.sp_stride = (uint32_t)nthreads();
+    L.sp = k.spill + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    L.sp_stride = gridDim.x * blockDim.x;
   }
-  const GNodes nodes{k.nodes};
   const uint32_t lane = threadIdx.x & 63u;
   const unsigned long long lt = (1ull << lane) - 1ull;
   uint64_t nxt = 0, lim = 0;
@@ -273,6 +283,18 @@ __global__ void __launch_bounds__(kT) k_prewalk(K k, unsigned long long *work) {
       if constexpr (EMIT) L.step(nodes, k.ext, k.tstep, s, k.k0, k.k1);
       else L.step(nodes, k.ext, k.tstep, cs, k.k0, k.k1);
     }
+  }
+}
+
+template <int FR, bool SPILL, bool EMIT, bool LDSN>
+__global__ void __launch_bounds__(LDSN ? 1024 : kT) k_prewalk(K k, unsigned long long *work) {
+  if constexpr (LDSN) {
+    extern __shared__ unsigned long long s_nodes[];
+    for (uint32_t i = threadIdx.x; i < k.n_nodes; i += blockDim.x) s_nodes[i] = k.nodes[i];
+    __syncthreads();
+    prewalk_body<FR, SPILL, EMIT>(k, work, LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
+  } else {
+    prewalk_body<FR, SPILL, EMIT>(k, work, GNodes{k.nodes});
   }
 }
 
@@ -948,17 +970,45 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     if (hipMallocAsync((void **)&spill_buf, words * 4, s) != hipSuccess) return fail("spill allocation");
   }
   k.spill = spill_buf;
+  // the nodes in LDS (1024-thread workgroups, one per CU at these register
+  // counts) when they fit in 96 KB; ISIM_DES_ITEMS_GLOBAL_NODES: always global
+  k.n_nodes = L.n_nodes;
+  const uint32_t lds_nodes = L.n_nodes * 8u;
+  const bool ldsn = lds_nodes <= 96u * 1024u && !std::getenv("ISIM_DES_ITEMS_GLOBAL_NODES");
+  auto launch = [&](auto kern, unsigned long long *w) {
+    if (ldsn) {
+      (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_nodes);
+      hipLaunchKernelGGL(kern, dim3(kPrewalkBlocks / 4), dim3(1024), lds_nodes, s, k, w);
+    } else {
+      hipLaunchKernelGGL(kern, dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+    }
+  };
   auto prewalk = [&](bool emit) {
     unsigned long long *w = work + (emit ? 1 : 0);
     if (spill) {
-      if (emit) hipLaunchKernelGGL((k_prewalk<8, true, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
-      else hipLaunchKernelGGL((k_prewalk<8, true, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      if (ldsn) {
+        if (emit) launch(k_prewalk<8, true, true, true>, w);
+        else launch(k_prewalk<8, true, false, true>, w);
+      } else {
+        if (emit) launch(k_prewalk<8, true, true, false>, w);
+        else launch(k_prewalk<8, true, false, false>, w);
+      }
     } else if (fr > 8) {
-      if (emit) hipLaunchKernelGGL((k_prewalk<16, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
-      else hipLaunchKernelGGL((k_prewalk<16, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      if (ldsn) {
+        if (emit) launch(k_prewalk<16, false, true, true>, w);
+        else launch(k_prewalk<16, false, false, true>, w);
+      } else {
+        if (emit) launch(k_prewalk<16, false, true, false>, w);
+        else launch(k_prewalk<16, false, false, false>, w);
+      }
     } else {
-      if (emit) hipLaunchKernelGGL((k_prewalk<8, false, true>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
-      else hipLaunchKernelGGL((k_prewalk<8, false, false>), dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
+      if (ldsn) {
+        if (emit) launch(k_prewalk<8, false, true, true>, w);
+        else launch(k_prewalk<8, false, false, true>, w);
+      } else {
+        if (emit) launch(k_prewalk<8, false, true, false>, w);
+        else launch(k_prewalk<8, false, false, false>, w);
+      }
     }
   };
   if (hipMemsetAsync(work, 0, 16, s) != hipSuccess) return fail("memset");
