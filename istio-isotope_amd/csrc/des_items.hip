@@ -376,19 +376,14 @@ __global__ void __launch_bounds__(kT) k_roots(K k, const uint32_t *inv) {
 // (finish groups keyed with the position below them, so a group's items come
 // position by position: k_fin sums runs), and the step-begin ops of the
 // multi-step items: (round, item << 16 | step), appended one atomic per wave
-__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *qk, uint32_t *fk, uint32_t *ids, uint32_t *sk,
-                                                    unsigned long long *sv, uint32_t *n_ops) {
+__global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *sk, unsigned long long *sv, uint32_t *n_ops) {
   const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t i0 = gid() - lane; i0 < k.M; i0 += nthreads()) {  // whole waves stay in the loop
     const uint64_t i = i0 + lane;
     uint32_t nst = 0;
     DesItemPos p{};
     if (i < k.M) {
-      const uint32_t v = k.ipos[i];
-      p = k.ip[v];
-      qk[i] = p.qround;
-      fk[i] = (p.fgroup << 16) | v;
-      ids[i] = (uint32_t)i;
+      p = k.ip[k.ipos[i]];
       nst = p.nsteps >= 2 ? p.nsteps : 0u;
     }
     // wave prefix sum of the op counts
@@ -417,6 +412,20 @@ __global__ void __launch_bounds__(kT) k_bounds(const uint32_t *keys, uint64_t m,
     const uint32_t lo = i == 0 ? 0u : (keys[i - 1] >> shift) + 1u;  // keys (keys[i-1], keys[i]] start here
     const uint32_t hi = i == m ? nb : (keys[i] >> shift);
     for (uint32_t b = lo; b <= hi && b <= nb; ++b) off[b] = (uint32_t)i;
+  }
+}
+
+// The rounds' and finish groups' item lists from the position-major ids: a
+// position's items are one contiguous range [poff[v], poff[v + 1]) in trace
+// order, so each list is its positions' ranges, concatenated in position
+// order (the host places them: qdst / fdst) — no sort of the items
+__global__ void __launch_bounds__(kT) k_scatter_ids(K k, const uint32_t *poff, const uint32_t *qdst,
+                                                    const uint32_t *fdst, uint32_t *qids, uint32_t *fids) {
+  for (uint64_t j = gid(); j < k.M; j += nthreads()) {
+    const uint32_t v = k.ipos[j];
+    const uint32_t rel = (uint32_t)j - poff[v];
+    qids[qdst[v] + rel] = (uint32_t)j;
+    fids[fdst[v] + rel] = (uint32_t)j;
   }
 }
 
@@ -1053,15 +1062,16 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
       pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops: rounds, (item, step)
-      M * 4, M * 4, M * 4, M * 4, M * 4, M * 4,                // qk fk ids qk2 qids fids (fk2 = qk)
+      M * 4, 4, M * 4, 4, M * 4, M * 4,                        // qk (spare) ids (spare) qids fids
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
-      (uint64_t)(R + 1) * 4, (uint64_t)(G + 1) * 4, 16,        // qoff foff; ovf: key overflow, no fixed point,
-                                                               // changed, multi-step items
+      4, 4, 16,                                                // (spare, spare); ovf: key overflow, no fixed
+                                                               // point, (unused), step-op count
       96,                                                      // two arrival-range slots; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
       M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
+      (uint64_t)(pl.pos.size() + 1) * 4, (uint64_t)pl.pos.size() * 4, (uint64_t)pl.pos.size() * 4,  // poff qdst fdst
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
@@ -1099,8 +1109,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint64_t *acc_b = (uint64_t *)carve(parts[9]);
   uint32_t *op_k = (uint32_t *)carve(parts[10]);
   unsigned long long *op_v = (unsigned long long *)carve(parts[11]);
-  uint32_t *qk = (uint32_t *)carve(parts[12]), *fk = (uint32_t *)carve(parts[13]);
-  uint32_t *ids = (uint32_t *)carve(parts[14]), *qk2 = (uint32_t *)carve(parts[15]);
+  uint32_t *qk = (uint32_t *)carve(parts[12]);
+  (void)carve(parts[13]);
+  uint32_t *ids = (uint32_t *)carve(parts[14]);
+  (void)carve(parts[15]);
   uint32_t *qids = (uint32_t *)carve(parts[16]), *fids = (uint32_t *)carve(parts[17]);
   uint64_t *key_a = (uint64_t *)carve(parts[18]), *key_b = (uint64_t *)carve(parts[19]);
   uint32_t *val_a = (uint32_t *)carve(parts[20]), *val_b = (uint32_t *)carve(parts[21]);
@@ -1108,7 +1120,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *rv_a = (uint32_t *)carve(parts[24]), *rv_b = (uint32_t *)carve(parts[25]);
   MP *mp_in = (MP *)carve(parts[26]), *mp_out = (MP *)carve(parts[27]);
   uint32_t *sid = (uint32_t *)carve(parts[28]);
-  uint32_t *d_qoff = (uint32_t *)carve(parts[29]), *d_foff = (uint32_t *)carve(parts[30]);
+  (void)carve(parts[29]);
+  (void)carve(parts[30]);
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
   uint64_t *mm = (uint64_t *)carve(parts[32]);
   uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] how many (debug)
@@ -1123,7 +1136,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.eT = (uint32_t *)carve(parts[41]);
   (void)carve(parts[42]);
   uint32_t *inv = (uint32_t *)carve(parts[43]);
-  void *tmp = carve(parts[44]);
+  uint32_t *d_poff = (uint32_t *)carve(parts[44]);
+  uint32_t *d_qdst = (uint32_t *)carve(parts[45]);
+  uint32_t *d_fdst = (uint32_t *)carve(parts[46]);
+  void *tmp = carve(parts[47]);
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -1165,42 +1181,57 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       break;
     }
     k.row_hold = d_row_hold;
-    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, fk, ids, op_k, op_v, ovf + 3);
-    size_t tb = tmp_bytes;
-    if (rocprim::radix_sort_pairs(tmp, tb, qk, qk2, ids, qids, (size_t)M, 0, bits_for(R), s) != hipSuccess) {
-      rc = fail("round sort");
-      break;
-    }
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk2, M, R, 0u, d_qoff);
-    tb = tmp_bytes;
-    if (rocprim::radix_sort_pairs(tmp, tb, fk, qk, ids, fids, (size_t)M, 0, bits_for(G) + 16, s) != hipSuccess) {
-      rc = fail("finish-group sort");
-      break;
-    }
-    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, qk, M, G, 16u, d_foff);
+    // the step-begin ops; each position's item range (k.ipos is sorted)
+    hipLaunchKernelGGL(k_bucket_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, op_k, op_v, ovf + 3);
+    const uint32_t NP = (uint32_t)pl.pos.size();
+    hipLaunchKernelGGL(k_bounds, dim3(grid_for(M + 1)), dim3(kT), 0, s, (const uint32_t *)k.ipos, M, NP, 0u, d_poff);
     uint32_t n_ops = 0;
-    if (hipMemcpyAsync(&n_ops, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-      rc = fail("step-op count read-back");
+    std::vector<uint32_t> poff(NP + 1);
+    if (hipMemcpyAsync(&n_ops, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(poff.data(), d_poff, (NP + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = fail("bucket read-back");
       break;
     }
+    // the rounds' and groups' lists: positions in increasing order within each
+    std::vector<uint32_t> qdst(NP), fdst(NP);
+    {
+      std::vector<uint64_t> qn(R + 1, 0), fn(G + 1, 0);
+      for (uint32_t v = 0; v < NP; ++v) {
+        qn[pl.item_pos[v].qround + 1] += poff[v + 1] - poff[v];
+        fn[pl.item_pos[v].fgroup + 1] += poff[v + 1] - poff[v];
+      }
+      for (uint32_t r = 0; r < R; ++r) qn[r + 1] += qn[r];
+      for (uint32_t g = 0; g < G; ++g) fn[g + 1] += fn[g];
+      for (uint32_t r = 0; r <= R; ++r) qoff[r] = (uint32_t)qn[r];
+      for (uint32_t g = 0; g <= G; ++g) foff[g] = (uint32_t)fn[g];
+      for (uint32_t v = 0; v < NP; ++v) {
+        const uint32_t c = poff[v + 1] - poff[v];
+        qdst[v] = (uint32_t)qn[pl.item_pos[v].qround];
+        qn[pl.item_pos[v].qround] += c;
+        fdst[v] = (uint32_t)fn[pl.item_pos[v].fgroup];
+        fn[pl.item_pos[v].fgroup] += c;
+      }
+    }
+    if (hipMemcpyAsync(d_qdst, qdst.data(), NP * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_fdst, fdst.data(), NP * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = fail("list upload");
+      break;
+    }
+    hipLaunchKernelGGL(k_scatter_ids, dim3(grid_for(M)), dim3(kT), 0, s, k, d_poff, d_qdst, d_fdst, qids, fids);
+    size_t tb = tmp_bytes;
     std::vector<uint32_t> soff(R + 1, 0);
     if (n_ops) {
-      tb = tmp_bytes;
       if (rocprim::radix_sort_pairs(tmp, tb, op_k, op_k2, op_v, op_v2, (size_t)n_ops, 0, bits_for(R), s) != hipSuccess) {
         rc = fail("step-op sort");
         break;
       }
       hipLaunchKernelGGL(k_bounds, dim3(grid_for(n_ops + 1)), dim3(kT), 0, s, op_k2, (uint64_t)n_ops, R, 0u, d_soff);
-      if (hipMemcpyAsync(soff.data(), d_soff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+      if (hipMemcpyAsync(soff.data(), d_soff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
         rc = fail("step-op offsets read-back");
         break;
       }
-    }
-    if (hipMemcpyAsync(qoff.data(), d_qoff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(foff.data(), d_foff, (G + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-      rc = fail("bucket read-back");
-      break;
     }
     const uint32_t row_bits = bits_for(max_row);
     // A/B switch: always the two-sort queue path
