@@ -137,3 +137,33 @@ def test_items_two_sort_queue_path(gpu, name, monkeypatch):
     # sorts), taken when row | replica | arrival does not fit one 64-bit key
     monkeypatch.setenv("ISIM_DES_ITEMS_TWO_SORTS", "1")
     DesCase(CASES[name](), 500_000).compare(31, 2500)
+
+
+def test_items_c5p_bench_batch_sparse_load(gpu):
+    """c5p exactly as bench.py builds it, at its bench batch (2^19 traces),
+    under a sparse load (mean gap 17 s against ~35 ms latencies): the
+    executed calls, hop counts and statuses of every trace are the lane tree
+    walk's (isim_serve on the same graph: queueing changes no skip and no
+    error), no latency is below the walk's (queueing only adds), and the
+    traces that do not overlap another — all but the ~0.2 % whose
+    exponential gap is shorter than a latency — equal it.  Size-independent
+    properties at the full size, where the event oracle is too slow to run."""
+    import bench
+    j, _ = bench.build_graph("c5p")
+    h = isim.Handler(isim.ServiceGraph.from_json(j), None, isim.SimParams())
+    n = bench.BENCH_BATCH["c5p"]
+    d = isim.DesHandler(h, 1 << 34)
+    assert d.info.items == 1
+    recs, stats, table = d.serve(1 << 31, n, device=0)
+    wrec, wstats = h.serve(1 << 31, n, device=0)
+    assert np.array_equal(recs["hops"], wrec["hops"])
+    assert np.array_equal(recs["status_err"], wrec["status_err"])
+    assert np.all(recs["latency_ns"] >= wrec["latency_ns"])
+    same = np.count_nonzero(recs["latency_ns"] == wrec["latency_ns"])
+    assert same >= 0.99 * n, same
+    rows = d.fold(table)
+    assert int(rows[:, native.DES_ROW_WORDS - 4].sum()) == int(recs["hops"].sum())
+    # the executed-call counters are the walk's too
+    fd, fw = h.fold(stats), h.fold(wstats)
+    assert np.array_equal(np.asarray(fd["site_calls"]), np.asarray(fw["site_calls"]))
+    assert np.array_equal(np.asarray(fd["svc_errs"]), np.asarray(fw["svc_errs"]))
