@@ -475,11 +475,12 @@ struct MPThen {
 // they were and the pass skips them).  The range words alternate between two
 // slots by launch; this launch empties the other slot for the next one.
 __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t m, uint32_t *repb,
-                                             unsigned long long *mm, unsigned long long *mm_next) {
+                                             unsigned long long *mm, unsigned long long *mm_next, uint32_t *bad) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
     atomicExch(mm_next, ~0ull);
     atomicExch(mm_next + 1, 0ull);
     atomicExch(mm_next + 2, 0ull);
+    atomicExch(bad, 0u);  // k_ordchk's flag
   }
   unsigned long long lo = ~0ull, hi = 0;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
@@ -538,21 +539,68 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
 
 // ONE sort key when the bits fit: row | replica | arrival - amin (the tie
 // order of equal keys is the item order: trace, hop)
+// (the value is the list index j: a cyclic schedule keeps each round's sorted
+// order for the next pass, k_ordchk)
 __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
                                               uint64_t amin, uint32_t rb, uint32_t ab, uint64_t *key, uint32_t *val) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
     const uint64_t row = k.pos[k.ipos[i]].row;
     key[j] = (((row << rb) | repb[j]) << ab) | (k.IA[i] - amin);
-    val[j] = i;
+    val[j] = (uint32_t)j;
+  }
+}
+
+// the previous pass's sorted order of a round (list indices j) against this
+// pass's (row, replica, arrival): when (row, replica, arrival, j) strictly
+// increases along it, it IS the stable sort of the round's queue keys, and
+// the sort is skipped (k_pairs1o); any inversion raises *bad (cleared by
+// k_qarr) and the host sorts (des_items_launch)
+__device__ __forceinline__ void qtuple(const K &k, const uint32_t *ids, const uint32_t *repb, uint32_t j,
+                                       uint64_t &hi, uint64_t &a) {
+  const uint32_t i = ids[j];
+  hi = ((uint64_t)k.pos[k.ipos[i]].row << 32) | repb[j];
+  a = k.IA[i];
+}
+__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *repb, const uint32_t *ord,
+                                               uint64_t m, uint32_t *bad) {
+  for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
+    bool inv = false;
+    if (jj > 0) {
+      const uint32_t j = ord[jj], jp = ord[jj - 1];
+      uint64_t h, a, hp, ap;
+      qtuple(k, ids, repb, j, h, a);
+      qtuple(k, ids, repb, jp, hp, ap);
+      inv = hp > h || (hp == h && (ap > a || (ap == a && jp > j)));
+    }
+    const unsigned long long bm = __ballot(inv);
+    if (bm && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)bm) - 1u &&
+        __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      atomicOr(bad, 1u);
+  }
+}
+
+// k_pairs1's outputs along a kept order
+__global__ void __launch_bounds__(kT) k_pairs1o(K k, uint64_t m, const uint32_t *ord, const uint32_t *ids,
+                                                const uint32_t *repb, uint32_t rb, uint32_t *segk, uint32_t *rowk,
+                                                MP *mp, uint32_t *sid) {
+  for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
+    const uint32_t j = ord[jj];
+    const uint32_t i = ids[j];
+    const uint32_t row = k.pos[k.ipos[i]].row;
+    const uint64_t hold = k.row_hold[row];
+    segk[jj] = (row << rb) | repb[j];
+    rowk[jj] = row;
+    mp[jj] = MP{hold, k.IA[i] + hold};
+    sid[jj] = i;
   }
 }
 
 // the segment key (row | replica), row, map (hold, a + hold) and item of
 // each position of the sorted order
-__global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *key, const uint32_t *items,
-                                               uint32_t rb, uint32_t ab, uint64_t amin, uint32_t *segk,
-                                               uint32_t *rowk, MP *mp, uint32_t *sid) {
+__global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *key, const uint32_t *js,
+                                               const uint32_t *ids, uint32_t rb, uint32_t ab, uint64_t amin,
+                                               uint32_t *segk, uint32_t *rowk, MP *mp, uint32_t *sid) {
   const uint64_t amask = (1ull << ab) - 1ull;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint64_t kk = key[j];
@@ -561,7 +609,7 @@ __global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *
     segk[j] = (uint32_t)(kk >> ab);
     rowk[j] = row;
     mp[j] = MP{hold, (kk & amask) + amin + hold};
-    sid[j] = items[j];
+    sid[j] = ids[js[j]];
   }
 }
 
@@ -1062,7 +1110,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
       pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops: rounds, (item, step)
-      M * 4, 4, M * 4, 4, M * 4, M * 4,                        // qk (spare) ids (spare) qids fids
+      M * 4, pl.cyclic ? M * 4 : 4, M * 4, 4, M * 4, M * 4,    // qk ord ids (spare) qids fids
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       4, 4, 16,                                                // (spare, spare); ovf: key overflow, no fixed
@@ -1110,7 +1158,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *op_k = (uint32_t *)carve(parts[10]);
   unsigned long long *op_v = (unsigned long long *)carve(parts[11]);
   uint32_t *qk = (uint32_t *)carve(parts[12]);
-  (void)carve(parts[13]);
+  uint32_t *ord = (uint32_t *)carve(parts[13]);  // per sort round: the last sorted order (list indices)
   uint32_t *ids = (uint32_t *)carve(parts[14]);
   (void)carve(parts[15]);
   uint32_t *qids = (uint32_t *)carve(parts[16]), *fids = (uint32_t *)carve(parts[17]);
@@ -1125,6 +1173,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
   uint64_t *mm = (uint64_t *)carve(parts[32]);
   uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] how many (debug)
+  uint32_t *ordbad = chg + 2;            // k_ordchk: the kept order is not this pass's
   uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
   unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
   uint32_t *d_soff = (uint32_t *)carve(parts[35]);
@@ -1247,6 +1296,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     uint64_t *acc_a = k.acc;
     uint32_t qn = 0;       // k_qarr launches: the arrival-range slot alternates
     uint64_t skipped = 0;  // queue rounds a quiet pass skipped (ISIM_DES_DEBUG)
+    uint64_t reused = 0;   // queue sorts a kept order replaced (ISIM_DES_DEBUG)
+    // A/B switch: never reuse a kept order
+    const bool keep_ord = pl.cyclic && std::getenv("ISIM_DES_ITEMS_NO_ORDER_REUSE") == nullptr;
+    std::vector<uint8_t> have_ord(R, 0);
     auto pass = [&](K &kk) {
     if (pl.cyclic) {
       std::swap(acc_a, acc_b);
@@ -1266,15 +1319,21 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
         ++qn;
         hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
-                           (unsigned long long *)slot, (unsigned long long *)slot_next);
+                           (unsigned long long *)slot, (unsigned long long *)slot_next, ordbad);
         const bool nosort = pl.round_nosort[r] && !two_sorts;
+        const bool chk = !nosort && have_ord[r];
+        if (chk)
+          hipLaunchKernelGGL(k_ordchk, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
+                             (const uint32_t *)rv_b, (const uint32_t *)(ord + qoff[r]), m, ordbad);
         // a quiet pass after the first: a round whose arrivals all equal the
         // previous pass's keeps its starts (its queues are skipped)
         // (sort rounds only: they read the range back anyway; a sort-free
         // round would pay a stream synchronisation for the check)
         const bool may_skip = kk.quiet && !kk.first && !nosort && !no_skip;
         uint64_t hmm[3] = {0, 0, 1};
+        uint32_t bad = 1;
         if ((!nosort || may_skip) && (hipMemcpyAsync(hmm, slot, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                                      (chk && hipMemcpyAsync(&bad, ordbad, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
                                       hipStreamSynchronize(s) != hipSuccess)) {
           rc = fail("arrival range read-back");
           break;
@@ -1285,7 +1344,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         }
         const uint32_t ab = bits_for(hmm[1] - hmm[0]);
         tb = tmp_bytes;
-        if (nosort) {
+        if (chk && !bad) {  // the kept order holds: no sort
+          ++reused;
+          hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
+                             (const uint32_t *)(qids + qoff[r]), (const uint32_t *)rv_b, rep_bits, rk_a, rk_b, mp_in,
+                             sid);
+        } else if (nosort) {
           hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b, mp_in,
                              sid);
         } else if (!two_sorts && row_bits + rep_bits + ab <= 64) {
@@ -1296,8 +1360,15 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
             rc = fail("queue sort");
             break;
           }
-          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b, rep_bits, ab, hmm[0],
-                             rk_a, rk_b, mp_in, sid);
+          if (keep_ord) {  // the next pass checks this order first
+            if (hipMemcpyAsync(ord + qoff[r], val_b, m * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+              rc = fail("order copy");
+              break;
+            }
+            have_ord[r] = 1;
+          }
+          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b,
+                             (const uint32_t *)(qids + qoff[r]), rep_bits, ab, hmm[0], rk_a, rk_b, mp_in, sid);
         } else {
           hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
                              key_a, val_a, ovf);
@@ -1361,8 +1432,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         if (!changed[0]) break;
       }
       if (debug)
-        std::fprintf(stderr, "isim des items: cyclic schedule, %u passes, %llu unchanged queue rounds skipped\n", p + 1,
-                     (unsigned long long)skipped);
+        std::fprintf(stderr,
+                   "isim des items: cyclic schedule, %u passes, %llu unchanged queue rounds skipped, %llu sorts "
+                   "replaced by the kept order\n",
+                   p + 1, (unsigned long long)skipped, (unsigned long long)reused);
       if (!rc && p == kMaxPasses) {
         static const uint32_t one = 1;
         if (hipMemcpyAsync(ovf + 1, &one, 4, hipMemcpyHostToDevice, s) != hipSuccess) rc = fail("flag");
