@@ -167,3 +167,22 @@ def test_items_c5p_bench_batch_sparse_load(gpu):
     fd, fw = h.fold(stats), h.fold(wstats)
     assert np.array_equal(np.asarray(fd["site_calls"]), np.asarray(fw["site_calls"]))
     assert np.array_equal(np.asarray(fd["svc_errs"]), np.asarray(fw["svc_errs"]))
+
+
+@pytest.mark.parametrize("mean", [50_000, 400_000])
+def test_items_kept_queue_order(gpu, mean, monkeypatch):
+    """A cyclic schedule's quiet passes reuse a sort round's previous sorted
+    order when it still sorts the new arrivals (k_ordchk / k_pairs1o); under
+    heavy and light contention, at a size where some kept orders hold and
+    some fail, everything equals the run that sorts every round
+    (ISIM_DES_ITEMS_NO_ORDER_REUSE) and, at a smaller size, the oracle."""
+    c = DesCase(CASES["mesh_des"](), mean)
+    assert c.d.info.items == 1 and c.d.info.cyclic == 1
+    c.compare(7, 1500)
+    n = 40_000
+    got = c.d.serve(1 << 20, n, device=0)
+    monkeypatch.setenv("ISIM_DES_ITEMS_NO_ORDER_REUSE", "1")
+    ref = c.d.serve(1 << 20, n, device=0)
+    assert np.array_equal(got[0], ref[0])
+    assert np.array_equal(np.asarray(got[1]), np.asarray(ref[1]))
+    assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))
