@@ -670,15 +670,15 @@ __global__ void __launch_bounds__(kT) k_pairs2(K k, uint64_t m, const uint32_t *
 // thread's span are summed before the atomics)
 constexpr uint32_t kQSpan = 16;
 __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rkb, const uint32_t *sid,
-                                             const MP *in, const MP *inc) {
+                                             const MP *in, const MP *inc, uint32_t span) {
   // the chunk's first row's queue figures in LDS (a chunk of 4,096 items is
   // mostly one row: one global atomic per figure and chunk, not per lane run)
   __shared__ unsigned long long s_n, s_sw, s_mw, s_sh;
   __shared__ uint32_t s_row;
-  // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
-  // count: its barriers), a wave 64 x kQSpan, lane l the items l, l + 64, ...
+  // a workgroup takes kT x span consecutive sorted items (uniform trip
+  // count: its barriers), a wave 64 x span, lane l the items l, l + 64, ...
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  constexpr uint64_t kChunk = (uint64_t)kT * kQSpan;
+  const uint64_t kChunk = (uint64_t)kT * span;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < m; c0 += (uint64_t)gridDim.x * kChunk) {
     if (!k.quiet) {
       if (threadIdx.x == 0) {
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
       __syncthreads();
     }
     const uint32_t hrow = k.quiet ? kNone : s_row;
-    const uint64_t j0 = c0 + (uint64_t)wave * 64 * kQSpan;
+    const uint64_t j0 = c0 + (uint64_t)wave * 64 * span;
     uint32_t row = kNone;
     unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
     auto flush = [&]() {
@@ -706,7 +706,7 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
       if (mw) atomicMax(tr + ISIM_DES_MAX_WAIT, mw);
       if (sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, sh);
     };
-    for (uint64_t j = j0 + lane; j < j0 + 64 * kQSpan && j < m; j += 64) {
+    for (uint64_t j = j0 + lane; j < j0 + 64 * span && j < m; j += 64) {
       const uint32_t i = sid[j];
       const uint32_t r = rkb[j];
       const uint64_t hold = k.row_hold[r];
@@ -743,7 +743,7 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
 // item the finish and its callee maximum into the caller's slot; the
 // statistics summed over a thread's run of one position (and one bucket for
 // the histogram) before the atomics
-__global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m) {
+__global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m, uint32_t span) {
   __shared__ uint8_t lut[kLutEntries];
   // the duration histogram of the chunk's first row (a chunk of 4,096 sorted
   // items is mostly one position): LDS atomics, one global add per bucket
@@ -752,12 +752,12 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
   // and the chunk's first position's duration sums and site counts
   __shared__ unsigned long long f_d0, f_d1, f_n, f_n5;
   if (!k.quiet) lut_init(lut);
-  // a workgroup takes kT x kQSpan consecutive sorted items (uniform trip
-  // count: its barriers), a wave 64 x kQSpan of them, lane l the items
+  // a workgroup takes kT x span consecutive sorted items (uniform trip
+  // count: its barriers), a wave 64 x span of them, lane l the items
   // l, l + 64, ...: coalesced loads, and a lane's items mostly share a
   // position, so its runs sum before the atomics
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  constexpr uint64_t kChunk = (uint64_t)kT * kQSpan;
+  const uint64_t kChunk = (uint64_t)kT * span;
   for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < m; c0 += (uint64_t)gridDim.x * kChunk) {
     if (!k.quiet) {
       for (uint32_t x = threadIdx.x; x < 2 * ISIM_N_PROM; x += kT) hist[x] = 0;
@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       __syncthreads();
     }
     const uint32_t hrow = k.quiet ? kNone : s_row, hpos = k.quiet ? kNone : s_pos;
-    const uint64_t j0 = c0 + (uint64_t)wave * 64 * kQSpan;
+    const uint64_t j0 = c0 + (uint64_t)wave * 64 * span;
     uint32_t v_run = kNone, b_run = kNone;
     DesPos P{};
     DesItemPos p{};
@@ -799,7 +799,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
         if (n5) atomicAdd(k.stats + ISIM_ST_SITES + k.n_slots + P.slot, n5);
       }
     };
-    for (uint64_t j = j0 + lane; j < j0 + 64 * kQSpan && j < m; j += 64) {
+    for (uint64_t j = j0 + lane; j < j0 + 64 * span && j < m; j += 64) {
       const uint32_t i = ids[j];
       const uint32_t v = k.ipos[i];
       if (v != v_run) {
@@ -1287,6 +1287,13 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     const bool two_sorts = std::getenv("ISIM_DES_ITEMS_TWO_SORTS") != nullptr;
     // A/B switch: never skip an unchanged round
     const bool no_skip = std::getenv("ISIM_DES_ITEMS_NO_SKIP") != nullptr;
+    // A/B switch: quiet passes with the statistics pass's 16 items per lane
+    const bool fat_quiet = std::getenv("ISIM_DES_ITEMS_FAT_QUIET") != nullptr;
+    uint32_t stats_span = kQSpan;  // A/B: ISIM_DES_ITEMS_STATS_SPAN (1..64)
+    if (const char *e = std::getenv("ISIM_DES_ITEMS_STATS_SPAN")) {
+      const long v = std::strtol(e, nullptr, 10);
+      if (v >= 1 && v <= 64) stats_span = (uint32_t)v;
+    }
     // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
     // every time: the iteration only raises values) until no stored value
     // changes, then the pass that records the statistics (des.hip des_launch)
@@ -1310,6 +1317,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       rc = fail("memset");
       return;
     }
+    // items per lane of k_qout / k_fin: runs of one row / position summed
+    // before the statistics atomics; a quiet pass records none, and one item
+    // per lane gives its finish groups (~0.8 M items on c4d) 16x the waves
+    const uint32_t span = kk.quiet && !fat_quiet ? 1u : stats_span;
     for (uint32_t r = 0; r < R && !rc; ++r) {
       if (soff[r + 1] > soff[r])
         hipLaunchKernelGGL(k_steps, dim3(grid_for(soff[r + 1] - soff[r])), dim3(kT), 0, s, kk, op_v2 + soff[r],
@@ -1391,14 +1402,14 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           rc = fail("queue scan");
           break;
         }
-        hipLaunchKernelGGL(k_qout, dim3(grid_for((m + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk, m, rk_b, sid,
-                           mp_in, mp_out);
+        hipLaunchKernelGGL(k_qout, dim3(grid_for((m + span - 1) / span)), dim3(kT), 0, s, kk, m, rk_b, sid,
+                           mp_in, mp_out, span);
       }
     finishes:
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
         const uint64_t mg = foff[gi + 1] - foff[gi];
-        if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for((mg + kQSpan - 1) / kQSpan)), dim3(kT), 0, s, kk,
-                                   fids + foff[gi], mg);  // grid_for(ceil(mg / kQSpan)) blocks of kT: >= the chunks
+        if (mg) hipLaunchKernelGGL(k_fin, dim3(grid_for((mg + span - 1) / span)), dim3(kT), 0, s, kk,
+                                   fids + foff[gi], mg, span);  // grid_for(ceil(mg / span)) blocks of kT: >= the chunks
       }
     }
     };
