@@ -343,7 +343,8 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
                        des_fused_leaves=d.info.n_fused,
                        des_engine="items (dynamic walk)" if items else "level-synchronous rows",
                        des_rows="u64" if wide[0] or items else "u32", des_cyclic=bool(d.info.cyclic),
-                       workspace_bytes=wsb),
+                       workspace_bytes=wsb, rccl_ranks=multi.n_ranks if multi is not None else None,
+                       traces_per_rank=args.steps * B),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("des_items k_* + rocPRIM sorts/scans per step" if items else
@@ -664,7 +665,8 @@ def main():
                        error_mode=args.mode, hop_visits_per_trace=hops_per_trace,
                        parallelism=f"trace-shard x{world}", merge=merge_label, records=not args.no_records,
                        static_walk=bool(info.static_walk), program_len=info.program_len,
-                       launch=launch),
+                       launch=launch, rccl_ranks=multi.n_ranks if multi is not None else None,
+                       traces_per_rank=args.steps * B),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "isim_fill_const (draw-free walk: one trace walked, records filled)"

@@ -266,7 +266,11 @@ ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32
  * over 256 sets per (handler, device); at most 256 launches
  * of one handler may be in flight on one device at once (launches on ONE
  * stream are ordered and never collide; with more than 256 streams in
- * flight, order them with events or use one handler per stream). */
+ * flight, order them with events or use one handler per stream).  A lane tree
+ * walk deeper than 16 calling invocations spills frames to one of 4 areas per
+ * (handler, device): each such launch waits for the previous launch that used
+ * its area (an event recorded after every spilling launch), so launches on
+ * different streams never share frames. */
 ISIM_API int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces,
                       isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
 

@@ -83,8 +83,14 @@ struct DevState {
   isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
   uint32_t *d_sum_row = nullptr;        // kind 7: per LDS sum index, its row
   uint32_t *d_slot_tc = nullptr;        // kind 7: per slot, the leaf callee's latency
-  uint32_t *d_spill = nullptr;          // kind 7: frames below the register stack
+  uint32_t *d_spill = nullptr;          // kind 7: frames below the register stack, kSpillAreas areas
   uint32_t spill_lanes = 0;
+  size_t spill_words = 0;               // u32 words of one area
+  hipEvent_t spill_ev[isim::kSpillAreas] = {};     // recorded after each area's latest launch
+  hipStream_t spill_last[isim::kSpillAreas] = {};  // the stream of that launch
+  bool spill_used[isim::kSpillAreas] = {};
+  uint32_t spill_next = 0;
+  hipMemPool_t des_pool = nullptr;      // the item engine's per-batch arrays (a private pool)
 };
 
 void free_dev(DevState &d) {
@@ -97,6 +103,9 @@ void free_dev(DevState &d) {
                   (void *)d.d_des_sround, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
                   (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill})
     if (q) (void)hipFree(q);
+  for (hipEvent_t e : d.spill_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (d.des_pool) (void)hipMemPoolDestroy(d.des_pool);
   d = DevState();
 }
 
@@ -110,6 +119,7 @@ struct isim_handler {
   isim::Program prog;
   isim_params params{};
   std::mutex mu;
+  std::mutex spill_mu;  // kind 7 spill areas: area choice, wait, launch, record
   std::map<int, DevState> dev;
   // the DES plan is built on first use (des_ensure): it unrolls the whole
   // invocation tree, which walks never need
@@ -353,10 +363,14 @@ int build_device(isim_handler *h, int device, DevState &st) {
   st.max_mult = std::max<uint64_t>(1, p.hops_upper);
   if (tree) {
     st.max_mult = std::max<uint32_t>(1, p.tree_mult);
-    if (p.tree_frames > isim::kTreeRegFrames) {  // the spill area: frames below the 8 register frames
+    if (p.tree_frames > isim::kTreeRegFrames) {
+      // the spill areas: frames below the 8 register frames, one column per
+      // lane of a full grid; a launch waits for the area's previous launch
+      // (launch_walk_one)
       st.spill_lanes = st.max_blocks * st.threads;
-      const size_t words = (size_t)(p.tree_frames - 8u) * isim::kTreeSpillWords * st.spill_lanes;
-      HIPCHK(hipMalloc(&st.d_spill, words * sizeof(uint32_t)));
+      st.spill_words = (size_t)(p.tree_frames - 8u) * isim::kTreeSpillWords * st.spill_lanes;
+      HIPCHK(hipMalloc(&st.d_spill, st.spill_words * isim::kSpillAreas * sizeof(uint32_t)));
+      for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
   }
   if (is_stream(st.kind)) {
@@ -603,7 +617,6 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.tree_dyn = st->d_tree_dyn;
   kp.sum_row = st->d_sum_row;
   kp.slot_tc = st->d_slot_tc;
-  kp.spill = st->d_spill;
   kp.spill_lanes = st->spill_lanes;
   kp.n_pos = (uint32_t)h->prog.tree_nodes.size();
   kp.n_rows = (uint32_t)h->prog.row_svc.size();
@@ -623,7 +636,30 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
-  HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, (hipStream_t)hip_stream));
+  if (st->d_spill) {
+    // a spilling walk: the area its stream used last (else the next one,
+    // round robin), ordered after the area's previous launch by an event; the
+    // wait, launch and record are one step under the handler's lock.  A
+    // capturing stream that used the area last skips the wait (its own order
+    // covers it, and a capture may not wait on work from outside it).
+    const hipStream_t hs = (hipStream_t)hip_stream;
+    std::lock_guard<std::mutex> lk(h->spill_mu);
+    uint32_t a = isim::kSpillAreas;
+    for (uint32_t i = 0; i < isim::kSpillAreas; ++i)
+      if (st->spill_used[i] && st->spill_last[i] == hs) a = i;
+    if (a == isim::kSpillAreas) a = st->spill_next++ % isim::kSpillAreas;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(hs, &cs);
+    if (st->spill_used[a] && !(cs == hipStreamCaptureStatusActive && st->spill_last[a] == hs))
+      HIPCHK(hipStreamWaitEvent(hs, st->spill_ev[a], 0));
+    kp.spill = st->d_spill + a * st->spill_words;
+    HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, hs));
+    HIPCHK(hipEventRecord(st->spill_ev[a], hs));
+    st->spill_last[a] = hs;
+    st->spill_used[a] = true;
+  } else {
+    HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, (hipStream_t)hip_stream));
+  }
   if (is_stream(st->kind) && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;
@@ -826,6 +862,16 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
   if (!up((void **)&st->d_des_pipe, pipe.data(), pipe.size() * 4)) return fail(ISIM_EHIP, "DES plan upload failed");
   if (d.items) {
     const isim::Program &p = h->prog;
+    // the per-batch item arrays come from a pool of this handler's own (kept
+    // between batches: a release threshold of ~0 on a pool nobody else uses)
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = device;
+    uint64_t keep = ~0ull;
+    if (hipMemPoolCreate(&st->des_pool, &props) != hipSuccess ||
+        hipMemPoolSetAttribute(st->des_pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
+      return fail(ISIM_EHIP, "DES item pool creation failed");
     if (!up(&st->d_des_ipos, d.item_pos.data(), d.item_pos.size() * sizeof(isim::DesItemPos)) ||
         !up((void **)&st->d_des_sround, d.step_round.data(), d.step_round.size() * 4) ||
         !up(&st->d_des_nodes, p.tree_nodes.data(), p.tree_nodes.size() * sizeof(isim::TreeNode)) ||
@@ -907,6 +953,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.mean_ns = dp->mean_interarrival_ns;
     L.seed = h->params.seed;
     L.n_slots = (uint32_t)h->prog.n_slots;
+    L.pool = st->des_pool;
     std::string e;
     const int irc = isim::des_items_launch(L, hip_stream, e);
     if (irc == 2) return fail(ISIM_EINVAL, e);

@@ -209,8 +209,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
 
 // The item engine (des_items.hip): one batch of a dynamic walk's DES.  Device
 // per-trace workspace bytes; the per-item arrays are allocated on `stream`
-// (hipMallocAsync) once the batch's executed invocations are counted, which
-// synchronizes the stream once per batch.
+// from `pool` (the handler's private hipMemPool_t on this device) once the
+// batch's executed invocations are counted.
 struct DesItemsLaunch {
   const DesPlan *plan;
   const void *d_pos, *d_item_pos, *d_steps;  // DesPos[n_pos], DesItemPos[n_pos], DesStep[]
@@ -222,6 +222,7 @@ struct DesItemsLaunch {
   isim_trace_rec *d_records;
   uint64_t n_traces, trace_begin, mean_ns, seed;
   uint32_t n_slots;
+  void *pool;  // hipMemPool_t
 };
 uint64_t des_items_workspace_bytes(uint64_t n);
 int des_items_launch(const DesItemsLaunch &L, void *stream, std::string &err);

@@ -615,8 +615,10 @@ __global__ void __launch_bounds__(kT) k_pairs1(K k, uint64_t m, const uint64_t *
 
 // a round whose positions need no sort (DesPlan::round_nosort): its items in
 // their (position, trace) order are each position's FIFO already; the
-// segment key is the position (two positions of one zero-hold service stay
-// two segments)
+// segment key is the position.  A zero-hold position (its arrivals need not
+// come in trace order) starts each item at its own arrival (des_oracle.c: an
+// invocation holding its worker for 0 starts when it arrives): every item is
+// a segment of its own, keys alternating by list index above any position
 __global__ void __launch_bounds__(kT) k_pairs0(K k, const uint32_t *ids, uint64_t m, uint32_t *segk, uint32_t *rowk,
                                                MP *mp, uint32_t *sid) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
@@ -624,7 +626,7 @@ __global__ void __launch_bounds__(kT) k_pairs0(K k, const uint32_t *ids, uint64_
     const uint32_t v = k.ipos[i];
     const uint32_t row = k.pos[v].row;
     const uint64_t hold = k.row_hold[row];
-    segk[j] = v;
+    segk[j] = hold ? v : 0x80000000u | (uint32_t)(j & 1u);
     rowk[j] = row;
     mp[j] = MP{hold, k.IA[i] + hold};
     sid[j] = i;
@@ -1020,11 +1022,25 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   // 2. pre-walk: count, offsets, emit
   const uint32_t fr = L.tree_frames;
   const bool spill = fr > 16;
+  // per-batch buffers come from the handler's private pool (L.pool: never the
+  // device's default pool, whose attributes belong to the application) and go
+  // back to it on every return
+  struct PoolBuf {
+    void *p = nullptr;
+    hipStream_t s;
+    ~PoolBuf() {
+      if (p) (void)hipFreeAsync(p, s);
+    }
+  } spill_mem{nullptr, s}, item_mem{nullptr, s};
+  auto pool_alloc = [&](PoolBuf &b, uint64_t bytes) {
+    return hipMallocFromPoolAsync(&b.p, bytes, (hipMemPool_t)L.pool, s) == hipSuccess;
+  };
   uint32_t *spill_buf = nullptr;
   const uint64_t pw_threads = (uint64_t)kPrewalkBlocks * kT;
   if (spill) {
     const uint64_t words = (uint64_t)(fr - 8 + 1) * kTreeSpillWords * pw_threads;
-    if (hipMallocAsync((void **)&spill_buf, words * 4, s) != hipSuccess) return fail("spill allocation");
+    if (!pool_alloc(spill_mem, words * 4)) return fail("spill allocation");
+    spill_buf = (uint32_t *)spill_mem.p;
   }
   k.spill = spill_buf;
   // the nodes in LDS (1024-thread workgroups, one per CU at these register
@@ -1078,7 +1094,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       hipStreamSynchronize(s) != hipSuccess)
     return fail("item count read-back");
   if (M >= 0xFFFFFFFFull) {
-    if (spill_buf) (void)hipFreeAsync(spill_buf, s);
     err = "DES items: a batch of more than 2^32 - 1 executed invocations (use smaller batches)";
     return 2;
   }
@@ -1103,7 +1118,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   std::vector<uint64_t> row_hold(std::max<size_t>(1, max_row + 1), 0);
   for (const DesPos &q : pl.pos) row_hold[q.row] = q.hold;
   const size_t rows_n = row_hold.size();
-  if (bits_for(G) + 16 > 32) return fail("more than 65535 finish groups");
   const uint64_t parts[] = {
       M * 4, M * 4, M * 4, M,                                  // ipos ipar itr iown
       M * 8, M * 8, M * 8,                                     // IA IS IF
@@ -1123,23 +1137,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       tmp_bytes};
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
-  // keep the freed item arrays in the device's pool between batches (the
-  // default release threshold 0 hands them back at every synchronisation,
-  // and the next batch maps them again)
-  {
-    int dev = 0;
-    hipMemPool_t pool;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t keep = ~0ull;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-  }
-  char *base = nullptr;
-  if (hipMallocAsync((void **)&base, total, s) != hipSuccess) {
-    if (spill_buf) (void)hipFreeAsync(spill_buf, s);
-    return fail("item allocation");
-  }
-  char *at = base;
+  if (!pool_alloc(item_mem, total)) return fail("item allocation");
+  char *at = (char *)item_mem.p;
   auto carve = [&](uint64_t bytes) {
     char *p = at;
     at += al256(bytes ? bytes : 1);
@@ -1461,8 +1460,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     hipLaunchKernelGGL(k_flag_retry, dim3(1), dim3(1), 0, s, k.stats, ovf);
     if (hipGetLastError() != hipSuccess) rc = fail("kernel launch");
   } while (0);
-  (void)hipFreeAsync(base, s);
-  if (spill_buf) (void)hipFreeAsync(spill_buf, s);
   return rc;
 }
 

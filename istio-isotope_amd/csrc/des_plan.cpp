@@ -569,6 +569,11 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
         out.item_bk = std::max<uint32_t>(out.item_bk, ip.nsteps);
       }
     }
+    // the finish sort keys hold group | position bits (des_items.hip)
+    if (out.fin_off.size() - 1 > 65535) {
+      err = "DES of a dynamic walk: more than 65535 finish groups";
+      return ISIM_EINVAL;
+    }
     for (uint32_t gi = 0; gi + 1 < out.fin_off.size(); ++gi)
       for (uint32_t j = out.fin_off[gi]; j < out.fin_off[gi + 1]; ++j) out.item_pos[out.fin_pos[j]].fgroup = gi;
     out.round_nosort.assign(R, 1);

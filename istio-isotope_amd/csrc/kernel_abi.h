@@ -138,6 +138,7 @@ constexpr uint32_t kTreeMaxPositions = 0xFFFFu;  // u16 sizes and slots
 constexpr uint32_t kTreeRegFrames = 16;          // deepest register stack; deeper walks spill (kTreeMaxFrames)
 constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations below the current one
 constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
+constexpr uint32_t kSpillAreas = 4;              // spill areas per (handler, device): launches in flight
 // LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
 // workgroups per CU, and the whole CU.
 constexpr uint32_t kTreeLutBytes = 512;  // the duration-bucket table by ceil(t / 1 ms), after the histograms

@@ -41,7 +41,38 @@ def _sleepy(doc, pre="400us", post="100us"):
     return doc
 
 
+def _zero_hold_min():
+    """A sleep-free (zero-hold) service `z` called in the entry's second call
+    step, after a probabilistic call: its arrivals leave trace order whenever
+    a trace that ran `b` reaches `z` after a later one that skipped it; each
+    invocation of `z` must start at its own arrival (des_oracle.c), not at
+    the latest arrival before it (the sort-free rounds)."""
+    return {"services": [
+        {"name": "a", "isEntrypoint": True,
+         "script": [{"sleep": "300us"}, {"call": {"service": "b", "probability": 50}}, {"call": "z"}]},
+        {"name": "b", "script": [{"sleep": "1ms"}]},
+        {"name": "z"},
+    ]}
+
+
+def _zero_hold_mix():
+    """Zero-hold services as leaves and as callers (`w` calls `b`), a
+    replicated entry, and `b` reached from three positions."""
+    return {"services": [
+        {"name": "a", "isEntrypoint": True, "numReplicas": 2,
+         "script": [{"sleep": "200us"}, {"call": {"service": "b", "probability": 50}}, {"call": "z"},
+                    [{"call": {"service": "c", "probability": 60}}, {"call": "w"}], {"call": "z"},
+                    {"sleep": "50us"}]},
+        {"name": "b", "script": [{"sleep": "700us"}]},
+        {"name": "c", "script": [{"sleep": "300us"}, {"call": {"service": "b", "probability": 50}}]},
+        {"name": "w", "script": [{"call": {"service": "b", "probability": 40}}, {"call": "z"}]},
+        {"name": "z"},
+    ]}
+
+
 CASES = {
+    "zero_hold_min": _zero_hold_min,
+    "zero_hold_mix": _zero_hold_mix,
     "real300p60": lambda: realistic_topology(300, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.3),
                                              probability=60),
     "real300seq_p75": lambda: realistic_topology(300, sleep_ms=(1, 5), error_rate=(0.0, 0.3), probability=75),
@@ -186,3 +217,57 @@ def test_items_kept_queue_order(gpu, mean, monkeypatch):
     assert np.array_equal(got[0], ref[0])
     assert np.array_equal(np.asarray(got[1]), np.asarray(ref[1]))
     assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))
+
+
+def _bench_case(cfg):
+    import bench
+    j, _ = bench.build_graph(cfg)
+    mean = 150_000 if cfg == "c4d" else 6_000_000  # bench.py's default gaps
+    return DesCase(j, mean), bench.BENCH_BATCH[cfg]
+
+
+def test_items_c5p_bench_graph_and_load(gpu):
+    """c5p exactly as bench.py builds it (config 3's 10k
+    graph at probability 50) at the bench's own mean gap of 6 ms: 20,000
+    traces bit-exact against des_oracle.c — records, stats and the DES table
+    (the oracle runs ~3 s)."""
+    c, _ = _bench_case("c5p")
+    assert c.d.info.items == 1
+    _, _, rows = c.compare(1000, 20_000)
+    assert int(rows[:, native.DES_SUM_WAIT].sum()) > 0  # contended
+
+
+def test_items_c4d_bench_graph_and_load(gpu):
+    """c4d exactly as bench.py builds it (config 4's 100k
+    mesh with sleeps, a cyclic schedule) at the bench's own mean gap of
+    150 us: 20,000 traces bit-exact against des_oracle.c, and a second window
+    whose trace ids cross 2^32."""
+    c, _ = _bench_case("c4d")
+    assert c.d.info.items == 1 and c.d.info.cyclic == 1
+    _, _, rows = c.compare(0, 20_000)
+    assert int(rows[:, native.DES_SUM_WAIT].sum()) > 0
+    c.compare((1 << 32) - 7000, 14_000)
+
+
+def test_items_c4d_bench_batch(gpu):
+    """c4d at its bench batch (2^23 traces per step, mean gap 150 us), where the
+    event oracle would take minutes: the executed calls, hops and statuses of
+    every trace are the lane tree walk's (isim_serve on the same graph:
+    queueing changes no skip and no error), no latency is below the walk's
+    (queueing only adds), the DES table counts every executed invocation once,
+    and the call counters equal the walk's (executable.go:84-105,
+    svc/service.go:30-31)."""
+    c, n = _bench_case("c4d")
+    recs, stats, table = c.d.serve(1 << 23, n, device=0)
+    wrec, wstats = c.h.serve(1 << 23, n, device=0)
+    assert np.array_equal(recs["hops"], wrec["hops"])
+    assert np.array_equal(recs["status_err"], wrec["status_err"])
+    assert np.all(recs["latency_ns"] >= wrec["latency_ns"])
+    rows = c.d.fold(table)
+    assert int(rows[:, native.DES_ROW_WORDS - 4].sum()) == int(recs["hops"].sum())
+    assert int(rows[:, native.DES_SUM_WAIT].sum()) > 0
+    fd, fw = c.h.fold(stats), c.h.fold(wstats)
+    assert np.array_equal(np.asarray(fd["site_calls"]), np.asarray(fw["site_calls"]))
+    assert np.array_equal(np.asarray(fd["svc_calls"]), np.asarray(fw["svc_calls"]))
+    assert np.array_equal(np.asarray(fd["svc_errs"]), np.asarray(fw["svc_errs"]))
+    assert fd["n_traces"] == n and fd["sum_hops"] == fw["sum_hops"]

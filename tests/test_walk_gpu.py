@@ -317,3 +317,48 @@ def test_tree_row_counter_split(gpu):
     assert info["kernel_kind"] == 7 and info["lds_counters"] == 1
     assert info["max_launch_traces"] == 0xFFFFFFFF // 1600
     c.compare(5, 300)
+
+
+def _prob_chain(depth, p=90):
+    """A chain of `depth` calling services, every call probabilistic: a
+    dynamic walk whose frames go deeper than the 16 register frames of the
+    lane tree walk (the spill areas)."""
+    doc = json.loads(_chain(depth, 1))
+    for s in doc["services"]:
+        for st in s.get("script", []):
+            for c in (st if isinstance(st, list) else [st]):
+                if "call" in c:
+                    c["call"] = {"service": c["call"], "probability": p}
+    return json.dumps(doc)
+
+
+def test_tree_spill_two_streams(gpu):
+    """a spilling lane tree walk (call depth 40 > 16 register
+    frames) launched on two streams at once, many launches each, must give
+    every launch its own frames: each stream's accumulated stats and its last
+    records equal the sequential walk's (and the oracle's, on a window)."""
+    import torch
+    c = Case(_prob_chain(40), None, isim.SimParams())
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7 and c.handler.info.max_depth == 40
+    n = li["max_blocks"] * li["wg_threads"] + 777  # every lane of the grid walks (and spills)
+    begins = (1 << 20, (1 << 32) - 5000)
+    ref = [c.gpu(b, n) for b in begins]
+    c.compare(begins[1], 3000)
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev) for _ in begins]
+    st = [torch.zeros(c.handler.stats_words, dtype=torch.int64, device=dev) for _ in begins]
+    rec = [torch.zeros(n * 16, dtype=torch.uint8, device=dev) for _ in begins]
+    k = 6
+    torch.cuda.synchronize()
+    for _ in range(k):
+        for i, b in enumerate(begins):
+            c.handler.serve_device(b, n, rec[i].data_ptr(), st[i].data_ptr(), streams[i].cuda_stream)
+    torch.cuda.synchronize()
+    for i in range(len(begins)):
+        r = rec[i].cpu().numpy().view(isim.REC_DTYPE)
+        assert np.array_equal(r, ref[i][0])
+        fk, f1 = c.handler.fold(st[i].cpu().numpy().view(np.uint64)), c.handler.fold(ref[i][1])
+        assert fk["n_traces"] == k * n and fk["sum_latency"] == k * f1["sum_latency"]
+        assert fk["sum_hops"] == k * f1["sum_hops"] and fk["n_500"] == k * f1["n_500"]
+        assert np.array_equal(fk["site_calls"], k * f1["site_calls"])
