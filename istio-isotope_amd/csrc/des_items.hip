@@ -537,8 +537,8 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
   }
 }
 
-// ONE sort key when the bits fit: row | replica | arrival - amin (the tie
-// order of equal keys is the item order: trace, hop)
+// ONE sort key when the bits fit: row | replica | arrival - amin (equal keys
+// are put in (trace, hop) order afterwards: k_tiefix)
 // (the value is the list index j: a cyclic schedule keeps each round's sorted
 // order for the next pass, k_ordchk)
 __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
@@ -562,6 +562,38 @@ __device__ __forceinline__ void qtuple(const K &k, const uint32_t *ids, const ui
   hi = ((uint64_t)k.pos[k.ipos[i]].row << 32) | repb[j];
   a = k.IA[i];
 }
+// the oracle's tie order of equal (row, replica, arrival): (trace, hop) —
+// the event heap pops the earlier trace first (des_oracle.c).  The rounds'
+// lists are position-major, so a stable sort alone would break such ties by
+// position (a service reached from several positions, arrivals that meet
+// exactly: starts chained by a hold equal to a hop cost, for one)
+__device__ __forceinline__ uint64_t tie_key(const K &k, uint32_t i) {
+  return ((uint64_t)k.itr[i] << 32) | k.ihop[i];
+}
+// runs of equal keys in a sorted round, re-ordered by (trace, hop): the run's
+// first thread insertion-sorts it (runs are rare and short).  LIST: the
+// values are list indices into ids (k_qkey1), else item ids (k_qkey2)
+template <bool LIST>
+__global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_t *val, uint64_t m,
+                                               const uint32_t *ids) {
+  auto tk = [&](uint32_t v) { return tie_key(k, LIST ? ids[v] : v); };
+  for (uint64_t j = gid(); j + 1 < m; j += nthreads()) {
+    const uint64_t kj = key[j];
+    if (key[j + 1] != kj || (j > 0 && key[j - 1] == kj)) continue;  // the first of a run of ties only
+    uint64_t e = j + 2;
+    while (e < m && key[e] == kj) ++e;
+    for (uint64_t x = j + 1; x < e; ++x) {
+      const uint32_t v = val[x];
+      const uint64_t t = tk(v);
+      uint64_t y = x;
+      while (y > j && tk(val[y - 1]) > t) {
+        val[y] = val[y - 1];
+        --y;
+      }
+      val[y] = v;
+    }
+  }
+}
 __global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *repb, const uint32_t *ord,
                                                uint64_t m, uint32_t *bad) {
   for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
@@ -571,7 +603,7 @@ __global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const u
       uint64_t h, a, hp, ap;
       qtuple(k, ids, repb, j, h, a);
       qtuple(k, ids, repb, jp, hp, ap);
-      inv = hp > h || (hp == h && (ap > a || (ap == a && jp > j)));
+      inv = hp > h || (hp == h && (ap > a || (ap == a && tie_key(k, ids[jp]) > tie_key(k, ids[j]))));
     }
     const unsigned long long bm = __ballot(inv);
     if (bm && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)bm) - 1u &&
@@ -1370,6 +1402,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
             rc = fail("queue sort");
             break;
           }
+          hipLaunchKernelGGL(k_tiefix<true>, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint64_t *)key_b, val_b, m,
+                             (const uint32_t *)(qids + qoff[r]));
           if (keep_ord) {  // the next pass checks this order first
             if (hipMemcpyAsync(ord + qoff[r], val_b, m * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) {
               rc = fail("order copy");
@@ -1386,6 +1420,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
             rc = fail("arrival sort");
             break;
           }
+          // ties of (replica, arrival) by (trace, hop); the stable row sort keeps them
+          hipLaunchKernelGGL(k_tiefix<false>, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint64_t *)key_b, val_b, m,
+                             (const uint32_t *)nullptr);
           hipLaunchKernelGGL(k_rkeys, dim3(grid_for(m)), dim3(kT), 0, s, kk, val_b, m, rk_a, rv_a);
           tb = tmp_bytes;
           if (rocprim::radix_sort_pairs(tmp, tb, rk_a, rk_b, rv_a, rv_b, (size_t)m, 0, row_bits, s) != hipSuccess) {

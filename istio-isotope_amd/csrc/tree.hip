@@ -94,8 +94,8 @@ struct GlobalNodes {
 struct TreeSink {
   uint32_t *cnt;                // LDS: per slot calls | 500s << 16 (cnt16), else [2][n_slots] u32
   const uint8_t *lut;           // LDS duration-bucket table
-  unsigned long long *sum200;   // LDS [n_sum]
-  uint32_t *dyn;                // LDS bucket tables of the varying rows
+  uint32_t *sum200;             // LDS [n_sum]: code-200 duration sums, low 32 bits (carries go to HBM)
+  uint32_t *dyn;                // LDS bucket tables of the varying rows (code 200, guarded u16 pairs)
   uint64_t *svc_tab;            // HBM duration table, or null (ISIM_FLAG_NO_SVC_DUR)
   const uint32_t *sum_row;      // per LDS sum index: its row (code-500 sums go to HBM)
   uint32_t n_slots;
@@ -105,7 +105,7 @@ struct TreeSink {
   // A guarded 16-bit field reached 2^15: 2^15 of its events go to the stats
   // now, with what the flush derives from them (static duration buckets,
   // leaf-callee sums; for 500s, moved from code 200 to code 500)
-  __device__ __attribute__((noinline)) void move(uint32_t slot, bool err) {
+  __device__ __forceinline__ void move(uint32_t slot, bool err) {
     constexpr unsigned long long K = 0x8000ull;
     atomicAdd(sites + (err ? n_slots : 0u) + slot, K);
     lds_add(cnt + slot, err ? 0x80000000u : 0xFFFF8000u);  // the field less 2^15 (no borrow: it is >= 2^15)
@@ -171,18 +171,35 @@ struct TreeSink {
       atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
       return;
     }
+    // an LDS row (round 5: 4-byte sums and u16 code-200 buckets, so about
+    // twice the rows fit; 500s — errorRate-rare — go to HBM by atomics)
+    if (st) {
+      unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS);
+      if (place != kTreeStaticRow) atomicAdd(r + ISIM_N_PROM + lut_bucket(lut, T), 1ull);
+      atomicAdd(r + 2 * ISIM_N_PROM + 1, (unsigned long long)T);
+      return;
+    }
     if (place != kTreeStaticRow) {  // the row's LDS bucket table: header b_lo | width << 8
       const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
       uint32_t b = lut_bucket(lut, T) - lo;
       b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
-      lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
+      const uint32_t sh = (b & 1u) * 16u;
+      uint32_t *wd = dyn + place + 1u + (b >> 1);
+      const uint32_t old = lds_add_rtn(wd, 1u << sh);
+      if (((old >> sh) & 0xFFFFu) == 0x7FFFu) bucket_move(wd, sh, sum_row[idx], lo + b);
     }
-    if (st) {
-      unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS);
-      atomicAdd(r + 2 * ISIM_N_PROM + 1, (unsigned long long)T);
-    } else {
-      lds_add(sum200 + idx, (unsigned long long)T);
-    }
+    const uint32_t o = lds_add_rtn(sum200 + idx, T);
+    if (o + T < o) sum_carry(sum_row[idx]);
+  }
+  // a u16 bucket field reached 2^15: 2^15 of its counts go to the row in HBM
+  __device__ __forceinline__ void bucket_move(uint32_t *wd, uint32_t sh, uint32_t row, uint32_t bucket) {
+    atomicAdd((unsigned long long *)(svc_tab + (uint64_t)dur_row(row) * ISIM_SVC_DUR_WORDS) + bucket, 0x8000ull);
+    lds_add(wd, 0u - (0x8000u << sh));  // the field less 2^15 (no borrow: it is >= 2^15)
+  }
+  // the 32-bit LDS sum wrapped: 2^32 to the row's code-200 sum in HBM
+  __device__ __forceinline__ void sum_carry(uint32_t row) {
+    atomicAdd((unsigned long long *)(svc_tab + (uint64_t)dur_row(row) * ISIM_SVC_DUR_WORDS) + 2 * ISIM_N_PROM,
+              1ull << 32);
   }
 };
 
@@ -204,7 +221,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
   c.cnt = reinterpret_cast<uint32_t *>(lds + lay.off_cnt);
   c.n_slots = S;
-  unsigned long long *sum200 = reinterpret_cast<unsigned long long *>(lds + lay.off_sums);
+  uint32_t *sum200 = reinterpret_cast<uint32_t *>(lds + lay.off_sums);
   uint32_t *dyn = reinterpret_cast<uint32_t *>(lds + lay.off_dyn);
   const uint8_t *lut = lds + kLdsAccBytes + kHistWords * 4u;
   // zero the accumulators (everything before the nodes), copy the nodes in
@@ -355,7 +372,10 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       atomicMax(&c.acc->notmin, (unsigned long long)nmn);
     }
   }
-  if (lane_id() == 0 && atomicAdd(kp.work + kWorkQueues * kWorkLine, 1ull) == stride - 1) {
+  // (the wave count recomputed from the scalar launch sizes: kept from the
+  // prologue it was one VGPR pair spilled to scratch across the loop)
+  const uint64_t nwaves = (uint64_t)__builtin_amdgcn_readfirstlane(gridDim.x) * (blockDim.x >> 6);
+  if (lane_id() == 0 && atomicAdd(kp.work + kWorkQueues * kWorkLine, 1ull) == nwaves - 1) {
     for (uint32_t i = 0; i <= kWorkQueues; ++i) atomicExch(kp.work + i * kWorkLine, 0ull);
   }
   __syncthreads();
@@ -406,8 +426,10 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       }
     }
     for (uint32_t r = threadIdx.x; r < lay.n_sum; r += blockDim.x)
-      if (sum200[r]) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, sum200[r]);
-    // the varying LDS rows' bucket tables: one thread per (row, word)
+      if (sum200[r])
+        atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM,
+                  (unsigned long long)sum200[r]);
+    // the varying LDS rows' code-200 bucket tables (u16 pairs): one thread per (row, word)
     for (uint32_t i = threadIdx.x; i < kp.dyn_words; i += blockDim.x) {
       const uint32_t v = dyn[i];
       if (!v) continue;
@@ -420,8 +442,10 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       }
       const TreeDynRow d = kp.tree_dyn[lo];
       if (i == d.off) continue;  // the header
-      const uint32_t j = i - d.off - 1, code = j >= d.width ? 1u : 0u, b = d.b_lo + j - code * d.width;
-      atomicAdd(tab + (uint64_t)dur_row(d.row) * ISIM_SVC_DUR_WORDS + code * ISIM_N_PROM + b, (unsigned long long)v);
+      const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
+      unsigned long long *row = tab + (uint64_t)dur_row(d.row) * ISIM_SVC_DUR_WORDS;
+      if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));
+      if (v >> 16) atomicAdd(row + b + 1u, (unsigned long long)(v >> 16));
     }
     // the entry's row: its invocations are the traces (end-to-end histogram and sums)
     unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;

@@ -54,12 +54,16 @@ struct Item {
 
 struct Sink {
   std::vector<Item> *items;
+  std::vector<uint64_t> *dur_of;  // per item: its duration without contention
   uint64_t base;
   uint32_t t;
   void call(uint32_t) {}
   void resp_leaf(uint32_t, bool) {}
   void resp(uint32_t, uint32_t, uint32_t, bool) {}
-  void dur(uint32_t, uint32_t) {}
+  void dur(uint32_t hop, uint32_t T) {
+    if (dur_of->size() <= base + hop) dur_of->resize(base + hop + 1);
+    (*dur_of)[base + hop] = T;
+  }
   void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
     if (items->size() <= base + hop) items->resize(base + hop + 1);
     (*items)[base + hop] = Item{p, caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller), t,
@@ -113,13 +117,14 @@ int main(int argc, char **argv) {
   }
   // 2. pre-walk
   std::vector<Item> items;
+  std::vector<uint64_t> dur_of;
   std::vector<uint64_t> toff(n + 1, 0);
   std::vector<uint32_t> terr(n);
   {
     tw::Lane<kTreeMaxFrames + 1, false, true, false, true> L;
     const tw::CpuNodes nodes{prog.tree_nodes.data()};
     for (uint64_t t = 0; t < n; ++t) {
-      Sink s{&items, toff[t], (uint32_t)t};
+      Sink s{&items, &dur_of, toff[t], (uint32_t)t};
       L.start(begin + t);
       while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), s, (uint32_t)seed,
                              (uint32_t)(seed >> 32));
@@ -142,6 +147,23 @@ int main(int argc, char **argv) {
     qlist[p.qround].push_back(i);
     flist[p.fgroup].push_back(i);
   }
+  // the engine's own choices, restated: the first quiet pass of a cyclic
+  // schedule starts its cut step begins from the contention-free callee
+  // maxima (des_items.hip k_relmax), and a round the plan marks sort-free
+  // (DesPlan::round_nosort) takes its items in (position, item) order, a
+  // zero-hold item starting at its own arrival (k_pairs0)
+  dur_of.resize(M, 0);
+  std::vector<uint64_t> relmax(M * aw, 0);
+  for (uint64_t i = 0; i < M; ++i) {
+    const uint32_t par = items[i].par;
+    if (par == kNone) continue;
+    const DesItemPos &p = pl.item_pos[items[i].pos], &pp = pl.item_pos[items[par].pos];
+    if (pp.nsteps < 2) continue;
+    const uint64_t h = pl.pos[items[i].pos].off - (p.kstep == 0 ? pl.steps[pp.bk_first].add : 0ull);
+    uint64_t &m = relmax[(uint64_t)par * aw + p.kstep];
+    m = std::max(m, h + dur_of[i]);
+  }
+  bool first_pass = pl.cyclic;
   bool changed = false;
   auto store = [&](uint64_t &dst, uint64_t v) {
     if (dst != v) changed = true;
@@ -164,7 +186,8 @@ int main(int argc, char **argv) {
             v = IS[i];
           } else {
             v = bk[i * bw + s - 1] + st.smax;
-            const uint64_t c = ((sr & kDesStepCut) ? accp : acc)[i * aw + s - 1];
+            uint64_t c = ((sr & kDesStepCut) ? accp : acc)[i * aw + s - 1];
+            if ((sr & kDesStepCut) && first_pass) c = bk[i * bw + s - 1] + relmax[i * aw + s - 1];
             v = std::max(v, c);
           }
           store(bk[i * bw + s], v + st.add);
@@ -185,7 +208,11 @@ int main(int argc, char **argv) {
         IA[i] = a;
         uint32_t rep = 0;
         if (P.reps > 1) rep = draw0(begin + it.t, (uint32_t)(i - toff[it.t]), 0x80000002u, seed) % P.reps;
-        q.emplace_back(P.row, rep, a, i);
+        // sort-free round: the key is (position, item); a zero-hold item its own queue
+        if (pl.round_nosort[r])
+          q.emplace_back(it.pos, P.hold ? 0u : (uint32_t)i, P.hold ? i : 0u, i);
+        else
+          q.emplace_back(P.row, rep, a, i);
       }
       std::sort(q.begin(), q.end());
       for (size_t j = 0; j < q.size(); ++j) {
@@ -193,6 +220,7 @@ int main(int argc, char **argv) {
         const DesPos &P = pl.pos[items[i].pos];
         const bool first = j == 0 || std::get<0>(q[j - 1]) != std::get<0>(q[j]) ||
                            std::get<1>(q[j - 1]) != std::get<1>(q[j]);
+        if (pl.round_nosort[r]) std::get<2>(q[j]) = IA[i];
         const uint64_t a = std::get<2>(q[j]);
         const uint64_t free_at = first ? 0 : IS[std::get<3>(q[j - 1])] + P.hold;
         store(IS[i], std::max(a, free_at));
@@ -242,6 +270,7 @@ int main(int argc, char **argv) {
     for (; p < 256; ++p) {
       changed = false;
       pass(true);
+      first_pass = false;
       if (!changed) break;
     }
     if (p == 256) return 5;

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <map>
 #include <sstream>
 #include <vector>
 
@@ -31,7 +32,8 @@ struct Sink {
   std::vector<uint64_t> calls, errs;                // per slot
   std::vector<uint64_t> sum200, sum500;             // per row (HBM in the kernel, or its LDS sums)
   std::vector<std::vector<uint64_t>> gbucket;       // per row: [2][33] the global-atomic buckets
-  std::vector<uint32_t> dyn;                        // the LDS bucket tables (tree_dyn layout)
+  std::map<uint32_t, std::vector<uint64_t>> dyn;    // the LDS code-200 bucket tables, by header offset
+  std::map<uint32_t, uint32_t> hdr;                 // their header words (b_lo | width << 8)
   bool out_of_table = false;
   void call(uint32_t slot) { calls[slot] += 1; }
   void resp_leaf(uint32_t slot, bool st) {
@@ -45,12 +47,15 @@ struct Sink {
       (st ? sum500 : sum200)[idx] += T;
       return;
     }
-    if (place != kTreeStaticRow) {  // an LDS bucket table, with the range check made an error
-      const uint32_t lo = dyn[place] & 0xFFu, w = dyn[place] >> 8, b = prom_bucket_ns(T);
-      if (b < lo || b >= lo + w) out_of_table = true;
-      else dyn[place + 1 + (st ? w : 0) + (b - lo)] += 1;
+    const uint32_t row = prog->sum_row[idx];
+    if (place != kTreeStaticRow) {  // an LDS bucket table (code 200), with the range check made an error
+      std::vector<uint64_t> &tb = dyn.at(place);
+      const uint32_t lo = hdr.at(place) & 0xFFu, w = hdr.at(place) >> 8, b = prom_bucket_ns(T);
+      if (st) gbucket[row][ISIM_N_PROM + b] += 1;  // 500s: global atomics in the kernel
+      else if (b < lo || b >= lo + w) out_of_table = true;
+      else tb[b - lo] += 1;
     }
-    (st ? sum500 : sum200)[prog->sum_row[idx]] += T;
+    (st ? sum500 : sum200)[row] += T;
   }
 };
 }  // namespace
@@ -98,8 +103,10 @@ int main(int argc, char **argv) {
   sk.sum200.assign(R, 0);
   sk.sum500.assign(R, 0);
   sk.gbucket.assign(R, std::vector<uint64_t>(2 * ISIM_N_PROM, 0));
-  sk.dyn.assign(prog.tree_dyn_words, 0);
-  for (const TreeDynRow &d : prog.tree_dyn) sk.dyn[d.off] = d.b_lo | (d.width << 8);
+  for (const TreeDynRow &d : prog.tree_dyn) {
+    sk.hdr[d.off] = d.b_lo | (d.width << 8);
+    sk.dyn[d.off].assign(d.width, 0);
+  }
   std::vector<uint64_t> root_hist(2 * ISIM_N_PROM, 0), root_sum(2, 0);
   const bool modeb = p.error_mode == ISIM_MODE_B;
   // one Lane per depth variant, reused trace after trace as a GPU lane is
@@ -175,8 +182,7 @@ int main(int argc, char **argv) {
     for (uint32_t w = 0; w < 2 * ISIM_N_PROM; ++w) row[r][w] += sk.gbucket[r][w];
   }
   for (const TreeDynRow &d : prog.tree_dyn)
-    for (uint32_t code = 0; code < 2; ++code)
-      for (uint32_t j = 0; j < d.width; ++j) row[d.row][code * ISIM_N_PROM + d.b_lo + j] += sk.dyn[d.off + 1 + code * d.width + j];
+    for (uint32_t j = 0; j < d.width; ++j) row[d.row][d.b_lo + j] += sk.dyn[d.off][j];
   for (uint32_t s = 0; s < S; ++s) {  // the kernel's flush: static buckets and leaf sums from the counters
     const uint32_t w = prog.slot_tbkt[s], r = w & kTreeRowMask, b = w >> 24;
     if (b != kTreeDynBucket) {
