@@ -48,6 +48,9 @@ BENCH_BATCH = {
     # config 3's graph with a probability on every call: the lane tree walk
     # over a 10,000-position tree
     "c3p": 1 << 22,
+    # the same graph in the generator's sequential shape (a ~30 s latency
+    # bound: the lane tree walk with u64 time)
+    "c3s": 1 << 22,
     # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
     # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
     # the pipelined queue pass's fill and drain (2^16 20.8,
@@ -75,10 +78,10 @@ def parse():
     # 2^24 traces (256 MB of records) per launch: the per-launch flush and
     # tail amortise (config 3: 2^22 335, 2^23 339, 2^24 340 M traces/s)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c4", "c5", "c5p", "c4d"])
-    ap.add_argument("--prob", type=int, default=50, help="c3p: the probability on every call (1..99)")
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c3s", "c4", "c5", "c5p", "c4d"])
+    ap.add_argument("--prob", type=int, default=50, help="c3p / c3s: the probability on every call (1..99)")
     ap.add_argument("--no-wave-leg", action="store_true",
-                    help="c3p: skip the wave-interpreter leg (kinds 2/3, ISIM_FLAG_WAVE_WALK) on the same graph")
+                    help="c3p / c3s: skip the wave-interpreter leg (kinds 2/3, ISIM_FLAG_WAVE_WALK) on the same graph")
     ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
                     "fill the records (the library default) instead of walking every trace")
     ap.add_argument("--wide-rows", action="store_true", help="c5: 64-bit DES rows (default: 32-bit, "
@@ -102,8 +105,8 @@ def parse():
 
 
 def build_graph(config: str, prob: int = 50):
-    from isim.generators import (config2_topology, config3_topology, config3p_topology, mesh_des_topology,
-                                 mesh_topology)
+    from isim.generators import (config2_topology, config3_topology, config3p_topology, config3s_topology,
+                                 mesh_des_topology, mesh_topology)
     from isim.yamljson import obj_to_json, yaml_to_json
     if config == "c1":
         j = yaml_to_json(open(os.path.join(ROOT, "tests", "golden", "topologies", "canonical.yaml"), "rb").read())
@@ -122,6 +125,12 @@ def build_graph(config: str, prob: int = 50):
         j = obj_to_json(config3p_topology(prob))
         desc = {"workload": f"config 3's 10k-service graph with probability {prob} on every call (the reference "
                             "runtime's only randomness, executable.go:84-90): dynamic walk, lane tree walk",
+                "services": 10000, "probability": prob}
+    elif config == "c3s":
+        j = obj_to_json(config3s_topology(prob))
+        desc = {"workload": f"config 3's 10k-service graph in create_realistic_topology.py's sequential shape "
+                            f"(one call step per child) with probability {prob} on every call: dynamic walk with a "
+                            "~30 s latency bound, lane tree walk with u64 time",
                 "services": 10000, "probability": prob}
     elif config == "c5":
         j = obj_to_json(config3_topology())
@@ -678,7 +687,7 @@ def main():
     }
     if args.config == "c3" and args.mode == "A" and not args.no_mode_b:
         line.update(mode_b_legs(args, json_text, rank, world, dev, multi))
-    if args.config == "c3p" and not args.no_wave_leg:
+    if args.config in ("c3p", "c3s") and not args.no_wave_leg:
         line["wave_walk"] = wave_walk_leg(args, json_text, params, rank, world, dev, multi)
         line["speedup_vs_wave_walk"] = value / line["wave_walk"]["value"]
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -233,7 +233,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
     st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames,
                                   p.tree_frames > isim::kTreeRegFrames, p.tree_layout.nodes_lds != 0,
                                   (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
-                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"));
+                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"), p.tree_t64);
     st.lds_bytes = p.tree_layout.bytes;
     st.lds_counters = 1;
     // the workgroup size with the most resident waves per CU (registers and
@@ -368,7 +368,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
       // lane of a full grid; a launch waits for the area's previous launch
       // (launch_walk_one)
       st.spill_lanes = st.max_blocks * st.threads;
-      st.spill_words = (size_t)(p.tree_frames - 8u) * isim::kTreeSpillWords * st.spill_lanes;
+      st.spill_words = (size_t)(p.tree_frames - 8u) *
+                       (p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) * st.spill_lanes;
       HIPCHK(hipMalloc(&st.d_spill, st.spill_words * isim::kSpillAreas * sizeof(uint32_t)));
       for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
@@ -942,6 +943,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.d_ext = st->d_des_text;
     L.d_tstep = st->d_des_tstep;
     L.tree_frames = h->prog.tree_frames;
+    L.tree_t64 = h->prog.tree_t64 ? 1u : 0u;
     L.tree_flags = h->prog.tree_flags;
     L.n_nodes = (uint32_t)h->prog.tree_nodes.size();
     L.workspace = d_workspace;

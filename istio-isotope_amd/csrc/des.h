@@ -217,6 +217,7 @@ struct DesItemsLaunch {
   const uint32_t *d_step_round;              // [steps]
   const void *d_nodes, *d_ext, *d_tstep;     // the lane tree walk's TreeNode/TreeExt/TreeStep
   uint32_t tree_frames, tree_flags, n_nodes;
+  uint32_t tree_t64;  // the walk keeps u64 time (Program::tree_t64)
   void *workspace;
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;

@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -193,7 +194,8 @@ struct GNodes {
 struct CountSink {
   __device__ __forceinline__ void call(uint32_t) {}
   __device__ __forceinline__ void resp_leaf(uint32_t, bool) {}
-  __device__ __forceinline__ void resp(uint32_t, uint32_t, uint32_t, bool) {}
+  template <typename TT>
+  __device__ __forceinline__ void resp(uint32_t, uint32_t, TT, bool) {}
 };
 struct EmitSink : CountSink {
   uint32_t *epos, *eT;
@@ -206,7 +208,11 @@ struct EmitSink : CountSink {
     const uint32_t par = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
     erec[i] = (unsigned long long)par | (unsigned long long)(t | (own ? 0x80000000u : 0u)) << 32;
   }
-  __device__ __forceinline__ void dur(uint32_t hop, uint32_t T) { eT[base + hop] = T; }
+  // (a lower bound is all k_relmax needs: u64 durations saturate at 2^32 - 1)
+  template <typename TT>
+  __device__ __forceinline__ void dur(uint32_t hop, TT T) {
+    eT[base + hop] = (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
+  }
 };
 
 // One trace per lane; a lane whose trace has responded takes the next trace
@@ -223,12 +229,12 @@ struct LNodes {
   }
 };
 
-template <int FR, bool SPILL, bool EMIT, class Nodes>
+template <int FR, bool SPILL, bool EMIT, bool T64, class Nodes>
 __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *work, const Nodes &nodes) {
   // no error draws in the walk (DRAW = false): in mode A an invocation's own
   // error changes no skip, so the walks only need the skip residues; the
   // errors are drawn per item afterwards (k_own), fully parallel
-  tw::Lane<FR, false, true, SPILL, false> L;
+  tw::Lane<FR, false, true, SPILL, false, std::conditional_t<T64, uint64_t, uint32_t>> L;
   if constexpr (SPILL) {
     L.sp = k.spill + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
     L.sp_stride = gridDim.x * blockDim.x;
@@ -286,15 +292,16 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   }
 }
 
-template <int FR, bool SPILL, bool EMIT, bool LDSN>
+template <int FR, bool SPILL, bool EMIT, bool LDSN, bool T64>
 __global__ void __launch_bounds__(LDSN ? 1024 : kT) k_prewalk(K k, unsigned long long *work) {
   if constexpr (LDSN) {
     extern __shared__ unsigned long long s_nodes[];
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += blockDim.x) s_nodes[i] = k.nodes[i];
     __syncthreads();
-    prewalk_body<FR, SPILL, EMIT>(k, work, LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
+    prewalk_body<FR, SPILL, EMIT, T64>(k, work,
+                                       LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
   } else {
-    prewalk_body<FR, SPILL, EMIT>(k, work, GNodes{k.nodes});
+    prewalk_body<FR, SPILL, EMIT, T64>(k, work, GNodes{k.nodes});
   }
 }
 
@@ -1070,7 +1077,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *spill_buf = nullptr;
   const uint64_t pw_threads = (uint64_t)kPrewalkBlocks * kT;
   if (spill) {
-    const uint64_t words = (uint64_t)(fr - 8 + 1) * kTreeSpillWords * pw_threads;
+    const uint64_t words = (uint64_t)(fr - 8 + 1) * (L.tree_t64 ? kTreeSpillWords64 : kTreeSpillWords) * pw_threads;
     if (!pool_alloc(spill_mem, words * 4)) return fail("spill allocation");
     spill_buf = (uint32_t *)spill_mem.p;
   }
@@ -1088,33 +1095,27 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       hipLaunchKernelGGL(kern, dim3(kPrewalkBlocks), dim3(kT), 0, s, k, w);
     }
   };
-  auto prewalk = [&](bool emit) {
+  // the variant: register frames (8 + spill, 16, 8), nodes in LDS, time width
+  auto pw = [&](auto fr_c, auto spill_c, auto t64_c, bool emit) {
+    constexpr int FRc = decltype(fr_c)::value;
+    constexpr bool SP = decltype(spill_c)::value, T6 = decltype(t64_c)::value;
     unsigned long long *w = work + (emit ? 1 : 0);
-    if (spill) {
-      if (ldsn) {
-        if (emit) launch(k_prewalk<8, true, true, true>, w);
-        else launch(k_prewalk<8, true, false, true>, w);
-      } else {
-        if (emit) launch(k_prewalk<8, true, true, false>, w);
-        else launch(k_prewalk<8, true, false, false>, w);
-      }
-    } else if (fr > 8) {
-      if (ldsn) {
-        if (emit) launch(k_prewalk<16, false, true, true>, w);
-        else launch(k_prewalk<16, false, false, true>, w);
-      } else {
-        if (emit) launch(k_prewalk<16, false, true, false>, w);
-        else launch(k_prewalk<16, false, false, false>, w);
-      }
+    if (ldsn) {
+      if (emit) launch(k_prewalk<FRc, SP, true, true, T6>, w);
+      else launch(k_prewalk<FRc, SP, false, true, T6>, w);
     } else {
-      if (ldsn) {
-        if (emit) launch(k_prewalk<8, false, true, true>, w);
-        else launch(k_prewalk<8, false, false, true>, w);
-      } else {
-        if (emit) launch(k_prewalk<8, false, true, false>, w);
-        else launch(k_prewalk<8, false, false, false>, w);
-      }
+      if (emit) launch(k_prewalk<FRc, SP, true, false, T6>, w);
+      else launch(k_prewalk<FRc, SP, false, false, T6>, w);
     }
+  };
+  auto prewalk_t = [&](auto t64_c, bool emit) {
+    if (spill) pw(std::integral_constant<int, 8>{}, std::true_type{}, t64_c, emit);
+    else if (fr > 8) pw(std::integral_constant<int, 16>{}, std::false_type{}, t64_c, emit);
+    else pw(std::integral_constant<int, 8>{}, std::false_type{}, t64_c, emit);
+  };
+  auto prewalk = [&](bool emit) {
+    if (L.tree_t64) prewalk_t(std::true_type{}, emit);
+    else prewalk_t(std::false_type{}, emit);
   };
   if (hipMemsetAsync(work, 0, 16, s) != hipSuccess) return fail("memset");
   prewalk(false);

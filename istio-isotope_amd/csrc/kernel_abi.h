@@ -141,6 +141,7 @@ constexpr uint32_t kTreeMaxPositions = 0xFFFFu;  // u16 sizes and slots
 constexpr uint32_t kTreeRegFrames = 16;          // deepest register stack; deeper walks spill (kTreeMaxFrames)
 constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations below the current one
 constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
+constexpr uint32_t kTreeSpillWords64 = 7;        // ... with u64 time (acc and step max take two words each)
 constexpr uint32_t kSpillAreas = 4;              // spill areas per (handler, device): launches in flight
 // LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
 // workgroups per CU, and the whole CU.
@@ -219,15 +220,19 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters);
 // kind 7 variant (tree.hip, compiled once per mode and concurrency):
 // register-stack depth (4, 6, 8, 12, 16; `spill`: 8 registers + the rest in
 // global memory), nodes in LDS or global, the error-block cache.
-void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
-void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
-void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
-void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2);
-// occ2: the LDS layout fits two workgroups per CU (kernels built for 80 VGPRs)
-inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw, bool occ2) {
+void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
+void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
+void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
+void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
+// occ2: the LDS layout fits two workgroups per CU (kernels built for 80 VGPRs);
+// t64: u64 time (Program::tree_t64)
+inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw, bool occ2,
+                         bool t64) {
   if (modeb)
-    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2) : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2);
-  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2) : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2);
+    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2, t64)
+                : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2, t64);
+  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64)
+              : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64);
 }
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

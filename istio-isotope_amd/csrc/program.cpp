@@ -183,7 +183,10 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     out.tree_step.clear();
     out.tree_why = why;
   };
-  if (out.max_latency >= (1ull << 32)) return give_up("latency bound >= 2^32 ns (the tree walk keeps u32 time)");
+  // u64 time when the latency bound reaches 2^32 ns; each position's own
+  // figures (hop cost, callee time, step facts, leaf latency) stay 32-bit
+  out.tree_t64 = out.max_latency >= (1ull << 32);
+  constexpr uint64_t k32 = 1ull << 32;
   if (out.n_slots > (int32_t)kTreeMaxPositions) return give_up("more than 65535 call sites");
   const int32_t n = (int32_t)g.services.size();
   std::vector<ScriptTimes> shape(n);
@@ -246,6 +249,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e) | (probk0[e] ? TF_PROBK0 : 0));
   if (root.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
   TreeExt rx{};
+  if (own_time(e) >= k32) return give_up("a script whose time outside its call steps is >= 2^32 ns");
   rx.tc = (uint32_t)own_time(e);
   rx.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
   out.tree_nodes.push_back(root);
@@ -281,6 +285,8 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       if (row_bw[row]) row_through[row] += 1;
       const double heat = top.heat * (nd.prob ? nd.prob / 100.0 : 1.0);
       row_heat[row] += heat;
+      if (st.hop >= k32 || own_time(c) >= k32 || cs.pre >= k32 || cs.cmax0 >= k32)
+        return give_up("a hop cost, script time or step sleep >= 2^32 ns");
       TreeExt x{};
       x.H = (uint32_t)st.hop;
       x.tc = (uint32_t)own_time(c);
@@ -321,6 +327,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     const uint32_t r = (uint32_t)out.svc_row[s];
     const uint32_t b = (leaf[s] || !row_bw[r]) ? prom_bucket_ns(tmin[s]) : kTreeDynBucket;
     out.slot_tbkt[sl] = r | (leaf[s] ? kTreeLeafSlot : 0u) | (b << 24);
+    if (leaf[s] && out.svc_time[s] >= k32) return give_up("a leaf latency >= 2^32 ns");
     out.slot_tc[sl] = leaf[s] ? (uint32_t)out.svc_time[s] : 0u;
   }
   out.tree_mult = 1;

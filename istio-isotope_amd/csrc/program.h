@@ -59,6 +59,7 @@ struct Program {
   std::vector<uint32_t> tree_row_place, tree_row_index, tree_row_blo;  // per row (place_tree)
   TreeLayout tree_layout{};
   uint32_t tree_frames = 0;         // frames the walk needs (open calling invocations - 1)
+  bool tree_t64 = false;            // the latency bound reaches 2^32 ns: the walk keeps u64 time
   uint32_t tree_mult = 0;           // most positions through one slot or into one bucket-table row (LDS u32
                                     // counter overflow guard)
   uint32_t tree_flags = 0;          // kTreeAnyProb | kTreeAnyDraw | kTreeAnyConc

@@ -73,6 +73,9 @@ __device__ __forceinline__ uint32_t lut_bucket(const uint8_t *lut, uint32_t t) {
   const uint32_t c = t < 500000001u ? t : 500000001u;
   return ((const __attribute__((address_space(3))) uint8_t *)lut)[(c + 999999u) / 1000000u];
 }
+__device__ __forceinline__ uint32_t lut_bucket(const uint8_t *lut, uint64_t t) {
+  return lut_bucket(lut, (uint32_t)(t < 500000001ull ? t : 500000001ull));
+}
 
 // Node accessors of tree_walk.h: LDS (ds_read_b64) or global memory
 // (global_load_dwordx2, L2-resident).
@@ -155,7 +158,10 @@ struct TreeSink {
 #endif
     if (st) count(slot, true);
   }
-  __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
+  // T: the callee's duration (u32, or u64 in the walks whose latency bound
+  // reaches 2^32 ns: a duration of 2^32 ns or more adds to the row's sum in HBM)
+  template <typename TT>
+  __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, TT T, bool st) {
 #ifdef TREE_NO_SINK
     return;
 #endif
@@ -188,8 +194,15 @@ struct TreeSink {
       const uint32_t old = lds_add_rtn(wd, 1u << sh);
       if (((old >> sh) & 0xFFFFu) == 0x7FFFu) bucket_move(wd, sh, sum_row[idx], lo + b);
     }
-    const uint32_t o = lds_add_rtn(sum200 + idx, T);
-    if (o + T < o) sum_carry(sum_row[idx]);
+    if (sizeof(TT) == 8 && ((uint64_t)T >> 32)) {
+      atomicAdd((unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS) +
+                    2 * ISIM_N_PROM,
+                (unsigned long long)T);
+      return;
+    }
+    const uint32_t t32 = (uint32_t)T;
+    const uint32_t o = lds_add_rtn(sum200 + idx, t32);
+    if (o + t32 < o) sum_carry(sum_row[idx]);
   }
   // a u16 bucket field reached 2^15: 2^15 of its counts go to the row in HBM
   __device__ __forceinline__ void bucket_move(uint32_t *wd, uint32_t sh, uint32_t row, uint32_t bucket) {
@@ -206,10 +219,12 @@ struct TreeSink {
 // WPE: waves per SIMD the register allocation must allow — 6 (80 VGPRs: two
 // 768-thread workgroups per CU) when the LDS layout fits half the CU, else 4
 // (one 1024-thread workgroup per CU: up to 128 VGPRs, no spills).
-template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE>
+// T64: u64 time (a latency bound of 2^32 ns or more; tree_walk.h Lane TT).
+template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE, bool T64 = false>
 __global__ void __launch_bounds__(kWgThreads, WPE)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
+  using TT = std::conditional_t<T64, uint64_t, uint32_t>;
   extern __shared__ __align__(16) unsigned char lds[];
   const uint32_t S = kp.n_slots, P = kp.n_pos;
   const TreeLayout &lay = kp.lay;
@@ -282,7 +297,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   bool dry = b >= n_batches;
   uint64_t nxt = dry ? 0 : b * 64, lim = dry ? 0 : (b * 64 + 64 < n ? b * 64 + 64 : n);
   const uint64_t lt = ((uint64_t)1 << lane_id()) - 1;  // lanes below this one
-  tw::Lane<FRAMES, MODEB, CONC, SPILL, DRAW> L;
+  tw::Lane<FRAMES, MODEB, CONC, SPILL, DRAW, TT> L;
   if constexpr (SPILL) {
     L.sp = kp.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     L.sp_stride = kp.spill_lanes;
@@ -292,27 +307,29 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   // per-lane sums in 32 bits (a latency sum that wraps carries 2^32 into the
   // workgroup's u64 accumulator at once); trace and 500 counts follow from
   // the histograms at the flush
-  uint32_t a_lat = 0, a_lat500 = 0, a_hops = 0, a_err = 0, a_max = 0, a_min = 0xFFFFFFFFu;
+  // (u64 time: u64 per-lane sums, no carries)
+  TT a_lat = 0, a_lat500 = 0, a_max = 0, a_min = ~(TT)0;
+  uint32_t a_hops = 0, a_err = 0;
   while (true) {
     // responded traces: record, histograms, sums
     const uint64_t fin = ballot(active && L.done);
     if (fin) {
       const bool mine = lane_in(fin);
-      const uint32_t lat = L.lat;
+      const TT lat = L.lat;
       const bool is500 = L.root500;
       if (mine) {
         uint4 r;
-        r.x = lat;
-        r.y = 0u;
+        r.x = (uint32_t)lat;
+        r.y = T64 ? (uint32_t)((uint64_t)lat >> 32) : 0u;
         r.z = L.hops();
         r.w = (is500 ? 0x80000000u : 0u) | L.errs();
         if (c.records) *reinterpret_cast<uint4 *>(c.records + idx) = r;
-        const uint32_t nl = a_lat + lat;
-        if (nl < a_lat) lds_add(&c.acc->sum_latency, 1ull << 32);
+        const TT nl = a_lat + lat;
+        if (!T64 && nl < a_lat) lds_add(&c.acc->sum_latency, 1ull << 32);
         a_lat = nl;
         if (is500) {
-          const uint32_t n5 = a_lat500 + lat;
-          if (n5 < a_lat500) lds_add(&c.acc->sum_latency500, 1ull << 32);
+          const TT n5 = a_lat500 + lat;
+          if (!T64 && n5 < a_lat500) lds_add(&c.acc->sum_latency500, 1ull << 32);
           a_lat500 = n5;
         }
         a_hops += L.hops();
@@ -326,7 +343,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       // buckets mostly differ, so a wave-aggregated add would loop per bucket)
       if (mine) {
         lds_add(c.hist + (is500 ? ISIM_N_PROM : 0u) + lut_bucket(lut, lat), 1u);
-        const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll(lat);
+        const uint32_t l2 = lat == 0 ? 0u : 64u - (uint32_t)__builtin_clzll((uint64_t)lat);
         lds_add(c.hist + 2 * ISIM_N_PROM + (is500 ? ISIM_N_LOG2 : 0u) + l2, 1u);
       }
 #endif
@@ -362,7 +379,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   {
     const uint64_t s_lat = wave_sum64(a_lat), s_hops = wave_sum64(a_hops), s_err = wave_sum64(a_err);
     const uint64_t s_500 = wave_sum64(a_lat500);
-    const uint64_t mx = wave_max64(a_max), nmn = wave_max64(~(uint64_t)a_min);
+    const uint64_t mx = wave_max64(a_max), nmn = wave_max64(T64 ? ~(uint64_t)a_min : ~(uint64_t)(uint32_t)a_min);
     if (lane_id() == 0) {
       lds_add(&c.acc->sum_latency, (unsigned long long)s_lat);
       lds_add(&c.acc->sum_hops, (unsigned long long)s_hops);
@@ -486,9 +503,14 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
 #define TREE_WPE2 6
 #endif
 template <bool NLDS, bool DRAW>
-static void *tree_pick(uint32_t frames, bool spill, bool occ2) {
+static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
+  if (t64) {  // u64 time: register stacks of 8 or 16 frames, or 8 + the spill; 4 waves per SIMD
+    if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW, 4, true>;
+    if (frames <= 8) return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, 4, true>;
+    return (void *)&isim_tree<M, 16, false, NLDS, C, DRAW, 4, true>;
+  }
   if (occ2 && !spill && frames <= 8) {
     if (frames <= 4) return (void *)&isim_tree<M, 4, false, NLDS, C, DRAW, TREE_WPE2>;
     if (frames <= 6) return (void *)&isim_tree<M, 6, false, NLDS, C, DRAW, TREE_WPE2>;
@@ -505,9 +527,10 @@ static void *tree_pick(uint32_t frames, bool spill, bool occ2) {
 #define TREE_CAT2(a, b, c) a##b##c
 #define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
 void *TREE_CAT(tree_kernel_m, TREE_MODEB, TREE_CAT(c, TREE_CONC, ))(uint32_t frames, bool spill, bool nodes_lds,
-                                                                      bool draw, bool occ2) {
-  if (nodes_lds) return draw ? tree_pick<true, true>(frames, spill, occ2) : tree_pick<true, false>(frames, spill, occ2);
-  return draw ? tree_pick<false, true>(frames, spill, occ2) : tree_pick<false, false>(frames, spill, occ2);
+                                                                      bool draw, bool occ2, bool t64) {
+  if (nodes_lds)
+    return draw ? tree_pick<true, true>(frames, spill, occ2, t64) : tree_pick<true, false>(frames, spill, occ2, t64);
+  return draw ? tree_pick<false, true>(frames, spill, occ2, t64) : tree_pick<false, false>(frames, spill, occ2, t64);
 }
 
 }  // namespace isim

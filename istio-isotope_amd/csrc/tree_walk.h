@@ -159,25 +159,31 @@ struct has_exec<S, decltype((void)&S::exec)> {
 // global memory, one column per lane; the CPU check: a vector).
 // DRAW: some callee draws its error against a threshold (without, no error
 // block is cached: 5 registers fewer).
-template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true>
+// TT: the time type — uint32_t when the walk's latency bound is below 2^32
+// ns, else uint64_t (round 5: a sequential 10k-service tree's bound is ~30 s;
+// every position's own H, tc and step facts still fit 32 bits, program.cpp)
+template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true, typename TT = uint32_t>
 struct Lane {
+  // u32 words of a spilled frame: pos|end, hop|flags, residues, time, step max
+  static constexpr uint32_t kSW = sizeof(TT) == 8 ? kTreeSpillWords64 : kTreeSpillWords;
   uint32_t t_lo = 0, t_hi = 0;
   uint32_t p = 0, d = 0, end = 0;
   uint32_t he = 0;  // executed invocations (hop ids handed out) | invocations that responded 500 << 16
   bool done = true;
-  uint32_t lat = 0;
+  TT lat = 0;
   bool root500 = false;
   // current invocation: f_hf = hop | fl << 16 (fl: FL_* | call block of f_res << KB_SHIFT), packed
   // as its frame is (one register fewer; HF() shifts a flag into place)
-  uint32_t f_pos = 0, f_acc = 0, f_cmax = 0, f_hf = 0, f_res = 0;
+  uint32_t f_pos = 0, f_hf = 0, f_res = 0;
+  TT f_acc = 0, f_cmax = 0;
   static constexpr uint32_t HF(uint32_t fl) { return fl << 16; }
   ISIM_TW uint32_t hops() const { return he & 0xFFFFu; }
   ISIM_TW uint32_t errs() const { return he >> 16; }
   ISIM_TW uint32_t f_kb() const { return (f_hf >> (16 + KB_SHIFT)) & KB_NONE; }
   ISIM_TW void set_kb(uint32_t kb) { f_hf = (f_hf & ~HF(KB_NONE << KB_SHIFT)) | HF(kb << KB_SHIFT); }
   // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time
-  uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1],
-      s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
+  uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1];
+  TT s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
   uint32_t *sp = nullptr;  // SPILL: this lane's column of the spill area
   uint32_t sp_stride = 1;
   // cached error block: words of Philox (t, ek_blk, 0, 0)
@@ -223,7 +229,7 @@ struct Lane {
     f_hf = 0;
   }
 
-  ISIM_TW void fold(uint32_t c, bool st, bool conc) {
+  ISIM_TW void fold(TT c, bool st, bool conc) {
     if (CONC && conc) {
       f_cmax = c > f_cmax ? c : f_cmax;
       if (MODEB && st) f_hf |= HF(FL_CERR);
@@ -236,12 +242,16 @@ struct Lane {
   ISIM_TW void push() {
     const uint32_t pe = f_pos | (end << 16), hf = f_hf;
     if (SPILL && d >= (uint32_t)FRAMES) {
-      uint32_t *q = sp + (d - (uint32_t)FRAMES) * kTreeSpillWords * sp_stride;
+      uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
       q[0] = pe;
       q[sp_stride] = hf;
       q[2 * sp_stride] = f_res;
-      q[3 * sp_stride] = f_acc;
-      q[4 * sp_stride] = f_cmax;
+      q[3 * sp_stride] = (uint32_t)f_acc;
+      q[4 * sp_stride] = (uint32_t)f_cmax;
+      if constexpr (sizeof(TT) == 8) {
+        q[5 * sp_stride] = (uint32_t)((uint64_t)f_acc >> 32);
+        q[6 * sp_stride] = (uint32_t)((uint64_t)f_cmax >> 32);
+      }
     } else {
 TW_PRAGMA_UNROLL
       for (int i = 0; i < FRAMES; ++i) {
@@ -258,14 +268,19 @@ TW_PRAGMA_UNROLL
 
   ISIM_TW void pop() {
     --d;
-    uint32_t pe = 0, hf = 0, r = 0, a = 0, c = 0;
+    uint32_t pe = 0, hf = 0, r = 0;
+    TT a = 0, c = 0;
     if (SPILL && d >= (uint32_t)FRAMES) {
-      const uint32_t *q = sp + (d - (uint32_t)FRAMES) * kTreeSpillWords * sp_stride;
+      const uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
       pe = q[0];
       hf = q[sp_stride];
       r = q[2 * sp_stride];
       a = q[3 * sp_stride];
       c = q[4 * sp_stride];
+      if constexpr (sizeof(TT) == 8) {
+        a |= (TT)((uint64_t)q[5 * sp_stride] << 32);
+        c |= (TT)((uint64_t)q[6 * sp_stride] << 32);
+      }
     } else {
 TW_PRAGMA_UNROLL
       for (int i = 0; i < FRAMES; ++i) {
@@ -290,7 +305,7 @@ TW_PRAGMA_UNROLL
   // only, TF_XPRE: mode A folds it into the caller's tc —, a concurrent step
   // starts) on copies of the frame's time and flags; returns false when the
   // script has failed (mode B: it runs no further step).
-  ISIM_TW bool step_begin(const NodeW &n, const TreeStep *stp, uint32_t &acc, uint32_t &fl, uint32_t &cm) const {
+  ISIM_TW bool step_begin(const NodeW &n, const TreeStep *stp, TT &acc, uint32_t &fl, TT &cm) const {
     if (!(n.flags() & TF_STEP)) return true;
     if (CONC && (fl & HF(FL_INCONC))) {
       acc += cm;
@@ -317,7 +332,8 @@ TW_PRAGMA_UNROLL
   // close f_pos: its response folds into its caller (false: the entry responded)
   template <class Nodes, class Sink>
   ISIM_TW bool close(const Nodes &nodes, const TreeExt *ext, Sink &sink) {
-    uint32_t T = f_acc, fl = f_hf;
+    TT T = f_acc;
+    uint32_t fl = f_hf;
     if (CONC && (fl & HF(FL_INCONC))) {
       T += f_cmax;
       if (MODEB && (fl & HF(FL_CERR))) fl |= HF(FL_FAILED);
@@ -335,7 +351,7 @@ TW_PRAGMA_UNROLL
     }
     sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
     if constexpr (has_exec<Sink>::value) sink.dur(f_hf & 0xFFFFu, T);
-    const uint32_t c = x.H + T;
+    const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
     pop();
     fold(c, st, cc);
@@ -380,7 +396,7 @@ TW_PRAGMA_UNROLL
       }
       sink.resp_leaf(n.slot(), own);
       if constexpr (has_exec<Sink>::value) sink.dur(hop, x.tc);
-      fold(x.H + x.tc, own, (fl & TF_CONC) != 0);
+      fold((TT)x.H + x.tc, own, (fl & TF_CONC) != 0);
       p += 1;
       return;
     }
@@ -403,7 +419,8 @@ TW_PRAGMA_UNROLL
   ISIM_TW bool scan(const Nodes &nodes, const TreeStep *stp) {
     const NodeW n = nodes.load(p);
     if (!n.prob() || f_kb() != ((uint32_t)n.k() >> 2) || !skipped(n)) return false;
-    uint32_t acc = f_acc, fl = f_hf, cm = f_cmax;
+    TT acc = f_acc, cm = f_cmax;
+    uint32_t fl = f_hf;
     if (!step_begin(n, stp, acc, fl, cm)) return false;
     f_acc = acc;
     f_hf = fl;

@@ -170,6 +170,16 @@ def config3p_topology(probability: int = 50, n: int = 10_000, seed: int = 42) ->
                               error_rate=(0.0, 0.01), probability=probability)
 
 
+def config3s_topology(probability: int = 50, n: int = 10_000, seed: int = 42) -> Dict[str, Any]:
+    """Config 3's graph in the reference generator's SEQUENTIAL shape (each
+    child called in its own step, create_realistic_topology.py:176-182) with
+    config 3's sleeps and error rates and `probability` on every call: the
+    latency bound is ~30 s, past the u32 nanosecond clock, so the lane tree
+    walk keeps u64 time (bench.py --config c3s)."""
+    return realistic_topology(n, "multitier", seed, concurrent=False, sleep_ms=(1, 5),
+                              error_rate=(0.0, 0.01), probability=probability)
+
+
 def config2_topology() -> Dict[str, Any]:
     """BASELINE config 2: tree depth 4 x fan-out 8, sequential requests."""
     return tree_topology(4, 8, sequential=True)

@@ -59,8 +59,8 @@ struct Sink {
   uint32_t t;
   void call(uint32_t) {}
   void resp_leaf(uint32_t, bool) {}
-  void resp(uint32_t, uint32_t, uint32_t, bool) {}
-  void dur(uint32_t hop, uint32_t T) {
+  void resp(uint32_t, uint32_t, uint64_t, bool) {}
+  void dur(uint32_t hop, uint64_t T) {
     if (dur_of->size() <= base + hop) dur_of->resize(base + hop + 1);
     (*dur_of)[base + hop] = T;
   }
@@ -121,7 +121,7 @@ int main(int argc, char **argv) {
   std::vector<uint64_t> toff(n + 1, 0);
   std::vector<uint32_t> terr(n);
   {
-    tw::Lane<kTreeMaxFrames + 1, false, true, false, true> L;
+    tw::Lane<kTreeMaxFrames + 1, false, true, false, true, uint64_t> L;
     const tw::CpuNodes nodes{prog.tree_nodes.data()};
     for (uint64_t t = 0; t < n; ++t) {
       Sink s{&items, &dur_of, toff[t], (uint32_t)t};

@@ -39,7 +39,7 @@ struct Sink {
   void resp_leaf(uint32_t slot, bool st) {
     if (st) errs[slot] += 1;
   }
-  void resp(uint32_t slot, uint32_t roww, uint32_t T, bool st) {
+  void resp(uint32_t slot, uint32_t roww, uint64_t T, bool st) {
     const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
     if (st) errs[slot] += 1;
     if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // as tree.hip TreeSink::resp: a row in global memory
@@ -121,10 +121,20 @@ int main(int argc, char **argv) {
   tw::Lane<8, false> a8;
   tw::Lane<16, false> a16;
   tw::Lane<8, false, true, true> as;
+  // u64 time (Program::tree_t64): the kernel's 8- and 16-frame and spilling variants
+  tw::Lane<8, true, true, false, true, uint64_t> c8;
+  tw::Lane<16, true, true, false, true, uint64_t> c16;
+  tw::Lane<8, true, true, true, true, uint64_t> cs;
+  tw::Lane<8, false, true, false, true, uint64_t> d8;
+  tw::Lane<16, false, true, false, true, uint64_t> d16;
+  tw::Lane<8, false, true, true, true, uint64_t> ds;
+  std::vector<uint32_t> spill64((size_t)kTreeMaxFrames * kTreeSpillWords64, 0);
   bs.sp = as.sp = spill.data();
+  cs.sp = ds.sp = spill64.data();
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
   for (uint64_t i = 0; i < n; ++i) {
-    uint32_t lat = 0, hops = 0, errh = 0;
+    uint64_t lat = 0;
+    uint32_t hops = 0, errh = 0;
     bool r500 = false;
     auto run = [&](auto &L) {
       L.start(begin + i);
@@ -137,7 +147,17 @@ int main(int argc, char **argv) {
     // the register-stack depth the device compiles for this graph (tree.hip tree_kernel)
     const uint32_t fr = prog.tree_frames;
     const bool spills = fr > kTreeRegFrames || std::getenv("ISIM_TW_SPILL") != nullptr;
-    if (modeb) {
+    if (prog.tree_t64) {
+      if (modeb) {
+        if (spills) run(cs);
+        else if (fr <= 8) run(c8);
+        else run(c16);
+      } else {
+        if (spills) run(ds);
+        else if (fr <= 8) run(d8);
+        else run(d16);
+      }
+    } else if (modeb) {
       if (spills) run(bs);
       else if (fr <= 4) run(b4);
       else if (fr <= 8) run(b8);
@@ -148,7 +168,7 @@ int main(int argc, char **argv) {
       else if (fr <= 8) run(a8);
       else run(a16);
     }
-    std::printf("rec %u %u %d %u\n", lat, hops, r500 ? 1 : 0, errh);
+    std::printf("rec %llu %u %d %u\n", (unsigned long long)lat, hops, r500 ? 1 : 0, errh);
     root_hist[(r500 ? ISIM_N_PROM : 0) + prom_bucket_ns(lat)] += 1;
     root_sum[r500 ? 1 : 0] += lat;
   }

@@ -76,6 +76,8 @@ CASES = {
     "real300p60": lambda: realistic_topology(300, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.3),
                                              probability=60),
     "real300seq_p75": lambda: realistic_topology(300, sleep_ms=(1, 5), error_rate=(0.0, 0.3), probability=75),
+    # a latency bound past 2^32 ns: the pre-walk keeps u64 time (Program::tree_t64)
+    "real300seq_t64": lambda: realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.3), probability=75),
     "mesh_des": lambda: mesh_des_topology(4000, 6, 3, 40),
     "canonical_p50": lambda: _sleepy(_prob_canonical()),
     "tree_reps_p70": lambda: _with_prob(_sleepy_tree(3, 4, reps_leaves=3), 70),
@@ -271,3 +273,15 @@ def test_items_c4d_bench_batch(gpu):
     assert np.array_equal(np.asarray(fd["svc_calls"]), np.asarray(fw["svc_calls"]))
     assert np.array_equal(np.asarray(fd["svc_errs"]), np.asarray(fw["svc_errs"]))
     assert fd["n_traces"] == n and fd["sum_hops"] == fw["sum_hops"]
+
+
+def test_items_c3s_u64_walk(gpu):
+    """c3s (config 3's 10k graph in the generator's
+    sequential shape at probability 50; a ~30 s latency bound, the lane tree
+    walk's u64 time) is in the item engine's DES class: 4,000 traces at the
+    config-5 load bit-exact against des_oracle.c."""
+    import bench
+    j, _ = bench.build_graph("c3s")
+    c = DesCase(j, 6_000_000)
+    assert c.d.info.items == 1 and c.h.info.time_bits == 64
+    c.compare(1 << 20, 4000)

@@ -287,3 +287,23 @@ def test_config3p_bench_batch(gpu, prob):
     _launch_edge_windows(c, rec, begin, n, L, width=128)
     _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=9)
     c.compare(begin + n - 2048, 4096)
+
+
+def test_config3s_bench_batch(gpu):
+    """c3s exactly as bench.py times it: config 3's 10k
+    graph in the generator's sequential shape at probability 50, whose ~30 s
+    latency bound needs u64 time — on the lane tree walk (kind 7), not the
+    wave interpreter — BENCH_BATCH["c3s"] traces per launch, two launches
+    into one stats buffer; oracle windows at every launch edge and split,
+    sampled windows, and the full stats of a window."""
+    j, _ = bench.build_graph("c3s", 50)
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    assert c.handler.info.time_bits == 64 and c.handler.info.max_latency_ns >= 1 << 32
+    assert c.handler.launch_info(0)["kernel_kind"] == 7
+    n, L = bench.BENCH_BATCH["c3s"], 2
+    begin = (1 << 33) - n // 2
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    _launch_edge_windows(c, rec, begin, n, L, width=128)
+    _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=11)
+    c.compare(begin + n - 2048, 4096)

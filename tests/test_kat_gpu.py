@@ -45,7 +45,8 @@ def test_kat_hip(gpu, case, kernel):
     if kernel == "dynamic_wave":
         assert kind in (2, 3)
     elif kernel.startswith("dynamic"):
-        assert kind == (7 if h.info.time_bits == 32 else 3)
+        # the lane tree walk (u32 or u64 time); kind 3 only when a position's own time reaches 2^32 ns
+        assert kind == 7 or (h.info.time_bits == 64 and kind == 3)
     elif kernel == "interp":
         assert kind in (0, 1) or not h.info.static_walk
     n = 3000

@@ -19,7 +19,7 @@ from hypothesis import strategies as st
 
 import kat
 from conftest import ROOT, TOPOLOGIES
-from isim.generators import config3p_topology, mesh_topology, realistic_topology
+from isim.generators import config3p_topology, config3s_topology, mesh_topology, realistic_topology
 from isim.yamljson import obj_to_json, yaml_to_json
 from oracle import executor as oc
 from oracle import graph_ref as gr
@@ -199,3 +199,27 @@ def test_spill_variant(checker, tmp_path, mode, monkeypatch):
     assert compare(checker, tmp_path, obj_to_json(deep), mode, n=300)
     assert compare(checker, tmp_path, with_defaults(obj_to_json(mesh_topology(1200, 11, fanout=2, seed=5, probability=70)),
                                                     errorRate=0.05), mode, n=1000)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_u64_time(checker, tmp_path, mode):
+    """Walks whose latency bound reaches 2^32 ns keep u64 time (round 5,
+    Program::tree_t64): config 3's 10k graph in the generator's sequential
+    shape at probability 50 (c3s: a ~30 s bound, frames spill), a 2,000-service
+    sequential graph with probabilities on a third of the services, and a
+    chain of 1.5 s sleeps whose traces themselves exceed 2^32 ns."""
+    j = obj_to_json(config3s_topology(50))
+    assert compare(checker, tmp_path, j, mode, n=120, begin=(1 << 32) - 50)
+    d = realistic_topology(2000, "multitier", seed=3, concurrent=False, sleep_ms=(1, 5), error_rate=(0, 0.05))
+    for i, s in enumerate(d["services"]):
+        if i % 3 == 0:
+            s["script"] = [({"call": {"service": c["call"], "probability": 60}} if isinstance(c, dict) and "call" in c
+                            else c) for c in s["script"]]
+    assert compare(checker, tmp_path, obj_to_json(d), mode, n=200)
+    svcs = [{"name": f"s{i}", "errorRate": 0.1,
+             "script": [{"sleep": "1500ms"}] + ([[{"call": {"service": f"s{i + 1}", "probability": 90}},
+                                              {"call": f"s{i + 1}"}]] if i < 3 else [])} for i in range(4)]
+    svcs[0]["isEntrypoint"] = True
+    got = run_check(checker, tmp_path, json.dumps({"services": svcs}), mode, n=50)
+    assert got is not None and max(r[0] for r in got[0]) > 1 << 32
+    assert compare(checker, tmp_path, json.dumps({"services": svcs}), mode, n=400)

@@ -34,11 +34,11 @@ STREAM_KINDS = (4, 5, 6)
 
 
 def dynamic_kind(handler, flags):
-    """Kernel kind a dynamic walk takes: 7 (lane tree walk) unless the wave
-    walk is asked for or the tree does not fit (u64 time), else 2/3."""
-    tb64 = handler.info.time_bits == 64
-    if (flags & isim.native.FLAG_WAVE_WALK) or tb64:
-        return 2 + int(tb64)
+    """Kernel kind a dynamic walk takes: 7 (the lane tree walk, u32 or — a
+    latency bound of 2^32 ns or more — u64 time) unless the wave walk is
+    asked for: then 2/3 by the time width."""
+    if flags & isim.native.FLAG_WAVE_WALK:
+        return 2 + int(handler.info.time_bits == 64)
     return 7
 
 
@@ -172,7 +172,10 @@ def test_realistic_sequential_probability(gpu):
                            for c in s["script"]]
     j = obj_to_json(d)
     for mode in (isim.MODE_A, isim.MODE_B):
-        Case(j, None, isim.SimParams(error_mode=mode)).compare(0, 2000)
+        c = Case(j, None, isim.SimParams(error_mode=mode))
+        # a ~6.5 s latency bound: the lane tree walk with u64 time (round 5), no longer kinds 2/3
+        assert c.handler.info.time_bits == 64 and c.handler.launch_info(0)["kernel_kind"] == 7
+        c.compare(0, 2000)
 
 
 def test_mesh_config4(gpu):
@@ -362,3 +365,25 @@ def test_tree_spill_two_streams(gpu):
         assert fk["n_traces"] == k * n and fk["sum_latency"] == k * f1["sum_latency"]
         assert fk["sum_hops"] == k * f1["sum_hops"] and fk["n_500"] == k * f1["n_500"]
         assert np.array_equal(fk["site_calls"], k * f1["site_calls"])
+
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_tree_u64_time(gpu, mode):
+    """The lane tree walk with u64 time (Program::tree_t64): a chain of 1.5 s
+    sleeps with probabilistic concurrent calls, whose traces exceed 2^32 ns,
+    bit-exact against the oracle — records (both latency words), stats and
+    the per-service duration rows (durations past 2^32 ns go to their
+    row's sum in HBM) — on the kernel kind 7, next to the wave interpreter
+    (kind 3) on the same graph."""
+    svcs = [{"name": f"s{i}", "errorRate": 0.1,
+             "script": [{"sleep": "1500ms"}] + ([[{"call": {"service": f"s{i + 1}", "probability": 90}},
+                                                  {"call": f"s{i + 1}"}]] if i < 3 else [])} for i in range(4)]
+    svcs[0]["isEntrypoint"] = True
+    j = json.dumps({"services": svcs})
+    c = Case(j, None, isim.SimParams(error_mode=mode))
+    assert c.handler.info.time_bits == 64 and c.handler.launch_info(0)["kernel_kind"] == 7
+    recs, _ = c.compare((1 << 32) - 1000, 3000)
+    assert int(recs["latency_ns"].max()) > 1 << 32
+    w = Case(j, None, isim.SimParams(error_mode=mode, flags=isim.native.FLAG_WAVE_WALK))
+    assert w.handler.launch_info(0)["kernel_kind"] == 3
+    w.compare(7, 1000)
