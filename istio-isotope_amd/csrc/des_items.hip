@@ -153,6 +153,16 @@ struct K {
   uint32_t quiet;
   uint32_t *changed;
   uint32_t first;                  // the first quiet pass: acc_prev holds contention-free relative maxima
+  // incremental quiet passes (round 5): traces in chunks of 2^cshift; a pass
+  // recomputes the step begins, arrivals and finishes of the items whose
+  // chunk had a value change in the previous pass (dcur; null: every item),
+  // and marks the chunks whose values it changes (dnext).  Queue scans stay
+  // whole-round (a change moves later traces of the queue: their chunks are
+  // marked as their starts change)
+  const uint8_t *dcur;
+  uint8_t *dnext;
+  uint32_t cshift;
+  uint16_t *irep;                  // per item: its replica (drawn once per batch)
   uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
   uint32_t count_changes;          // ISIM_DES_DEBUG: changed[1] counts the values a quiet pass changed
 };
@@ -160,9 +170,10 @@ struct K {
 // a quiet pass flags a change with ONE atomic per wave, and none once the
 // flag is set (millions of lanes changing values in the first passes would
 // otherwise serialise on the flag's address)
-__device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v) {
+__device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v, uint32_t item) {
   if (k.changed) {
     const bool diff = *p != v;
+    if (diff && k.dnext) k.dnext[k.itr[item] >> k.cshift] = 1;
     const unsigned long long m = __ballot(diff);
     if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1u) {
       // ISIM_DES_DEBUG: count the changed values (one atomic per wave)
@@ -174,6 +185,8 @@ __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t 
 }
 
 __device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * kT + threadIdx.x; }
+// the item is recomputed in this pass (its chunk changed in the previous one)
+__device__ __forceinline__ bool live(const K &k, uint32_t i) { return !k.dcur || k.dcur[k.itr[i] >> k.cshift]; }
 __device__ __forceinline__ uint64_t nthreads() { return (uint64_t)gridDim.x * kT; }
 __device__ __forceinline__ uint64_t item_off(const K &k, uint64_t t) { return t ? k.tend[t - 1] : 0; }
 
@@ -375,6 +388,21 @@ __global__ void __launch_bounds__(kT) k_relmax(K k, const uint32_t *perm, unsign
   }
 }
 
+// a pass's callee maxima: for the items it recomputes, the maxima of the last
+// pass that computed them move to `prev` (a cut step begin reads them) and
+// the current ones restart from zero (a start can move down when a queue's
+// order changes, so maxima are never carried over); the other items keep
+// both (their finishes are not recomputed: the maxima they built stay valid)
+__global__ void __launch_bounds__(kT) k_acc_init(K k, uint64_t *prev, uint64_t *cur) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    if (!live(k, (uint32_t)i)) continue;
+    for (uint32_t s = 0; s < k.aw; ++s) {
+      if (prev) prev[i * k.aw + s] = cur[i * k.aw + s];
+      cur[i * k.aw + s] = 0ull;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kT) k_roots(K k, const uint32_t *inv) {
   for (uint64_t t = gid(); t < k.n; t += nthreads()) k.troot[t] = inv[item_off(k, t)];
 }
@@ -441,6 +469,7 @@ __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const unsigned long long op = ops[j];
     const uint64_t i = op >> 16;
+    if (!live(k, (uint32_t)i)) continue;
     const uint32_t s = (uint32_t)(op & 0xFFFFu);
     const DesItemPos p = k.ip[k.ipos[i]];
     const uint32_t b = p.bk_first + s;
@@ -459,7 +488,7 @@ __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops
       else c = k.acc_prev[i * k.aw + (s - 1)];
       v = c > v ? c : v;
     }
-    store_tracked(k, k.bk + i * k.bw + s, v + st.add);
+    store_tracked(k, k.bk + i * k.bw + s, v + st.add, (uint32_t)i);
   }
 }
 
@@ -481,8 +510,8 @@ struct MPThen {
 // that differs from the previous pass's (none: the round's queues are as
 // they were and the pass skips them).  The range words alternate between two
 // slots by launch; this launch empties the other slot for the next one.
-__global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t m, uint32_t *repb,
-                                             unsigned long long *mm, unsigned long long *mm_next, uint32_t *bad) {
+__global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t m, unsigned long long *mm,
+                                             unsigned long long *mm_next, uint32_t *bad) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // vector atomics: no scalar-cache stores
     atomicExch(mm_next, ~0ull);
     atomicExch(mm_next + 1, 0ull);
@@ -492,6 +521,7 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
   unsigned long long lo = ~0ull, hi = 0;
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
+    if (!live(k, i)) continue;  // its arrival is the previous pass's (the host keeps the round's range)
     const uint32_t v = k.ipos[i];
     const DesPos P = k.pos[v];
     const uint32_t par = k.ipar[i];
@@ -510,12 +540,6 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
         atomicOr(mm + 2, 1ull);
     }
     k.IA[i] = a;
-    uint32_t rep = 0;
-    if (P.reps > 1) {
-      const uint32_t hop = k.ihop[i];
-      rep = draw0(k.trace_begin + t, hop, 0x80000002u, k.k0, k.k1) % P.reps;
-    }
-    repb[j] = rep;
     lo = a < lo ? a : lo;
     hi = a > hi ? a : hi;
   }
@@ -544,16 +568,26 @@ __global__ void __launch_bounds__(kT) k_qarr(K k, const uint32_t *ids, uint64_t 
   }
 }
 
+// each item's replica (the oracle's draw at its hop), once per batch
+__global__ void __launch_bounds__(kT) k_reps(K k) {
+  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
+    const DesPos P = k.pos[k.ipos[i]];
+    uint32_t rep = 0;
+    if (P.reps > 1) rep = draw0(k.trace_begin + k.itr[i], k.ihop[i], 0x80000002u, k.k0, k.k1) % P.reps;
+    k.irep[i] = (uint16_t)rep;
+  }
+}
+
 // ONE sort key when the bits fit: row | replica | arrival - amin (equal keys
 // are put in (trace, hop) order afterwards: k_tiefix)
 // (the value is the list index j: a cyclic schedule keeps each round's sorted
 // order for the next pass, k_ordchk)
-__global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
-                                              uint64_t amin, uint32_t rb, uint32_t ab, uint64_t *key, uint32_t *val) {
+__global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, uint64_t amin, uint32_t rb,
+                                              uint32_t ab, uint64_t *key, uint32_t *val) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
     const uint64_t row = k.pos[k.ipos[i]].row;
-    key[j] = (((row << rb) | repb[j]) << ab) | (k.IA[i] - amin);
+    key[j] = (((row << rb) | k.irep[i]) << ab) | (k.IA[i] - amin);
     val[j] = (uint32_t)j;
   }
 }
@@ -563,10 +597,9 @@ __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t
 // increases along it, it IS the stable sort of the round's queue keys, and
 // the sort is skipped (k_pairs1o); any inversion raises *bad (cleared by
 // k_qarr) and the host sorts (des_items_launch)
-__device__ __forceinline__ void qtuple(const K &k, const uint32_t *ids, const uint32_t *repb, uint32_t j,
-                                       uint64_t &hi, uint64_t &a) {
+__device__ __forceinline__ void qtuple(const K &k, const uint32_t *ids, uint32_t j, uint64_t &hi, uint64_t &a) {
   const uint32_t i = ids[j];
-  hi = ((uint64_t)k.pos[k.ipos[i]].row << 32) | repb[j];
+  hi = ((uint64_t)k.pos[k.ipos[i]].row << 32) | k.irep[i];
   a = k.IA[i];
 }
 // the oracle's tie order of equal (row, replica, arrival): (trace, hop) —
@@ -601,15 +634,15 @@ __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_
     }
   }
 }
-__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *repb, const uint32_t *ord,
+__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *ord,
                                                uint64_t m, uint32_t *bad) {
   for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
     bool inv = false;
     if (jj > 0) {
       const uint32_t j = ord[jj], jp = ord[jj - 1];
       uint64_t h, a, hp, ap;
-      qtuple(k, ids, repb, j, h, a);
-      qtuple(k, ids, repb, jp, hp, ap);
+      qtuple(k, ids, j, h, a);
+      qtuple(k, ids, jp, hp, ap);
       inv = hp > h || (hp == h && (ap > a || (ap == a && tie_key(k, ids[jp]) > tie_key(k, ids[j]))));
     }
     const unsigned long long bm = __ballot(inv);
@@ -621,14 +654,14 @@ __global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const u
 
 // k_pairs1's outputs along a kept order
 __global__ void __launch_bounds__(kT) k_pairs1o(K k, uint64_t m, const uint32_t *ord, const uint32_t *ids,
-                                                const uint32_t *repb, uint32_t rb, uint32_t *segk, uint32_t *rowk,
+                                                uint32_t rb, uint32_t *segk, uint32_t *rowk,
                                                 MP *mp, uint32_t *sid) {
   for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
     const uint32_t j = ord[jj];
     const uint32_t i = ids[j];
     const uint32_t row = k.pos[k.ipos[i]].row;
     const uint64_t hold = k.row_hold[row];
-    segk[jj] = (row << rb) | repb[j];
+    segk[jj] = (row << rb) | k.irep[i];
     rowk[jj] = row;
     mp[jj] = MP{hold, k.IA[i] + hold};
     sid[jj] = i;
@@ -673,14 +706,14 @@ __global__ void __launch_bounds__(kT) k_pairs0(K k, const uint32_t *ids, uint64_
 }
 
 // TWO stable sorts otherwise: replica | arrival - amin first, then the row
-__global__ void __launch_bounds__(kT) k_qkey2(K k, const uint32_t *ids, uint64_t m, const uint32_t *repb,
-                                              uint64_t amin, uint32_t rb, uint64_t *key, uint32_t *val,
+__global__ void __launch_bounds__(kT) k_qkey2(K k, const uint32_t *ids, uint64_t m, uint64_t amin, uint32_t rb,
+                                              uint64_t *key, uint32_t *val,
                                               uint32_t *ovf) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const uint32_t i = ids[j];
     const uint64_t a = k.IA[i] - amin;
     if (rb && (a >> (64 - rb))) atomicOr(ovf, 1u);
-    key[j] = rb ? ((uint64_t)repb[j] << (64 - rb)) | a : a;
+    key[j] = rb ? ((uint64_t)k.irep[i] << (64 - rb)) | a : a;
     val[j] = i;
   }
 }
@@ -753,7 +786,7 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
       const uint64_t hold = k.row_hold[r];
       const uint64_t S = inc[j].C - hold;
       const uint64_t a = in[j].C - hold;
-      store_tracked(k, k.IS + i, S);
+      store_tracked(k, k.IS + i, S, i);
       if (r != row) {
         if (!k.quiet) flush();
         row = r;
@@ -842,6 +875,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
     };
     for (uint64_t j = j0 + lane; j < j0 + 64 * span && j < m; j += 64) {
       const uint32_t i = ids[j];
+      if (k.quiet && !live(k, i)) continue;
       const uint32_t v = k.ipos[i];
       if (v != v_run) {
         flush();
@@ -860,7 +894,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
         const uint64_t c = k.acc[(uint64_t)i * k.aw + last];
         F = (c > F ? c : F) + P.post;
       }
-      store_tracked(k, k.IF + i, F);
+      store_tracked(k, k.IF + i, F, i);
       const uint32_t par = k.ipar[i];
       if (par != kNone && !k.no_acc)
         atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
@@ -993,6 +1027,7 @@ size_t scan_u64_bytes(uint64_t n) {
 }
 constexpr uint32_t kPrewalkBlocks = 2048;  // pre-walk grid (waves refill from a global batch counter)
 constexpr uint32_t kMaxPasses = 256;       // fixed-point passes of a cyclic schedule (des.hip)
+constexpr uint32_t kChunkShift = 8;        // incremental quiet passes: chunks of 256 traces
 
 }  // namespace
 
@@ -1167,7 +1202,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
       M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
       (uint64_t)(pl.pos.size() + 1) * 4, (uint64_t)pl.pos.size() * 4, (uint64_t)pl.pos.size() * 4,  // poff qdst fdst
-      tmp_bytes};
+      tmp_bytes,
+      M * 2, (n >> kChunkShift) + 1, (n >> kChunkShift) + 1};  // replicas; the two chunk-change maps
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
   if (!pool_alloc(item_mem, total)) return fail("item allocation");
@@ -1221,6 +1257,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *d_qdst = (uint32_t *)carve(parts[45]);
   uint32_t *d_fdst = (uint32_t *)carve(parts[46]);
   void *tmp = carve(parts[47]);
+  k.irep = (uint16_t *)carve(parts[48]);
+  uint8_t *chg_a = (uint8_t *)carve(parts[49]), *chg_b = (uint8_t *)carve(parts[50]);
+  const uint64_t n_chunks = (n >> kChunkShift) + 1;
+  k.cshift = kChunkShift;
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -1249,6 +1289,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     hipLaunchKernelGGL(k_perm_inv, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
     hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
     hipLaunchKernelGGL(k_roots, dim3(grid_for(n)), dim3(kT), 0, s, k, inv);
+    hipLaunchKernelGGL(k_reps, dim3(grid_for(M)), dim3(kT), 0, s, k);
     if (pl.cyclic) {  // the first pass's cut step begins: contention-free callee maxima (k_relmax)
       if (hipMemsetAsync(k.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
         rc = fail("memset");
@@ -1329,26 +1370,23 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
     // every time: the iteration only raises values) until no stored value
     // changes, then the pass that records the statistics (des.hip des_launch)
-    // callee maxima: zeroed per pass (a start can move down when the order of
-    // a queue changes, so maxima are never carried over); a cut step begin
-    // reads the previous pass's (the two buffers swap)
-    uint64_t *acc_a = k.acc;
+    // callee maxima: restarted from zero for every item a pass recomputes (a
+    // start can move down when the order of a queue changes, so maxima are
+    // never carried over); a cut step begin reads the last computed ones
+    // (k_acc_init moves them to acc_prev).  After the first pass a quiet pass
+    // recomputes only the items of the trace chunks the previous pass
+    // changed (k.dcur; ISIM_DES_ITEMS_NO_INCR: every item)
     uint32_t qn = 0;       // k_qarr launches: the arrival-range slot alternates
     uint64_t skipped = 0;  // queue rounds a quiet pass skipped (ISIM_DES_DEBUG)
     uint64_t reused = 0;   // queue sorts a kept order replaced (ISIM_DES_DEBUG)
     // A/B switch: never reuse a kept order
     const bool keep_ord = pl.cyclic && std::getenv("ISIM_DES_ITEMS_NO_ORDER_REUSE") == nullptr;
     std::vector<uint8_t> have_ord(R, 0);
+    std::vector<uint64_t> rlo(R, ~0ull), rhi(R, 0);  // per sort round: its arrival range over the passes
+    // A/B switch: every quiet pass recomputes every item
+    const bool no_incr = std::getenv("ISIM_DES_ITEMS_NO_INCR") != nullptr;
     auto pass = [&](K &kk) {
-    if (pl.cyclic) {
-      std::swap(acc_a, acc_b);
-      kk.acc = acc_a;
-      kk.acc_prev = acc_b;
-    }
-    if (hipMemsetAsync(kk.acc, 0, M * 8 * k.aw, s) != hipSuccess) {
-      rc = fail("memset");
-      return;
-    }
+    hipLaunchKernelGGL(k_acc_init, dim3(grid_for(M)), dim3(kT), 0, s, kk, pl.cyclic ? acc_b : nullptr, kk.acc);
     // items per lane of k_qout / k_fin: runs of one row / position summed
     // before the statistics atomics; a quiet pass records none, and one item
     // per lane gives its finish groups (~0.8 M items on c4d) 16x the waves
@@ -1361,13 +1399,13 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       if (m) {
         uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
         ++qn;
-        hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b,
+        hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m,
                            (unsigned long long *)slot, (unsigned long long *)slot_next, ordbad);
         const bool nosort = pl.round_nosort[r] && !two_sorts;
         const bool chk = !nosort && have_ord[r];
         if (chk)
           hipLaunchKernelGGL(k_ordchk, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
-                             (const uint32_t *)rv_b, (const uint32_t *)(ord + qoff[r]), m, ordbad);
+                             (const uint32_t *)(ord + qoff[r]), m, ordbad);
         // a quiet pass after the first: a round whose arrivals all equal the
         // previous pass's keeps its starts (its queues are skipped)
         // (sort rounds only: they read the range back anyway; a sort-free
@@ -1385,19 +1423,26 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           ++skipped;
           goto finishes;
         }
+        if (!nosort) {
+          // the round's arrival range over the passes: the items a pass does
+          // not recompute keep their arrivals (a superset range is a valid key)
+          rlo[r] = std::min<uint64_t>(rlo[r], hmm[0]);
+          rhi[r] = std::max<uint64_t>(rhi[r], hmm[1]);
+          hmm[0] = rlo[r];
+          hmm[1] = rhi[r];
+        }
         const uint32_t ab = bits_for(hmm[1] - hmm[0]);
         tb = tmp_bytes;
         if (chk && !bad) {  // the kept order holds: no sort
           ++reused;
           hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
-                             (const uint32_t *)(qids + qoff[r]), (const uint32_t *)rv_b, rep_bits, rk_a, rk_b, mp_in,
-                             sid);
+                             (const uint32_t *)(qids + qoff[r]), rep_bits, rk_a, rk_b, mp_in, sid);
         } else if (nosort) {
           hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b, mp_in,
                              sid);
         } else if (!two_sorts && row_bits + rep_bits + ab <= 64) {
-          hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
-                             ab, key_a, val_a);
+          hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, hmm[0], rep_bits, ab,
+                             key_a, val_a);
           if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, row_bits + rep_bits + ab,
                                         s) != hipSuccess) {
             rc = fail("queue sort");
@@ -1415,7 +1460,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b,
                              (const uint32_t *)(qids + qoff[r]), rep_bits, ab, hmm[0], rk_a, rk_b, mp_in, sid);
         } else {
-          hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rv_b, hmm[0], rep_bits,
+          hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, hmm[0], rep_bits,
                              key_a, val_a, ovf);
           if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, 64, s) != hipSuccess) {
             rc = fail("arrival sort");
@@ -1452,8 +1497,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     };
     if (pl.cyclic) {
       if (hipMemsetAsync(k.IS, 0, M * 8, s) != hipSuccess || hipMemsetAsync(k.IF, 0, M * 8, s) != hipSuccess ||
-          (k.bw && hipMemsetAsync(k.bk, 0, M * 8 * k.bw, s) != hipSuccess) ||
-          hipMemsetAsync(acc_b, 0, M * 8 * k.aw, s) != hipSuccess) {
+          (k.bw && hipMemsetAsync(k.bk, 0, M * 8 * k.bw, s) != hipSuccess)) {
         rc = fail("memset");
         break;
       }
@@ -1464,13 +1508,18 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       uint32_t p = 0;
       for (; p < kMaxPasses && !rc; ++p) {
         uint32_t changed[2] = {1, 0};
-        if (hipMemsetAsync(kq.changed, 0, 8, s) != hipSuccess) {
+        if (hipMemsetAsync(kq.changed, 0, 8, s) != hipSuccess || hipMemsetAsync(chg_b, 0, n_chunks, s) != hipSuccess) {
           rc = fail("memset");
           break;
         }
         kq.first = p == 0 ? 1u : 0u;
+        // the first pass recomputes everything; later ones the chunks the
+        // previous pass changed
+        kq.dcur = p == 0 || no_incr ? nullptr : chg_a;
+        kq.dnext = chg_b;
         pass(kq);
         if (rc) break;
+        std::swap(chg_a, chg_b);
         if (hipMemcpyAsync(changed, kq.changed, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
           rc = fail("fixed-point read-back");
@@ -1491,7 +1540,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       if (rc) break;
     }
     k.acc_prev = acc_b;
-    pass(k);
+    pass(k);  // dcur null: every item
     if (rc) break;
     // 5. records and statistics
     hipLaunchKernelGGL(k_final, dim3(grid_for(n, 1024)), dim3(kT), 0, s, k);

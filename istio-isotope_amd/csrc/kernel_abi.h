@@ -118,13 +118,14 @@ struct TreeStep {
 };
 static_assert(sizeof(TreeStep) == 8, "TreeStep must be 8 bytes");
 // Placement of a non-leaf callee's duration row (TreeExt.row bits 16-31).  In
-// LDS (a sum index in bits 0-15): its code-200 duration sum (u32; a wrap
-// carries 2^32 to the row in HBM), and when its bucket varies
-// (prom_bucket(tmin) < prom_bucket(tmax)) a bucket table of the workgroup: a
-// header word (b_lo | width << 8), then the code-200 counts as u16 pairs
-// (ceil(width / 2) words; a field reaching 2^15 moves 2^15 to HBM); code-500
-// buckets and sums (errorRate-rare) by global atomics; flushed once per
-// workgroup.  In global memory (the duration-table
+// LDS (a sum index in bits 0-15): its code-200 duration sum, and when its
+// bucket varies (prom_bucket(tmin) < prom_bucket(tmax)) a bucket table of the
+// workgroup: a header word (b_lo | width << 8), then the counts.  Wide rows:
+// a u64 sum, [code 200|500][width] u32 counts.  Compact rows (TreeLayout
+// compact, when the wide ones do not all fit): a u32 sum (a wrap carries 2^32
+// to the row in HBM), the code-200 counts as u16 pairs (ceil(width / 2)
+// words; a field reaching 2^15 moves 2^15 to HBM), code-500 buckets and sums
+// (errorRate-rare) by global atomics.  Flushed once per workgroup.  In global memory (the duration-table
 // row in bits 0-15; rows the LDS budget does not hold, coldest first): sums,
 // and buckets when they vary, by global atomics per response.  A static
 // bucket follows from the slot counters at the flush.
@@ -151,13 +152,15 @@ constexpr uint32_t kTreeLdsFull = 160u * 1024u;
 // Layout chosen by the host (program.cpp place_tree): LDS byte offsets.
 struct TreeLayout {
   uint32_t off_cnt;     // [2][n_slots] u32: executed calls, callee 500s
-  uint32_t off_sums;    // [n_sum] u32: code-200 duration sums of the LDS rows (carries to HBM)
+  uint32_t off_sums;    // [n_sum] code-200 duration sums of the LDS rows: u64, or u32 when compact (carries to HBM)
   uint32_t off_dyn;     // dyn_words u32: the bucket tables
   uint32_t off_nodes;   // [n_pos] TreeNode (nodes_lds)
   uint32_t bytes;       // total
   uint32_t nodes_lds;   // 1: the nodes in LDS; 0: read from global memory
   uint32_t wg_per_cu;   // 2: the layout fits kTreeLdsHalf
   uint32_t n_sum;       // LDS sum rows
+  uint32_t compact;     // 1: compact rows (u32 sums, code-200 u16 bucket pairs, 500s in HBM): chosen when the
+                        // wide rows (u64 sums, [code][width] u32 buckets) do not all fit
   uint32_t cnt16;       // 1: one u32 per slot, calls | 500s << 16, each kept below 2^15 (a field reaching
                         // 2^15 moves 2^15 to the stats at once); 0: [2][n_slots] u32
 };

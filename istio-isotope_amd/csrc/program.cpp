@@ -79,10 +79,14 @@ ScriptTimes script_times(const Service &sv) {
 // per CU), nodes in LDS within the whole CU, nodes in global memory within
 // half, then within the whole CU; the first whose fixed part fits and which
 // holds every row wins, else the first whose fixed part fits.
-// LDS bytes of a calling row: a 32-bit code-200 duration sum (its carries go
-// to the row in HBM), and when the bucket varies a header word and the
-// code-200 bucket counts as guarded u16 pairs (500s are errorRate-rare: HBM)
-static uint32_t row_lds_bytes(uint32_t bw) { return 4u + (bw ? 4u + 4u * ((bw + 1u) / 2u) : 0u); }
+// LDS bytes of a calling row (kernel_abi.h TreeLayout): wide — a u64
+// code-200 sum, and when the bucket varies a header word and [2][width] u32
+// counts; compact — a u32 sum (carries to HBM), a header word and the code-200
+// counts as guarded u16 pairs (500s are errorRate-rare: HBM)
+static uint32_t row_lds_bytes(uint32_t bw, bool compact) {
+  if (compact) return 4u + (bw ? 4u + 4u * ((bw + 1u) / 2u) : 0u);
+  return 8u + (bw ? 4u + 8u * bw : 0u);
+}
 
 static bool place_tree(Program &out, const std::vector<double> &row_heat, const std::vector<uint32_t> &row_bw,
                        const std::vector<char> &row_nonleaf) {
@@ -102,6 +106,9 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   };
   const Cand cands[4] = {{true, kTreeLdsHalf}, {true, kTreeLdsFull}, {false, kTreeLdsHalf}, {false, kTreeLdsFull}};
   int pick = -1;
+  // wide rows unless they do not all fit in any candidate and compact ones
+  // hold more (ISIM_TREE_COMPACT / ISIM_TREE_WIDE force one: A/B measurements)
+  bool compact = false;
   // ISIM_TREE_NODES_GLOBAL set: only the layouts with the nodes in global memory (A/B measurements)
   // ISIM_TREE_NODES_LDS set: only the layouts with the nodes in LDS (A/B measurements)
   const int first = std::getenv("ISIM_TREE_NODES_GLOBAL") ? 2 : 0;
@@ -110,14 +117,18 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   // SIMD (tree.hip): one 1024-thread workgroup per CU whatever the layout, so
   // the half-CU layouts would only leave LDS unused
   const bool one_wg = out.tree_frames > 8;
-  for (int pass = 0; pass < 2 && pick < 0; ++pass) {
+  const bool force_c = std::getenv("ISIM_TREE_COMPACT") != nullptr, force_w = std::getenv("ISIM_TREE_WIDE") != nullptr;
+  // passes: every row fits (wide, then compact), else the fixed part fits (compact: more rows)
+  for (int pass = 0; pass < 3 && pick < 0; ++pass) {
+    compact = force_c || (!force_w && pass >= 1);
+    if (force_c && pass == 1) continue;
     for (int i = first; i < last && pick < 0; ++i) {
       if (one_wg && cands[i].limit == kTreeLdsHalf) continue;
       uint32_t fixed = ((head + cb * S + 7u) & ~7u) + (cands[i].nodes ? 8u * P + 8u : 0u);
       if (fixed > cands[i].limit) continue;
       uint32_t all = fixed;
-      for (uint32_t r : order) all += row_lds_bytes(row_bw[r]);
-      if (pass == 1 || all <= cands[i].limit) pick = i;
+      for (uint32_t r : order) all += row_lds_bytes(row_bw[r], compact);
+      if (pass == 2 || all <= cands[i].limit) pick = i;
     }
   }
   if (pick < 0) return false;
@@ -128,6 +139,7 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   L.wg_per_cu = c.limit == kTreeLdsHalf ? 2u : 1u;
   L.off_cnt = head;
   L.cnt16 = cb == 4u ? 1u : 0u;
+  L.compact = compact ? 1u : 0u;
   L.off_sums = (head + cb * S + 7u) & ~7u;
   uint32_t room = c.limit - L.off_sums - (c.nodes ? 8u * P + 8u : 0u);
   // rows into LDS while they fit: a sum word, and the bucket table when the bucket varies
@@ -137,7 +149,7 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   out.tree_dyn_words = 0;
   std::vector<uint32_t> lds_rows;
   for (uint32_t r : order) {
-    const uint32_t need = row_lds_bytes(row_bw[r]);
+    const uint32_t need = row_lds_bytes(row_bw[r], compact);
     if (need <= room && out.sum_row.size() < 0xFFFFu && out.tree_dyn_words + 4096u < 0xFFF0u) {
       room -= need;
       lds_rows.push_back(r);
@@ -153,7 +165,7 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
     if (row_bw[r]) {
       out.tree_row_place[r] = out.tree_dyn_words;
       out.tree_dyn.push_back(TreeDynRow{r, out.tree_dyn_words, out.tree_row_blo[r], row_bw[r]});
-      out.tree_dyn_words += 1u + (row_bw[r] + 1u) / 2u;
+      out.tree_dyn_words += 1u + (compact ? (row_bw[r] + 1u) / 2u : 2u * row_bw[r]);
     } else {
       out.tree_row_place[r] = kTreeStaticRow;
     }
@@ -162,7 +174,7 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
     if (out.tree_row_place[r] == kTreeGlobalDyn || out.tree_row_place[r] == kTreeGlobalStatic)
       out.tree_row_index[r] = r;
   L.n_sum = (uint32_t)out.sum_row.size();
-  L.off_dyn = L.off_sums + 4u * L.n_sum;
+  L.off_dyn = L.off_sums + (compact ? 4u : 8u) * L.n_sum;
   L.off_nodes = (L.off_dyn + 4u * out.tree_dyn_words + 7u) & ~7u;
   L.bytes = L.off_nodes + (c.nodes ? 8u * P : 0u);
   return L.bytes <= c.limit;

@@ -97,8 +97,9 @@ struct GlobalNodes {
 struct TreeSink {
   uint32_t *cnt;                // LDS: per slot calls | 500s << 16 (cnt16), else [2][n_slots] u32
   const uint8_t *lut;           // LDS duration-bucket table
-  uint32_t *sum200;             // LDS [n_sum]: code-200 duration sums, low 32 bits (carries go to HBM)
-  uint32_t *dyn;                // LDS bucket tables of the varying rows (code 200, guarded u16 pairs)
+  void *sum200;                 // LDS [n_sum]: code-200 duration sums (u64; compact: u32, carries go to HBM)
+  uint32_t *dyn;                // LDS bucket tables of the varying rows ([2][w] u32; compact: code 200, u16 pairs)
+  bool compact;                 // kernel_abi.h TreeLayout.compact
   uint64_t *svc_tab;            // HBM duration table, or null (ISIM_FLAG_NO_SVC_DUR)
   const uint32_t *sum_row;      // per LDS sum index: its row (code-500 sums go to HBM)
   uint32_t n_slots;
@@ -177,8 +178,23 @@ struct TreeSink {
       atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
       return;
     }
-    // an LDS row (round 5: 4-byte sums and u16 code-200 buckets, so about
-    // twice the rows fit; 500s — errorRate-rare — go to HBM by atomics)
+    if (!compact) {  // a wide LDS row
+      if (place != kTreeStaticRow) {  // the row's LDS bucket table: header b_lo | width << 8
+        const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
+        uint32_t b = lut_bucket(lut, T) - lo;
+        b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
+        lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
+      }
+      if (st) {
+        unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS);
+        atomicAdd(r + 2 * ISIM_N_PROM + 1, (unsigned long long)T);
+      } else {
+        lds_add((unsigned long long *)sum200 + idx, (unsigned long long)T);
+      }
+      return;
+    }
+    // a compact LDS row (round 5: 4-byte sums and u16 code-200 buckets, so
+    // about twice the rows fit; 500s — errorRate-rare — go to HBM by atomics)
     if (st) {
       unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)dur_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS);
       if (place != kTreeStaticRow) atomicAdd(r + ISIM_N_PROM + lut_bucket(lut, T), 1ull);
@@ -201,7 +217,7 @@ struct TreeSink {
       return;
     }
     const uint32_t t32 = (uint32_t)T;
-    const uint32_t o = lds_add_rtn(sum200 + idx, t32);
+    const uint32_t o = lds_add_rtn((uint32_t *)sum200 + idx, t32);
     if (o + t32 < o) sum_carry(sum_row[idx]);
   }
   // a u16 bucket field reached 2^15: 2^15 of its counts go to the row in HBM
@@ -236,7 +252,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   c.hist = reinterpret_cast<uint32_t *>(lds + kLdsAccBytes);
   c.cnt = reinterpret_cast<uint32_t *>(lds + lay.off_cnt);
   c.n_slots = S;
-  uint32_t *sum200 = reinterpret_cast<uint32_t *>(lds + lay.off_sums);
+  void *sum200 = lds + lay.off_sums;
   uint32_t *dyn = reinterpret_cast<uint32_t *>(lds + lay.off_dyn);
   const uint8_t *lut = lds + kLdsAccBytes + kHistWords * 4u;
   // zero the accumulators (everything before the nodes), copy the nodes in
@@ -258,7 +274,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     dyn[d.off] = d.b_lo | (d.width << 8);
   }
   __syncthreads();
-  TreeSink sink{c.cnt, lut, sum200, dyn, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
+  TreeSink sink{c.cnt, lut, sum200, dyn, lay.compact != 0, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
                 reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
 #ifdef ISIM_TREE_DEBUG
   sink.n_pos = P;
@@ -442,11 +458,12 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
         if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
       }
     }
-    for (uint32_t r = threadIdx.x; r < lay.n_sum; r += blockDim.x)
-      if (sum200[r])
-        atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM,
-                  (unsigned long long)sum200[r]);
-    // the varying LDS rows' code-200 bucket tables (u16 pairs): one thread per (row, word)
+    for (uint32_t r = threadIdx.x; r < lay.n_sum; r += blockDim.x) {
+      const unsigned long long v =
+          lay.compact ? (unsigned long long)((uint32_t *)sum200)[r] : ((unsigned long long *)sum200)[r];
+      if (v) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
+    }
+    // the varying LDS rows' bucket tables: one thread per (row, word)
     for (uint32_t i = threadIdx.x; i < kp.dyn_words; i += blockDim.x) {
       const uint32_t v = dyn[i];
       if (!v) continue;
@@ -459,10 +476,15 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       }
       const TreeDynRow d = kp.tree_dyn[lo];
       if (i == d.off) continue;  // the header
-      const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
       unsigned long long *row = tab + (uint64_t)dur_row(d.row) * ISIM_SVC_DUR_WORDS;
-      if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));
-      if (v >> 16) atomicAdd(row + b + 1u, (unsigned long long)(v >> 16));
+      if (lay.compact) {  // code-200 u16 pairs
+        const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
+        if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));
+        if (v >> 16) atomicAdd(row + b + 1u, (unsigned long long)(v >> 16));
+      } else {  // [code][width] u32
+        const uint32_t j = i - d.off - 1, code = j >= d.width ? 1u : 0u, b = d.b_lo + j - code * d.width;
+        atomicAdd(row + code * ISIM_N_PROM + b, (unsigned long long)v);
+      }
     }
     // the entry's row: its invocations are the traces (end-to-end histogram and sums)
     unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;
