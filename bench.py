@@ -315,13 +315,17 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
     rows = d.info.row_reads + d.info.row_writes
     items = d.info.items == 1
     hops = folded["sum_hops"] / total
+    batch = d.last_batch() if items else None
     if items:
         # the item engine: per executed invocation the
-        # pre-walk writes 13 B, the two bucket sorts move 2 x 16 B, the queue
-        # pass ~96 B (keys, two stable sorts, the scan's maps in and out, the
-        # start), the finish ~48 B (start, arrival, callee maximum, finish);
-        # per trace the gaps, arrivals, offsets, hops ~44 B and the record
-        alg_bytes = int(B * (hops * (13 + 32 + 96 + 48) + 44 + (0 if args.no_records else 16)))
+        # pre-walk writes 13 B, the renumbering moves 2 x 16 B, and every pass
+        # over the rounds (a cyclic schedule's quiet passes and the recording
+        # one: isim_des_last_batch) moves the queue's ~96 B (keys, the sort,
+        # the scan's maps in and out, the start) and the finish's ~48 B
+        # (start, arrival, callee maximum, finish); per trace the gaps,
+        # arrivals, offsets, hops ~44 B and the record
+        alg_bytes = int(B * (hops * (13 + 32 + (96 + 48) * batch["passes"]) + 44 +
+                             (0 if args.no_records else 16)))
     else:
         alg_bytes = B * (R * rows + npos // 4 + 44 + (0 if args.no_records else 16))
     achieved_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9
@@ -353,14 +357,16 @@ def main_des(args, h, json_text, desc, params, rank, world, dev, multi=None, mer
                        des_engine="items (dynamic walk)" if items else "level-synchronous rows",
                        des_rows="u64" if wide[0] or items else "u32", des_cyclic=bool(d.info.cyclic),
                        workspace_bytes=wsb, rccl_ranks=multi.n_ranks if multi is not None else None,
-                       traces_per_rank=args.steps * B),
+                       traces_per_rank=args.steps * B,
+                       des_passes_per_step=batch["passes"] if batch else 1,
+                       des_syncs_per_step=batch["syncs"] if batch else None),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ("des_items k_* + rocPRIM sorts/scans per step" if items else
                                 "des_* (arrivals, down and up passes of all levels, finalize) per step"),
                      "kernel_ms": kern_ms, "bytes_per_launch": alg_bytes,
-                     "basis": ("per executed invocation ~189 B of item arrays and sort traffic per pass "
-                               "(DESIGN.md §10.9)" if items else
+                     "basis": ("per executed invocation 45 B once and ~144 B of item arrays and sort traffic "
+                               "per pass over the rounds (DESIGN.md §10.9)" if items else
                                "workspace: the level-synchronous rows the algorithm streams (DESIGN.md §10.4)")},
         # the same time against the bytes any implementation must
         # move — the 16-B record per trace and the statistics written once

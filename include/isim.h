@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define ISIM_ABI_VERSION 9
+#define ISIM_ABI_VERSION 10
 
 #if defined(__GNUC__)
 #define ISIM_API __attribute__((visibility("default")))
@@ -332,10 +332,25 @@ typedef struct {
   int32_t row_writes;            /* rows it writes (the algorithmic bytes of bench.py's roofline) */
   int32_t items;                 /* 1: a dynamic walk (probabilistic calls, mode A) on the item engine (DESIGN.md
                                     §10.9): positions are the tree's POTENTIAL invocations, a batch simulates the
-                                    executed ones and synchronizes hip_stream twice (item count, bucket sizes) */
+                                    executed ones and synchronizes hip_stream at its item count and bucket sizes,
+                                    once per sort round whose arrival range it reads back, and (a cyclic schedule)
+                                    once per quiet pass — isim_des_last_batch reports the count */
 } isim_des_info;
 
 ISIM_API int isim_des_info_get(const isim_handler *h, isim_des_info *out);
+
+/* The item engine's (isim_des_info.items) last batch served through this
+ * handler, on any device, for reports: passes over the rounds (a cyclic
+ * schedule's quiet passes and the recording pass; 1 otherwise), host
+ * synchronisations of hip_stream (the item count, bucket sizes, each sort
+ * round's arrival range, each quiet pass's change flag), executed
+ * invocations.  Zero before the first item-engine batch. */
+typedef struct {
+  uint32_t passes;
+  uint32_t syncs;
+  uint64_t items;
+} isim_des_batch_stats;
+ISIM_API int isim_des_last_batch(const isim_handler *h, isim_des_batch_stats *out);
 /* Device workspace a batch of n_traces needs (either row width: 8 B per invocation per trace + ~40 B per trace). */
 ISIM_API int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes);
 /* One DES batch (trace ids [trace_begin, trace_begin+n_traces), arrivals from

@@ -129,6 +129,8 @@ struct isim_handler {
   int des_rc = ISIM_OK;
   std::string des_err;
   isim::DesPlan des;
+  std::mutex report_mu;
+  isim::DesItemsReport des_report{};  // the item engine's last batch (isim_des_last_batch)
   ~isim_handler() {
     for (auto &kv : dev) {
       int cur = 0;
@@ -905,6 +907,16 @@ int isim_des_info_get(const isim_handler *h, isim_des_info *out) {
   return ISIM_OK;
 }
 
+int isim_des_last_batch(const isim_handler *h, isim_des_batch_stats *out) {
+  if (!h || !out) return fail(ISIM_EINVAL, "null argument");
+  isim_handler *hm = const_cast<isim_handler *>(h);
+  std::lock_guard<std::mutex> lk(hm->report_mu);
+  out->passes = h->des_report.passes;
+  out->syncs = h->des_report.syncs;
+  out->items = h->des_report.items;
+  return ISIM_OK;
+}
+
 int isim_des_workspace_bytes(const isim_handler *h, uint64_t n_traces, uint64_t *bytes) {
   if (!h || !bytes) return fail(ISIM_EINVAL, "null argument");
   if (const int drc = des_ensure(h)) return drc;
@@ -956,8 +968,14 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.seed = h->params.seed;
     L.n_slots = (uint32_t)h->prog.n_slots;
     L.pool = st->des_pool;
+    isim::DesItemsReport rep{};
+    L.report = &rep;
     std::string e;
     const int irc = isim::des_items_launch(L, hip_stream, e);
+    {
+      std::lock_guard<std::mutex> lk(h->report_mu);
+      h->des_report = rep;
+    }
     if (irc == 2) return fail(ISIM_EINVAL, e);
     if (irc) return fail(ISIM_EHIP, e);
     return ISIM_OK;

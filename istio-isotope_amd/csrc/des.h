@@ -211,6 +211,11 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
 // per-trace workspace bytes; the per-item arrays are allocated on `stream`
 // from `pool` (the handler's private hipMemPool_t on this device) once the
 // batch's executed invocations are counted.
+struct DesItemsReport {
+  uint32_t passes;  // passes over the rounds (cyclic schedules: the quiet ones and the recording one)
+  uint32_t syncs;   // host synchronisations of the stream
+  uint64_t items;   // executed invocations
+};
 struct DesItemsLaunch {
   const DesPlan *plan;
   const void *d_pos, *d_item_pos, *d_steps;  // DesPos[n_pos], DesItemPos[n_pos], DesStep[]
@@ -224,6 +229,7 @@ struct DesItemsLaunch {
   uint64_t n_traces, trace_begin, mean_ns, seed;
   uint32_t n_slots;
   void *pool;  // hipMemPool_t
+  DesItemsReport *report;  // filled when the batch ends (null: none)
 };
 uint64_t des_items_workspace_bytes(uint64_t n);
 int des_items_launch(const DesItemsLaunch &L, void *stream, std::string &err);

@@ -435,7 +435,9 @@ __global__ void __launch_bounds__(kT) k_bucket_keys(K k, uint32_t *sk, unsigned 
     for (uint32_t s2 = 0; s2 < nst; ++s2) {
       const uint32_t o = base + incl - nst + s2;
       sk[o] = k.step_round[p.bk_first + s2] & ~kDesStepCut;
-      sv[o] = ((unsigned long long)i << 16) | s2;
+      // (item, step) and, in the top 16 bits, the item's trace chunk (k_steps'
+      // liveness test without a gather)
+      sv[o] = ((unsigned long long)(k.itr[i] >> k.cshift) << 48) | ((unsigned long long)i << 16) | s2;
     }
   }
 }
@@ -468,8 +470,8 @@ __global__ void __launch_bounds__(kT) k_scatter_ids(K k, const uint32_t *poff, c
 __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops, uint64_t m) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const unsigned long long op = ops[j];
-    const uint64_t i = op >> 16;
-    if (!live(k, (uint32_t)i)) continue;
+    if (k.dcur && !k.dcur[op >> 48]) continue;  // not recomputed in this pass
+    const uint64_t i = (op >> 16) & 0xFFFFFFFFull;
     const uint32_t s = (uint32_t)(op & 0xFFFFu);
     const DesItemPos p = k.ip[k.ipos[i]];
     const uint32_t b = p.bk_first + s;
@@ -634,11 +636,13 @@ __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_
     }
   }
 }
-__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *ord,
+__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *ord, const uint16_t *ordc,
                                                uint64_t m, uint32_t *bad) {
   for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
     bool inv = false;
-    if (jj > 0) {
+    // a pair of items neither of which this pass recomputes kept its keys:
+    // its order stands (ordc: their trace chunks, stored with the order)
+    if (jj > 0 && (!k.dcur || k.dcur[ordc[jj]] || k.dcur[ordc[jj - 1]])) {
       const uint32_t j = ord[jj], jp = ord[jj - 1];
       uint64_t h, a, hp, ap;
       qtuple(k, ids, j, h, a);
@@ -649,6 +653,17 @@ __global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const u
     if (bm && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)bm) - 1u &&
         __hip_atomic_load(bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
       atomicOr(bad, 1u);
+  }
+}
+
+// a sort round's order kept for the next pass: the list indices and the
+// items' trace chunks
+__global__ void __launch_bounds__(kT) k_keep_ord(K k, const uint32_t *js, const uint32_t *ids, uint64_t m,
+                                                 uint32_t *ord, uint16_t *ordc) {
+  for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
+    const uint32_t j = js[jj];
+    ord[jj] = j;
+    ordc[jj] = (uint16_t)(k.itr[ids[j]] >> k.cshift);
   }
 }
 
@@ -1027,7 +1042,9 @@ size_t scan_u64_bytes(uint64_t n) {
 }
 constexpr uint32_t kPrewalkBlocks = 2048;  // pre-walk grid (waves refill from a global batch counter)
 constexpr uint32_t kMaxPasses = 256;       // fixed-point passes of a cyclic schedule (des.hip)
-constexpr uint32_t kChunkShift = 8;        // incremental quiet passes: chunks of 256 traces
+// incremental quiet passes: chunks of 256 traces, or larger so that a chunk
+// id fits 16 bits (step ops and kept orders carry it)
+uint32_t chunk_shift(uint64_t n) { return std::max<uint32_t>(8u, bits_for(n) > 16u ? bits_for(n) - 16u : 0u); }
 
 }  // namespace
 
@@ -1088,6 +1105,19 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     err = std::string("DES items: ") + what;
     return 1;
   };
+  // the batch's report (isim_des_last_batch): host synchronisations, passes, items
+  DesItemsReport rep{};
+  auto sync_s = [&]() {
+    ++rep.syncs;
+    return hipStreamSynchronize(s);
+  };
+  struct ReportOut {
+    const DesItemsReport &r;
+    DesItemsReport *out;
+    ~ReportOut() {
+      if (out) *out = r;
+    }
+  } report_out{rep, L.report};
   // 1. arrivals
   hipLaunchKernelGGL(k_gaps, dim3(grid_for(n)), dim3(kT), 0, s, k);
   size_t b = scan_bytes;
@@ -1159,13 +1189,15 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     return fail("item offset scan");
   uint64_t M = 0;
   if (hipMemcpyAsync(&M, k.tend + (n - 1), 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
+      sync_s() != hipSuccess)
     return fail("item count read-back");
   if (M >= 0xFFFFFFFFull) {
     err = "DES items: a batch of more than 2^32 - 1 executed invocations (use smaller batches)";
     return 2;
   }
   k.M = M;
+  rep.items = M;
+  rep.passes = 1;
   // the per-item arrays and the rounds' sort buffers, one allocation
   const uint32_t R = pl.rounds();
   const uint32_t G = (uint32_t)pl.fin_off.size() - 1;
@@ -1203,7 +1235,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
       (uint64_t)(pl.pos.size() + 1) * 4, (uint64_t)pl.pos.size() * 4, (uint64_t)pl.pos.size() * 4,  // poff qdst fdst
       tmp_bytes,
-      M * 2, (n >> kChunkShift) + 1, (n >> kChunkShift) + 1};  // replicas; the two chunk-change maps
+      M * 2, (n >> chunk_shift(n)) + 1, (n >> chunk_shift(n)) + 1,  // replicas; the two chunk-change maps
+      pl.cyclic ? M * 2 : 2};                                   // kept orders' trace chunks
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
   if (!pool_alloc(item_mem, total)) return fail("item allocation");
@@ -1258,9 +1291,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *d_fdst = (uint32_t *)carve(parts[46]);
   void *tmp = carve(parts[47]);
   k.irep = (uint16_t *)carve(parts[48]);
+  k.cshift = chunk_shift(n);
+  const uint64_t n_chunks = (n >> k.cshift) + 1;
   uint8_t *chg_a = (uint8_t *)carve(parts[49]), *chg_b = (uint8_t *)carve(parts[50]);
-  const uint64_t n_chunks = (n >> kChunkShift) + 1;
-  k.cshift = kChunkShift;
+  uint16_t *ordc = (uint16_t *)carve(parts[51]);
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -1311,7 +1345,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     std::vector<uint32_t> poff(NP + 1);
     if (hipMemcpyAsync(&n_ops, ovf + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(poff.data(), d_poff, (NP + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
+        sync_s() != hipSuccess) {
       rc = fail("bucket read-back");
       break;
     }
@@ -1350,7 +1384,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       }
       hipLaunchKernelGGL(k_bounds, dim3(grid_for(n_ops + 1)), dim3(kT), 0, s, op_k2, (uint64_t)n_ops, R, 0u, d_soff);
       if (hipMemcpyAsync(soff.data(), d_soff, (R + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess) {
+          sync_s() != hipSuccess) {
         rc = fail("step-op offsets read-back");
         break;
       }
@@ -1405,7 +1439,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         const bool chk = !nosort && have_ord[r];
         if (chk)
           hipLaunchKernelGGL(k_ordchk, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
-                             (const uint32_t *)(ord + qoff[r]), m, ordbad);
+                             (const uint32_t *)(ord + qoff[r]), (const uint16_t *)(ordc + qoff[r]), m, ordbad);
         // a quiet pass after the first: a round whose arrivals all equal the
         // previous pass's keeps its starts (its queues are skipped)
         // (sort rounds only: they read the range back anyway; a sort-free
@@ -1415,7 +1449,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         uint32_t bad = 1;
         if ((!nosort || may_skip) && (hipMemcpyAsync(hmm, slot, 24, hipMemcpyDeviceToHost, s) != hipSuccess ||
                                       (chk && hipMemcpyAsync(&bad, ordbad, 4, hipMemcpyDeviceToHost, s) != hipSuccess) ||
-                                      hipStreamSynchronize(s) != hipSuccess)) {
+                                      sync_s() != hipSuccess)) {
           rc = fail("arrival range read-back");
           break;
         }
@@ -1451,10 +1485,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           hipLaunchKernelGGL(k_tiefix<true>, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint64_t *)key_b, val_b, m,
                              (const uint32_t *)(qids + qoff[r]));
           if (keep_ord) {  // the next pass checks this order first
-            if (hipMemcpyAsync(ord + qoff[r], val_b, m * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-              rc = fail("order copy");
-              break;
-            }
+            hipLaunchKernelGGL(k_keep_ord, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)val_b,
+                               (const uint32_t *)(qids + qoff[r]), m, ord + qoff[r], ordc + qoff[r]);
             have_ord[r] = 1;
           }
           hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b,
@@ -1521,10 +1553,11 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         if (rc) break;
         std::swap(chg_a, chg_b);
         if (hipMemcpyAsync(changed, kq.changed, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
+            sync_s() != hipSuccess) {
           rc = fail("fixed-point read-back");
           break;
         }
+        rep.passes = p + 2;  // the quiet passes so far and the recording pass
         if (debug) std::fprintf(stderr, "isim des items: pass %u changed %u values\n", p + 1, changed[1]);
         if (!changed[0]) break;
       }

@@ -35,6 +35,13 @@ class DesHandler:
         native.check(native.load().isim_des_info_get(handler._h, C.byref(info)))
         self.info = info
 
+    def last_batch(self) -> dict:
+        """isim_des_last_batch: the item engine's last batch on this handler
+        (passes over the rounds, host synchronisations, executed invocations)."""
+        st = native.DesBatchStats()
+        native.check(native.load().isim_des_last_batch(self.handler._h, C.byref(st)))
+        return {"passes": int(st.passes), "syncs": int(st.syncs), "items": int(st.items)}
+
     @property
     def table_words(self) -> int:
         return int(self.info.table_rows) * native.DES_ROW_WORDS

@@ -23,7 +23,7 @@ STATUS_NAMES = {0: "OK", 1: "EINVAL", 2: "ENOMEM", 3: "EHIP", 4: "EPARSE", 5: "E
                 6: "EDEPTH", 7: "ERANGE", 8: "ENOTFOUND", 9: "ENODEV",
                 10: "ECOMM"}
 MODE_A, MODE_B = 0, 1
-ABI_VERSION = 9  # include/isim.h ISIM_ABI_VERSION
+ABI_VERSION = 10  # include/isim.h ISIM_ABI_VERSION
 FLAG_NO_STREAM = 1
 FLAG_NO_SVC_DUR = 2
 FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk, then a fill)
@@ -95,6 +95,10 @@ class MultiId(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
 
+class DesBatchStats(C.Structure):
+    _fields_ = [("passes", C.c_uint32), ("syncs", C.c_uint32), ("items", C.c_uint64)]
+
+
 class DesInfo(C.Structure):
     _fields_ = [("n_positions", C.c_int32), ("n_levels", C.c_int32), ("max_width", C.c_int32),
                 ("table_rows", C.c_int32), ("n_fused", C.c_int32), ("cyclic", C.c_int32),
@@ -128,6 +132,7 @@ SIGNATURES = {
     "isim_stats_fold": (C.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "isim_stats_fold_durations": (C.c_int, [_VP, _VP, _VP]),
     "isim_des_info_get": (C.c_int, [_VP, C.POINTER(DesInfo)]),
+    "isim_des_last_batch": (C.c_int, [_VP, C.POINTER(DesBatchStats)]),
     "isim_des_workspace_bytes": (C.c_int, [_VP, C.c_uint64, C.POINTER(C.c_uint64)]),
     "isim_serve_des_device": (C.c_int, [_VP, C.POINTER(DesParams), C.c_uint64, C.c_uint64, _VP, _VP, _VP,
                                         _VP, C.c_uint64, _VP]),

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert native.load().isim_abi_version() == native.ABI_VERSION == 9
+    assert native.load().isim_abi_version() == native.ABI_VERSION == 10
 
 
 def _handler(doc, entry=None, **kw):
