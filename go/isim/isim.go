@@ -138,6 +138,23 @@ func (h *Handler) ServeUnderLoad(device int, begin uint64, meanGapNs uint64, rec
 	return stats, table, lastErr(rc)
 }
 
+// DesBatch is the item engine's report on the handler's last DES batch
+// (isim_des_last_batch): passes over the rounds, host synchronisations,
+// executed invocations.
+type DesBatch struct {
+	Passes, Syncs uint32
+	Items         uint64
+}
+
+// LastDesBatch reports the item engine's last batch (zero before the first).
+func (h *Handler) LastDesBatch() (DesBatch, error) {
+	var st C.isim_des_batch_stats
+	if rc := C.isim_des_last_batch(h.h, &st); rc != C.ISIM_OK {
+		return DesBatch{}, lastErr(rc)
+	}
+	return DesBatch{uint32(st.passes), uint32(st.syncs), uint64(st.items)}, nil
+}
+
 type Multi struct{ m *C.isim_multi }
 
 // u64ptr passes an empty slice as NULL (libisim then reports EINVAL) instead
