@@ -889,12 +889,13 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
     uint32_t mb[TPL];
 #pragma unroll
     for (int u = 0; u < TPL; ++u) mb[u] = 0;
-    for (uint32_t g = g0; g < g1; ++g) {
-      const Node4 nxt = load_group(stream + g + 1);  // zero tail padding
+    // one group: its Philox blocks, then per record the error bits shifted
+    // into mb and the record's count in lane r of lcnt
+    auto grp = [&](const Node4 &q, uint32_t g) {
       uint32_t x[TPL][4];
 #pragma unroll
       for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
-      if ((cur.n[0].thr | cur.n[1].thr | cur.n[2].thr | cur.n[3].thr) != 0) {
+      if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0) {
         if (hi_uniform) {
           philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
         } else {
@@ -905,7 +906,7 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
       auto records = [&](bool always) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const uint32_t thr = cur.n[j].thr, meta = cur.n[j].meta;
+          const uint32_t thr = q.n[j].thr, meta = q.n[j].meta;
           uint32_t n = 0;
 #pragma unroll
           for (int u = 0; u < TPL; ++u) {
@@ -920,9 +921,31 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
       };
       // errorRate-1 records (always 500) are rare: a branch per record only
       // in the groups that hold one
-      if (((cur.n[0].meta | cur.n[1].meta | cur.n[2].meta | cur.n[3].meta) & 0x80000000u) == 0) records(false);
+      if (((q.n[0].meta | q.n[1].meta | q.n[2].meta | q.n[3].meta) & 0x80000000u) == 0) records(false);
       else records(true);
-      cur = nxt;
+    };
+    // two groups per trip, each group's records loaded one group ahead into
+    // the other buffer (no register copy between them: with `cur = nxt` the
+    // compiler waited for each prefetch right after issuing it, so every
+    // group paid the scalar load's latency)
+    uint32_t g = g0;
+    for (; g + 1 < g1; g += 2) {
+      // the load of b issues after cur has arrived (an empty asm reads cur):
+      // scalar loads return out of order, so a wait for cur placed after
+      // b's issue would wait for b too
+      CNode4 *pb = stream + g + 1;
+      asm volatile("" : "+s"(pb) : "s"(cur.n[0].thr));
+      const Node4 b = load_group(pb);
+      grp(cur, g);
+      CNode4 *pc = stream + g + 2;  // zero tail padding
+      asm volatile("" : "+s"(pc) : "s"(b.n[0].thr));
+      cur = load_group(pc);
+      grp(b, g + 1);
+    }
+    if (g < g1) {
+      const Node4 b = load_group(stream + g + 1);
+      grp(cur, g);
+      cur = b;
     }
     // leaves respond with their own draw: their error counts (lane r =
     // record r) go to the site table in one ds_add, their 500s to errh

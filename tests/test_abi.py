@@ -169,3 +169,14 @@ def test_dynamic_walk_has_duration_table():
     off = _handler(doc, flags=native.FLAG_NO_SVC_DUR)
     assert off.info.svc_dur_rows == 0 and off.stats_words == native.ST_SITES + 2
     assert off.fold(off.new_stats())["svc_dur"] is None
+
+
+def test_des_last_batch_zero_before_any_batch():
+    """isim_des_last_batch (round 5) is host state: zero before the handler
+    served an item-engine batch; the DES class check itself needs no GPU."""
+    from isim.generators import config3p_topology
+    from isim.yamljson import obj_to_json
+    h = isim.Handler(isim.ServiceGraph.from_json(obj_to_json(config3p_topology(50, n=200))), None, isim.SimParams())
+    d = isim.DesHandler(h, 1_000_000)
+    assert d.info.items == 1
+    assert d.last_batch() == {"passes": 0, "syncs": 0, "items": 0}

@@ -211,7 +211,10 @@ def test_items_kept_queue_order(gpu, mean, monkeypatch):
     (ISIM_DES_ITEMS_NO_ORDER_REUSE) and, at a smaller size, the oracle."""
     c = DesCase(CASES["mesh_des"](), mean)
     assert c.d.info.items == 1 and c.d.info.cyclic == 1
-    c.compare(7, 1500)
+    recs, _, _ = c.compare(7, 1500)
+    # isim_des_last_batch: a cyclic schedule's quiet passes and the recording one
+    rep = c.d.last_batch()
+    assert rep["passes"] >= 2 and rep["syncs"] >= rep["passes"] and rep["items"] == int(recs["hops"].sum())
     n = 40_000
     got = c.d.serve(1 << 20, n, device=0)
     monkeypatch.setenv("ISIM_DES_ITEMS_NO_ORDER_REUSE", "1")
