@@ -300,12 +300,14 @@ ISIM_API int isim_stats_fold_durations(const isim_handler *h, const uint64_t *st
  * service.go:30-31) is a FIFO queue in front of ONE worker, held for the
  * invocation's sleep total; an invocation's script (Handler.ServeHTTP,
  * handler.go:37-79) starts when the worker takes it.  Statuses, hops and
- * call counters are those of the static walk; latencies and the per-service
- * durations include queueing.  Exact (bit-identical to the sequential
- * event-driven oracle) for the DES graph class of DESIGN.md §10.1: static
- * walks of at most 2^24 invocations and 65536 replicas per service, and
- * dynamic walks (probabilistic calls) in mode A whose lane-tree-walk tree was
- * built (isim_des_info.items; isim_des_info_get returns ISIM_EINVAL with the
+ * call counters are those of the walk; latencies and the per-service
+ * durations include queueing; in mode B a failed call step ends its script
+ * there (the worker hold stays the sleep total).  Exact (bit-identical to the
+ * sequential event-driven oracle) for the DES graph class of DESIGN.md
+ * §10.1: static walks of at most 2^24 invocations and 65536 replicas per
+ * service, and dynamic walks (probabilistic calls; in mode B, a step after
+ * one that can fail) whose lane-tree-walk tree was built
+ * (isim_des_info.items; isim_des_info_get returns ISIM_EINVAL with the
  * reason otherwise).  Times
  * are kept per trace relative to its arrival: in 32-bit rows by default;
  * a batch with a latency of 2^31 ns (2.1 s) or more is then not accumulated
@@ -330,7 +332,7 @@ typedef struct {
   int32_t cyclic;                /* 1: the call-step schedule is cyclic (fixed-point passes) */
   int32_t row_reads;             /* rows one trace's batch reads (queue + finish passes, one pass), 4 or 8 B each */
   int32_t row_writes;            /* rows it writes (the algorithmic bytes of bench.py's roofline) */
-  int32_t items;                 /* 1: a dynamic walk (probabilistic calls, mode A) on the item engine (DESIGN.md
+  int32_t items;                 /* 1: a dynamic walk (probabilistic calls, mode-B aborts) on the item engine (DESIGN.md
                                     §10.9): positions are the tree's POTENTIAL invocations, a batch simulates the
                                     executed ones and synchronizes hip_stream at its item count and bucket sizes,
                                     once per sort round whose arrival range it reads back, and (a cyclic schedule)

@@ -106,10 +106,11 @@ struct DesItemPos {
 static_assert(sizeof(DesItemPos) == 16, "DesItemPos must be 16 bytes");
 
 struct DesPlan {
-  // item engine (des_items.hip): a dynamic walk (probabilistic calls, mode A)
+  // item engine (des_items.hip): a dynamic walk (probabilistic calls, or mode-B aborts)
   // over the tree of potential invocations; only executed invocations
   // (ITEMS) are simulated
   bool items = false;
+  bool modeb = false;                // error mode B: the item engine's walks draw errors, failed steps end scripts
   std::vector<DesItemPos> item_pos;  // [n_pos]
   std::vector<uint32_t> step_round;  // [steps]: the round of each BK op | kDesStepCut
   uint32_t item_acc = 1;             // per item: callee finish maxima, one per call step (>= 1)

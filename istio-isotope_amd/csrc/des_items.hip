@@ -1,6 +1,7 @@
 // DES item engine: the exact per-replica worker-pool DES of
 // a DYNAMIC walk — probabilistic calls (shouldSkipRequest, isotope/service/
-// pkg/srv/executable.go:84-90), mode A — on the GPU.
+// pkg/srv/executable.go:84-90), and in mode B (EXT) scripts that a failed
+// call step ends (handler.go:66-75 with the 500 propagated) — on the GPU.
 //
 // The static engine (des.hip) keeps one row per (position, trace): every
 // invocation executes in every trace.  Here a trace executes a few of the
@@ -163,6 +164,10 @@ struct K {
   uint8_t *dnext;
   uint32_t cshift;
   uint16_t *irep;                  // per item: its replica (drawn once per batch)
+  // mode B: the walks draw the errors (a failed step ends its script); per
+  // item the call step it failed at (kNone: it did not fail)
+  uint32_t modeb;
+  uint32_t *ifst;
   uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
   uint32_t count_changes;          // ISIM_DES_DEBUG: changed[1] counts the values a quiet pass changed
 };
@@ -210,6 +215,7 @@ struct CountSink {
   template <typename TT>
   __device__ __forceinline__ void resp(uint32_t, uint32_t, TT, bool) {}
 };
+template <bool MB>
 struct EmitSink : CountSink {
   uint32_t *epos, *eT;
   unsigned long long *erec;
@@ -222,9 +228,12 @@ struct EmitSink : CountSink {
     erec[i] = (unsigned long long)par | (unsigned long long)(t | (own ? 0x80000000u : 0u)) << 32;
   }
   // (a lower bound is all k_relmax needs: u64 durations saturate at 2^32 - 1)
+  // mode B: the response status (a failed step, or the own error) into bit
+  // 63 of the record exec wrote; mode A draws the own errors afterwards (k_own)
   template <typename TT>
-  __device__ __forceinline__ void dur(uint32_t hop, TT T) {
+  __device__ __forceinline__ void dur(uint32_t hop, TT T, bool st) {
     eT[base + hop] = (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
+    if (MB && st) erec[base + hop] |= 1ull << 63;
   }
 };
 
@@ -242,12 +251,13 @@ struct LNodes {
   }
 };
 
-template <int FR, bool SPILL, bool EMIT, bool T64, class Nodes>
+template <int FR, bool SPILL, bool EMIT, bool T64, bool MB, class Nodes>
 __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *work, const Nodes &nodes) {
-  // no error draws in the walk (DRAW = false): in mode A an invocation's own
+  // mode A: no error draws in the walk (DRAW = false): an invocation's own
   // error changes no skip, so the walks only need the skip residues; the
-  // errors are drawn per item afterwards (k_own), fully parallel
-  tw::Lane<FR, false, true, SPILL, false, std::conditional_t<T64, uint64_t, uint32_t>> L;
+  // errors are drawn per item afterwards (k_own), fully parallel.  Mode B:
+  // the errors decide which steps run, so the walk draws them (MODEB, DRAW)
+  tw::Lane<FR, MB, true, SPILL, MB, std::conditional_t<T64, uint64_t, uint32_t>> L;
   if constexpr (SPILL) {
     L.sp = k.spill + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
     L.sp_stride = gridDim.x * blockDim.x;
@@ -257,7 +267,7 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   uint64_t nxt = 0, lim = 0;
   bool dry = false, active = false;
   uint32_t t = 0;
-  EmitSink s;
+  EmitSink<MB> s;
   s.epos = k.epos;
   s.eT = k.eT;
   s.erec = k.erec;
@@ -267,6 +277,9 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   while (true) {
     if (active && L.done) {
       if constexpr (!EMIT) k.cnt[t] = L.hops();
+      if constexpr (EMIT && MB) {  // the entry's status (its response ends the walk: no dur call)
+        if (L.root500) k.erec[s.base] |= 1ull << 63;
+      }
       active = false;
     }
     unsigned long long idle = __ballot(!active);
@@ -305,31 +318,32 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   }
 }
 
-template <int FR, bool SPILL, bool EMIT, bool LDSN, bool T64>
+template <int FR, bool SPILL, bool EMIT, bool LDSN, bool T64, bool MB>
 __global__ void __launch_bounds__(LDSN ? 1024 : kT) k_prewalk(K k, unsigned long long *work) {
   if constexpr (LDSN) {
     extern __shared__ unsigned long long s_nodes[];
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += blockDim.x) s_nodes[i] = k.nodes[i];
     __syncthreads();
-    prewalk_body<FR, SPILL, EMIT, T64>(k, work,
-                                       LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
+    prewalk_body<FR, SPILL, EMIT, T64, MB>(
+        k, work, LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
   } else {
-    prewalk_body<FR, SPILL, EMIT, T64>(k, work, GNodes{k.nodes});
+    prewalk_body<FR, SPILL, EMIT, T64, MB>(k, work, GNodes{k.nodes});
   }
 }
 
 // ---- 2a. own errors (RecordRequestReceived's status in mode A): word
 // (hop & 3) of Philox (t, hop >> 2, 0, 0) against the callee's threshold, as
 // the walk draws it (tree_walk.h own_error); the trace's 500 count by atomics
-// (errors are rare), its entry status below
+// (errors are rare), its entry status below.  Mode B: the walk wrote each
+// item's status (EmitSink::dur), only counted here
 __global__ void __launch_bounds__(kT) k_own(K k) {
   for (uint64_t i = gid(); i < k.M; i += nthreads()) {
     const unsigned long long r = k.erec[i];
     const uint32_t t = (uint32_t)(r >> 32) & 0x7FFFFFFFu;
     const uint32_t hop = (uint32_t)(i - item_off(k, t));
     const DesPos P = k.pos[k.epos[i]];
-    bool own = (P.flags & kDesFlagAlways) != 0;
-    if (!own && P.thr) {
+    bool own = k.modeb ? (r >> 63) != 0 : (P.flags & kDesFlagAlways) != 0;
+    if (!k.modeb && !own && P.thr) {
       uint32_t a = (uint32_t)(k.trace_begin + t), b = (uint32_t)((k.trace_begin + t) >> 32), c = hop >> 2, d = 0;
       tw::philox10(a, b, c, d, k.k0, k.k1);
       own = tw::word4(hop & 3u, a, b, c, d) < P.thr;
@@ -368,6 +382,15 @@ __global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm, co
     k.ipar[j] = par == kNone ? kNone : inv[par];
   }
 }
+// mode B: an item with a callee that responded 500 failed at that callee's
+// call step — the last it ran, so the smallest such step (statuses in iown)
+__global__ void __launch_bounds__(kT) k_fail(K k) {
+  for (uint64_t j = gid(); j < k.M; j += nthreads()) {
+    const uint32_t par = k.ipar[j];
+    if (par != kNone && k.iown[j]) atomicMin(k.ifst + par, (uint32_t)k.ip[k.ipos[j]].kstep);
+  }
+}
+
 // cyclic schedules: the first quiet pass starts its cut step begins from the
 // contention-free callee durations instead of zero (a lower bound of every
 // callee's finish: F(c) >= begin(step) + H(c) + T(c)), so the passes only
@@ -473,6 +496,7 @@ __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops
     if (k.dcur && !k.dcur[op >> 48]) continue;  // not recomputed in this pass
     const uint64_t i = (op >> 16) & 0xFFFFFFFFull;
     const uint32_t s = (uint32_t)(op & 0xFFFFu);
+    if (k.ifst && s > k.ifst[i]) continue;  // mode B: the script failed at an earlier step
     const DesItemPos p = k.ip[k.ipos[i]];
     const uint32_t b = p.bk_first + s;
     const uint32_t sr = k.step_round[b];
@@ -901,8 +925,16 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
         b_run = kNone;
       }
       uint64_t F;
+      const uint32_t fst = k.ifst ? k.ifst[i] : kNone;
       if (P.flags & kDesFlagLeaf) {
         F = k.IS[i] + P.floor;
+      } else if (fst != kNone) {
+        // mode B, failed at call step fst: that step's end (its begin plus its
+        // longest sleep, or its callees' finishes), no later command
+        const uint64_t b0 = p.nsteps >= 2 ? k.bk[(uint64_t)i * k.bw + fst] : k.IS[i];
+        const uint64_t sm = p.nsteps >= 2 && fst + 1u < p.nsteps ? k.steps[p.bk_first + fst + 1].smax : P.floor;
+        const uint64_t c = k.acc[(uint64_t)i * k.aw + fst];
+        F = c > b0 + sm ? c : b0 + sm;
       } else {
         const uint32_t last = p.nsteps >= 2 ? p.nsteps - 1u : 0u;
         F = (p.nsteps >= 2 ? k.bk[(uint64_t)i * k.bw + last] : k.IS[i]) + P.floor;
@@ -1091,6 +1123,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.k1 = (uint32_t)(L.seed >> 32);
   k.n_slots = L.n_slots;
   k.no_acc = std::getenv("ISIM_DES_ITEMS_NO_ACC") != nullptr;
+  k.modeb = pl.modeb ? 1u : 0u;
   const bool debug = std::getenv("ISIM_DES_DEBUG") != nullptr;
   k.count_changes = debug ? 1u : 0u;
   uint32_t max_reps = 1, max_row = 0;
@@ -1161,26 +1194,31 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     }
   };
   // the variant: register frames (8 + spill, 16, 8), nodes in LDS, time width
-  auto pw = [&](auto fr_c, auto spill_c, auto t64_c, bool emit) {
+  // (and the error mode: mode B walks draw errors)
+  auto pw = [&](auto fr_c, auto spill_c, auto t64_c, auto mb_c, bool emit) {
     constexpr int FRc = decltype(fr_c)::value;
-    constexpr bool SP = decltype(spill_c)::value, T6 = decltype(t64_c)::value;
+    constexpr bool SP = decltype(spill_c)::value, T6 = decltype(t64_c)::value, MB = decltype(mb_c)::value;
     unsigned long long *w = work + (emit ? 1 : 0);
     if (ldsn) {
-      if (emit) launch(k_prewalk<FRc, SP, true, true, T6>, w);
-      else launch(k_prewalk<FRc, SP, false, true, T6>, w);
+      if (emit) launch(k_prewalk<FRc, SP, true, true, T6, MB>, w);
+      else launch(k_prewalk<FRc, SP, false, true, T6, MB>, w);
     } else {
-      if (emit) launch(k_prewalk<FRc, SP, true, false, T6>, w);
-      else launch(k_prewalk<FRc, SP, false, false, T6>, w);
+      if (emit) launch(k_prewalk<FRc, SP, true, false, T6, MB>, w);
+      else launch(k_prewalk<FRc, SP, false, false, T6, MB>, w);
     }
   };
-  auto prewalk_t = [&](auto t64_c, bool emit) {
-    if (spill) pw(std::integral_constant<int, 8>{}, std::true_type{}, t64_c, emit);
-    else if (fr > 8) pw(std::integral_constant<int, 16>{}, std::false_type{}, t64_c, emit);
-    else pw(std::integral_constant<int, 8>{}, std::false_type{}, t64_c, emit);
+  auto prewalk_t = [&](auto t64_c, auto mb_c, bool emit) {
+    if (spill) pw(std::integral_constant<int, 8>{}, std::true_type{}, t64_c, mb_c, emit);
+    else if (fr > 8) pw(std::integral_constant<int, 16>{}, std::false_type{}, t64_c, mb_c, emit);
+    else pw(std::integral_constant<int, 8>{}, std::false_type{}, t64_c, mb_c, emit);
+  };
+  auto prewalk_m = [&](auto mb_c, bool emit) {
+    if (L.tree_t64) prewalk_t(std::true_type{}, mb_c, emit);
+    else prewalk_t(std::false_type{}, mb_c, emit);
   };
   auto prewalk = [&](bool emit) {
-    if (L.tree_t64) prewalk_t(std::true_type{}, emit);
-    else prewalk_t(std::false_type{}, emit);
+    if (pl.modeb) prewalk_m(std::true_type{}, emit);
+    else prewalk_m(std::false_type{}, emit);
   };
   if (hipMemsetAsync(work, 0, 16, s) != hipSuccess) return fail("memset");
   prewalk(false);
@@ -1236,7 +1274,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       (uint64_t)(pl.pos.size() + 1) * 4, (uint64_t)pl.pos.size() * 4, (uint64_t)pl.pos.size() * 4,  // poff qdst fdst
       tmp_bytes,
       M * 2, (n >> chunk_shift(n)) + 1, (n >> chunk_shift(n)) + 1,  // replicas; the two chunk-change maps
-      pl.cyclic ? M * 2 : 2};                                   // kept orders' trace chunks
+      pl.cyclic ? M * 2 : 2,                                    // kept orders' trace chunks
+      pl.modeb ? M * 4 : 4};                                    // mode B: failed call step per item
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
   if (!pool_alloc(item_mem, total)) return fail("item allocation");
@@ -1295,6 +1334,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   const uint64_t n_chunks = (n >> k.cshift) + 1;
   uint8_t *chg_a = (uint8_t *)carve(parts[49]), *chg_b = (uint8_t *)carve(parts[50]);
   uint16_t *ordc = (uint16_t *)carve(parts[51]);
+  uint32_t *ifst = (uint32_t *)carve(parts[52]);
+  k.ifst = pl.modeb ? ifst : nullptr;
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -1322,6 +1363,13 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     }
     hipLaunchKernelGGL(k_perm_inv, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
     hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
+    if (pl.modeb) {
+      if (hipMemsetAsync(ifst, 0xFF, M * 4, s) != hipSuccess) {
+        rc = fail("memset");
+        break;
+      }
+      hipLaunchKernelGGL(k_fail, dim3(grid_for(M)), dim3(kT), 0, s, k);
+    }
     hipLaunchKernelGGL(k_roots, dim3(grid_for(n)), dim3(kT), 0, s, k, inv);
     hipLaunchKernelGGL(k_reps, dim3(grid_for(M)), dim3(kT), 0, s, k);
     if (pl.cyclic) {  // the first pass's cut step begins: contention-free callee maxima (k_relmax)

@@ -100,10 +100,12 @@ void des_row_traffic(const DesPlan &plan, uint32_t &reads, uint32_t &writes) {
 
 int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan &out, std::string &err) {
   out = DesPlan();
+  out.modeb = modeb;
   // the positions: a static walk's draw stream (every invocation executes in
-  // every trace), or — probabilistic calls in mode A — the lane tree walk's
-  // unrolled tree of POTENTIAL invocations (kernel_abi.h TreeNode): the item
-  // engine (des_items.hip) simulates the executed ones only
+  // every trace), or — probabilistic calls, or mode-B aborts (a call step
+  // after one that can fail) — the lane tree walk's unrolled tree of
+  // POTENTIAL invocations (kernel_abi.h TreeNode): the item engine
+  // (des_items.hip) simulates the executed ones only
   struct Src {
     uint32_t slot, parent, thr;
     bool always;
@@ -118,7 +120,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
       stack.push_back(i);
       for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
     }
-  } else if (!p.static_walk && !p.tree_nodes.empty() && !modeb) {
+  } else if (!p.static_walk && !p.tree_nodes.empty()) {
     out.items = true;
     std::vector<std::pair<uint32_t, uint32_t>> stack;  // (position, end of its subtree)
     for (uint32_t i = 0; i < (uint32_t)p.tree_nodes.size(); ++i) {
@@ -130,8 +132,6 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
     }
   } else {
     err = p.static_walk ? "DES needs a static walk of at most 2^24 invocations"
-          : modeb       ? "DES in mode B needs a static walk (no probabilistic calls, no call step after one that "
-                          "can fail); dynamic walks run on the item engine in mode A only"
                         : "DES of a dynamic walk needs the lane tree walk's unrolled tree (" + p.tree_why + ")";
     return ISIM_EINVAL;
   }

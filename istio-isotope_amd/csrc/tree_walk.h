@@ -131,10 +131,10 @@ ISIM_TW uint32_t pack_res(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 // of a leaf callee (its duration is static); resp(slot, row word, T,
 // status) per response of a calling callee (the entry's is the trace result);
 // optionally exec(position, hop, caller hop, own error) per executed
-// invocation, entry included (caller hop kNoCaller), and then dur(hop, T)
-// per response of a callee (its duration without contention) — the DES
-// item engine's pre-walk (des_items.hip) records the executed invocations
-// with them.
+// invocation, entry included (caller hop kNoCaller), and then dur(hop, T,
+// status) per response of a callee (its duration without contention and its
+// status: the own error, or in mode B a failed step) — the DES item engine's
+// pre-walk (des_items.hip) records the executed invocations with them.
 constexpr uint32_t kNoCaller = 0xFFFFFFFFu;
 template <class S, class = void>
 struct has_exec {
@@ -350,7 +350,7 @@ TW_PRAGMA_UNROLL
       return false;
     }
     sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
-    if constexpr (has_exec<Sink>::value) sink.dur(f_hf & 0xFFFFu, T);
+    if constexpr (has_exec<Sink>::value) sink.dur(f_hf & 0xFFFFu, T, st);
     const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
     pop();
@@ -395,7 +395,7 @@ TW_PRAGMA_UNROLL
         return;
       }
       sink.resp_leaf(n.slot(), own);
-      if constexpr (has_exec<Sink>::value) sink.dur(hop, x.tc);
+      if constexpr (has_exec<Sink>::value) sink.dur(hop, x.tc, own);
       fold((TT)x.H + x.tc, own, (fl & TF_CONC) != 0);
       p += 1;
       return;

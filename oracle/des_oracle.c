@@ -15,11 +15,16 @@
  * over the SERVICE GRAPH (as isim_oracle.c's invoke() does), so this shares
  * no code or layout with the product's position arrays and level scans.
  *
- * Probabilistic calls (mode A): before the simulation, a walk of each trace
- * (as isim_oracle.c's invoke(): shouldSkipRequest with Intn(100) := draw %
- * 100, hop ids counting EXECUTED invocations in preorder) fixes which calls
+ * Probabilistic calls: before the simulation, a walk of each trace (as
+ * isim_oracle.c's invoke(): shouldSkipRequest with Intn(100) := draw % 100,
+ * hop ids counting EXECUTED invocations in preorder) fixes which calls
  * execute and every executed invocation's hop id; a skipped call sends no
- * request, holds nothing and takes no time.
+ * request, holds nothing and takes no time.  In mode B (EXT) the walk also
+ * draws the errors: a step with a callee that responded 500 fails the script
+ * (handler.go:66-75 with the 500 propagated), whose later commands never run
+ * — the walk records the command after which each invocation stops, and the
+ * simulation responds to the caller there (the worker hold stays the
+ * service's sleep total).
  *
  * Reference anchors (the simulated behaviour, not a Go transcription):
  *   Handler.ServeHTTP          isotope/service/pkg/srv/handler.go:37-79
@@ -167,7 +172,7 @@ static uint32_t subtree(sctx *c, int32_t s) {
     return (uint32_t)n;
 }
 
-/* ---- the executed invocations of one trace (mode A: skips only) ---- */
+/* ---- the executed invocations of one trace (skips; mode B: aborts) ---- */
 #define NO_HOP 0xFFFFFFFFu
 typedef struct {
     const sctx *c;
@@ -175,7 +180,8 @@ typedef struct {
     uint32_t next;       /* next hop id = executed invocations so far */
     uint32_t kid_next;
     uint32_t *kid_base;  /* [nodes] per hop: its entries in kid */
-    uint32_t *kid;       /* per (hop, call command k): the callee's hop, NO_HOP when skipped */
+    uint32_t *kid;       /* per (hop, call command k): the callee's hop, NO_HOP when skipped or aborted */
+    uint32_t *stop;      /* [nodes] per hop: script commands that run (mode B: up to the failed step) */
 } pwalk;
 
 /* shouldSkipRequest (executable.go:84-90) with Intn(100) := draw % 100 (isim_oracle.c skip_call) */
@@ -184,23 +190,44 @@ static int skip_call(uint64_t seed, uint64_t t, uint32_t hop, int32_t k, int32_t
     return draw(seed, t, hop, 1u + ((uint32_t)k >> 2), k & 3) % 100u < (uint32_t)(100 - q);
 }
 
-static uint32_t pre_walk(pwalk *w, int32_t s) {
+/* own error draw of invocation `hop` of service s (the respond point) */
+static int own_error(const sctx *c, uint64_t t, int32_t s, uint32_t hop) {
+    const uint64_t thr = c->g->thr[s];
+    if (thr >= (1ull << 32)) return 1;
+    return thr > 0 && (uint64_t)draw(c->p->seed, t, hop >> 2, 0u, (int)(hop & 3)) < thr;
+}
+
+/* *err: the invocation's status 500 (mode B: a failed step or its own error) */
+static uint32_t pre_walk(pwalk *w, int32_t s, int *err) {
     const ograph *g = w->c->g;
+    const int modeb = w->c->p->error_mode == 1;
     const uint32_t hop = w->next++;
     const uint32_t base = w->kid_next;
     w->kid_base[hop] = base;
     w->kid_next += w->c->ncalls[s];
+    int failed = 0;
+    uint32_t stop = (uint32_t)g->step_len[s];
     for (int32_t i = 0; i < g->step_len[s]; ++i) {
         const ocmd *x = &g->cmds[g->step_off[s] + i];
         const int32_t nsub = x->kind == K_CONC ? x->sub_len : 1;
+        int cerr = 0;
         for (int32_t j = 0; j < nsub; ++j) {
             const ocmd *y = x->kind == K_CONC ? &g->cmds[x->sub_off + j] : x;
             if (y->kind != K_CALL) continue;
-            w->kid[base + (uint32_t)y->k] = skip_call(w->c->p->seed, w->t, hop, y->k, g->site_prob[y->site])
-                                                ? NO_HOP
-                                                : pre_walk(w, g->site_callee[y->site]);
+            int e = 0;
+            w->kid[base + (uint32_t)y->k] =
+                failed || skip_call(w->c->p->seed, w->t, hop, y->k, g->site_prob[y->site])
+                    ? NO_HOP
+                    : pre_walk(w, g->site_callee[y->site], &e);
+            cerr |= e;
+        }
+        if (modeb && cerr && !failed) {  /* the script responds after this step */
+            failed = 1;
+            stop = (uint32_t)i + 1u;
         }
     }
+    w->stop[hop] = stop;
+    *err = modeb && (failed || own_error(w->c, w->t, s, hop));  /* mode A: unused, not drawn */
     return hop;
 }
 
@@ -308,11 +335,7 @@ static uint64_t finish(fstate *f, int32_t s, uint32_t hop, int *err) {
             if (cerr) failed = 1;
         }
     }
-    const uint64_t thr = g->thr[s];
-    int own = 0;
-    if (thr >= (1ull << 32)) own = 1;
-    else if (thr > 0) own = (uint64_t)draw(c->p->seed, f->t, hop >> 2, 0u, (int)(hop & 3)) < thr;
-    const int e = failed ? 1 : own;
+    const int e = failed ? 1 : own_error(c, f->t, s, hop);
     if (e) {
         st[ST_SVC + g->n_services + s] += 1;
         f->err_hops += 1;
@@ -347,6 +370,7 @@ typedef struct {
     uint32_t nodes;
     uint64_t trace_begin;
     const uint32_t *kid_base, *kid;  /* [n_traces][nodes]: the executed calls (pwalk) */
+    const uint32_t *stop;            /* [n_traces][nodes]: commands each invocation runs (pwalk) */
 } sim;
 
 static int advance(sim *m, uint64_t i, uint32_t hop);
@@ -377,7 +401,8 @@ static int advance(sim *m, uint64_t i, uint32_t hop) {
     const ograph *g = m->c->g;
     istate *st = &m->is[i * m->nodes + hop];
     const int32_t s = st->svc;
-    while (st->step < (uint32_t)g->step_len[s]) {
+    const uint32_t stop = m->stop[i * m->nodes + hop];
+    while (st->step < stop) {
         const ocmd *x = &g->cmds[g->step_off[s] + st->step];
         st->step++;
         if (x->kind == K_SLEEP) {
@@ -448,16 +473,18 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
      * executed invocation is a distinct potential position: <= nodes entries) */
     uint32_t *kid_base = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * nodes * sizeof(uint32_t));
     uint32_t *kid = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * nodes * sizeof(uint32_t));
+    uint32_t *stop = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * nodes * sizeof(uint32_t));
     uint32_t *hops = (uint32_t *)malloc((size_t)(n_traces ? n_traces : 1) * sizeof(uint32_t));
-    if (!is || !kid_base || !kid || !hops) return 2;
+    if (!is || !kid_base || !kid || !stop || !hops) return 2;
     for (uint64_t i = 0; i < n_traces; ++i) {
         is[i * nodes].parent = NO_PARENT;
         is[i * nodes].svc = p->entry;
-        pwalk w = {&c, trace_begin + i, 0, 0, kid_base + i * nodes, kid + i * nodes};
-        (void)pre_walk(&w, p->entry);
+        pwalk w = {&c, trace_begin + i, 0, 0, kid_base + i * nodes, kid + i * nodes, stop + i * nodes};
+        int e = 0;
+        (void)pre_walk(&w, p->entry, &e);
         hops[i] = w.next;
     }
-    sim m = {&c, &h, is, nodes, trace_begin, kid_base, kid};
+    sim m = {&c, &h, is, nodes, trace_begin, kid_base, kid, stop};
     while (h.n) {
         const ev e = hpop(&h);
         const uint64_t i = e.t - trace_begin;
@@ -500,6 +527,7 @@ int isim_oracle_des_run(const ograph *g, const oparams *p, const odes *d, uint64
     }
     free(h.v);
     free(hops);
+    free(stop);
     free(kid);
     free(kid_base);
     free(arr);

@@ -6,7 +6,8 @@
 // only: tests/test_des_items.py runs it and compares its records, stats and
 // DES table with the event-driven oracle (oracle/des_oracle.c) — the
 // algorithm checked on the CPU, the HIP kernels by tests/test_des_items_gpu.py.
-//   des_items_check <graph.json> <seed> <hop_base> <req_ps> <resp_ps> <mean_ns> <begin> <n> <out prefix>
+//   des_items_check <graph.json> <seed> <hop_base> <req_ps> <resp_ps> <mean_ns> <begin> <n> <out prefix> [mode]
+// (mode 1: error mode B — a failed call step ends its script)
 // writes <prefix>.rec (n x 16 B), <prefix>.stats (u64), <prefix>.table (u64 rows)
 #include <algorithm>
 #include <cstdio>
@@ -60,9 +61,12 @@ struct Sink {
   void call(uint32_t) {}
   void resp_leaf(uint32_t, bool) {}
   void resp(uint32_t, uint32_t, uint64_t, bool) {}
-  void dur(uint32_t hop, uint64_t T) {
+  // (after exec: the status replaces the own error — they differ only when a
+  // mode-B step failed)
+  void dur(uint32_t hop, uint64_t T, bool st) {
     if (dur_of->size() <= base + hop) dur_of->resize(base + hop + 1);
     (*dur_of)[base + hop] = T;
+    (*items)[base + hop].own = st ? 1 : 0;
   }
   void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
     if (items->size() <= base + hop) items->resize(base + hop + 1);
@@ -70,6 +74,23 @@ struct Sink {
                                 (uint8_t)(own ? 1 : 0)};
   }
 };
+
+template <bool MB>
+void walk_all(const Program &prog, uint64_t seed, uint64_t begin, uint64_t n, std::vector<Item> &items,
+              std::vector<uint64_t> &dur_of, std::vector<uint64_t> &toff, std::vector<uint32_t> &terr) {
+  tw::Lane<kTreeMaxFrames + 1, MB, true, false, true, uint64_t> L;
+  const tw::CpuNodes nodes{prog.tree_nodes.data()};
+  for (uint64_t t = 0; t < n; ++t) {
+    Sink s{&items, &dur_of, toff[t], (uint32_t)t};
+    L.start(begin + t);
+    while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), s, (uint32_t)seed,
+                           (uint32_t)(seed >> 32));
+    toff[t + 1] = toff[t] + L.hops();
+    items.resize(toff[t + 1]);
+    items[toff[t]].own = L.root500 ? 1 : 0;
+    terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
+  }
+}
 
 }  // namespace
 
@@ -93,7 +114,8 @@ int main(int argc, char **argv) {
   prm.hop_base_ns = std::stoull(argv[3]);
   prm.req_ps_per_byte = std::stoull(argv[4]);
   prm.resp_ps_per_byte = std::stoull(argv[5]);
-  prm.error_mode = ISIM_MODE_A;
+  const bool modeb = argc > 10 && std::stoi(argv[10]) == 1;
+  prm.error_mode = modeb ? ISIM_MODE_B : ISIM_MODE_A;
   prm.flags = ISIM_FLAG_DYNAMIC;
   const uint64_t mean = std::stoull(argv[6]), begin = std::stoull(argv[7]), n = std::stoull(argv[8]);
   const std::string out = argv[9];
@@ -103,7 +125,7 @@ int main(int argc, char **argv) {
     return 2;
   }
   DesPlan pl;
-  if (build_des_plan(g, prog, false, pl, err) != ISIM_OK || !pl.items) {
+  if (build_des_plan(g, prog, modeb, pl, err) != ISIM_OK || !pl.items) {
     std::fprintf(stderr, "plan: %s\n", err.c_str());
     return 3;
   }
@@ -120,20 +142,16 @@ int main(int argc, char **argv) {
   std::vector<uint64_t> dur_of;
   std::vector<uint64_t> toff(n + 1, 0);
   std::vector<uint32_t> terr(n);
-  {
-    tw::Lane<kTreeMaxFrames + 1, false, true, false, true, uint64_t> L;
-    const tw::CpuNodes nodes{prog.tree_nodes.data()};
-    for (uint64_t t = 0; t < n; ++t) {
-      Sink s{&items, &dur_of, toff[t], (uint32_t)t};
-      L.start(begin + t);
-      while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), s, (uint32_t)seed,
-                             (uint32_t)(seed >> 32));
-      toff[t + 1] = toff[t] + L.hops();
-      items.resize(toff[t + 1]);
-      terr[t] = (L.root500 ? 0x80000000u : 0u) | L.errs();
-    }
-  }
+  if (modeb) walk_all<true>(prog, seed, begin, n, items, dur_of, toff, terr);
+  else walk_all<false>(prog, seed, begin, n, items, dur_of, toff, terr);
   const uint64_t M = items.size();
+  // mode B: an invocation with a callee that responded 500 failed at that
+  // callee's call step (the last one it ran: no later step has callees)
+  std::vector<uint32_t> fst(M, kNone);
+  if (modeb)
+    for (uint64_t i = 0; i < M; ++i)
+      if (items[i].par != kNone && items[i].own)
+        fst[items[i].par] = std::min<uint32_t>(fst[items[i].par], pl.item_pos[items[i].pos].kstep);
   const uint32_t aw = pl.item_acc, bw = std::max<uint32_t>(1, pl.item_bk);
   std::vector<uint64_t> IA(M, 0), IS(M, 0), IF(M, 0), bk(M * bw, 0), acc(M * aw, 0), accp(M * aw, 0);
   const uint32_t n_slots = (uint32_t)prog.n_slots;
@@ -177,7 +195,7 @@ int main(int argc, char **argv) {
       for (uint64_t i = 0; i < M; ++i) {
         const DesItemPos &p = pl.item_pos[items[i].pos];
         if (p.nsteps < 2) continue;
-        for (uint32_t s = 0; s < p.nsteps; ++s) {
+        for (uint32_t s = 0; s < p.nsteps && s <= fst[i]; ++s) {  // (a failed script's later steps never begin)
           const uint32_t b = p.bk_first + s, sr = pl.step_round[b];
           if ((sr & ~kDesStepCut) != r) continue;
           const DesStep &st = pl.steps[b];
@@ -242,6 +260,13 @@ int main(int argc, char **argv) {
           uint64_t F;
           if (P.flags & kDesFlagLeaf) {
             F = IS[i] + P.floor;
+          } else if (fst[i] != kNone) {
+            // failed at call step j: the step's end — its begin plus its longest
+            // sleep, or its callees' finishes — and no later command
+            const uint32_t j = fst[i];
+            const uint64_t b0 = p.nsteps >= 2 ? bk[i * bw + j] : IS[i];
+            const uint64_t sm = p.nsteps >= 2 && j + 1u < p.nsteps ? pl.steps[p.bk_first + j + 1].smax : P.floor;
+            F = std::max(b0 + sm, acc[i * aw + j]);
           } else {
             const uint32_t last = p.nsteps >= 2 ? p.nsteps - 1u : 0u;
             F = (p.nsteps >= 2 ? bk[i * bw + last] : IS[i]) + P.floor;

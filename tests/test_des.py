@@ -103,7 +103,21 @@ def test_des_class():
     # probabilistic calls: the item engine (mode A) over the tree's potential invocations
     dm = isim.DesHandler(_handler(mesh_topology(800, 4)), 1_000_000)
     assert dm.info.items == 1 and dm.info.n_positions == 40 and dm.info.n_fused == 0
-    _rejects(_handler(mesh_topology(800, 4), error_mode=isim.MODE_B), "mode A")
+    # mode B: the same engine, its walks drawing the errors (a failed step ends the script)
+    db = isim.DesHandler(_handler(mesh_topology(800, 4), error_mode=isim.MODE_B), 1_000_000)
+    assert db.info.items == 1 and db.info.n_positions == 40
+    # a call step after one that can fail: dynamic in mode B only
+    seq = tree_topology(2, 3, sequential=True)
+    for sv in seq["services"]:
+        sv["errorRate"] = 0.1
+    assert isim.DesHandler(_handler(seq), 1_000_000).info.items == 0
+    assert isim.DesHandler(_handler(seq, error_mode=isim.MODE_B), 1_000_000).info.items == 1
+    # a dynamic walk needs the lane tree walk's tree (at most 65,535 potential invocations)
+    # (a chain of 17 services each calling the next twice: 2^17 - 1 positions)
+    big = {"services": [{"name": f"s{i}", "isEntrypoint": i == 0,
+                         "script": [{"call": {"service": f"s{i + 1}", "probability": 50}}] * 2 if i < 16 else []}
+                        for i in range(17)]}
+    _rejects(_handler(big), "unrolled tree")
     doc = tree_topology(3, 3)
     doc["services"][-1]["numReplicas"] = 65
     isim.DesHandler(_handler(doc), 1_000_000)  # no sleeps: never queues, replicas do not matter

@@ -20,7 +20,7 @@ from oracle import graph_ref as gr
 from oracle.executor_py import SimGraph
 
 from parity import assert_records_equal, assert_stats_equal, oracle_params
-from test_des_items_gpu import CASES
+from test_des_items_gpu import CASES, MODE_B_CASES
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "istio-isotope_amd", "csrc")
@@ -38,15 +38,18 @@ def checker(tmp_path_factory):
     return out
 
 
-def _check(checker, tmp_path, doc, mean, begin, n):
+def _check(checker, tmp_path, doc, mean, begin, n, mode=isim.MODE_A):
     j = obj_to_json(doc)
     (tmp_path / "g.json").write_text(j)
-    h = isim.Handler(isim.ServiceGraph.from_json(j), None, isim.SimParams(flags=isim.native.FLAG_DYNAMIC))
+    h = isim.Handler(isim.ServiceGraph.from_json(j), None,
+                     isim.SimParams(flags=isim.native.FLAG_DYNAMIC, error_mode=mode))
     d = isim.DesHandler(h, mean)
+    assert d.info.items == 1
     p = h.params
     prefix = str(tmp_path / "out")
     r = subprocess.run([checker, str(tmp_path / "g.json"), str(p.seed), str(p.hop_base_ns), str(p.req_ps_per_byte),
-                        str(p.resp_ps_per_byte), str(mean), str(begin), str(n), prefix],
+                        str(p.resp_ps_per_byte), str(mean), str(begin), str(n), prefix,
+                        "1" if mode == isim.MODE_B else "0"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr + r.stdout
     rec = np.fromfile(prefix + ".rec", np.uint64).reshape(n, 2)
@@ -80,3 +83,14 @@ def test_restatement_matches_event_oracle(checker, tmp_path, name, mean):
     if name in ("canonical_p50", "mesh_des"):
         assert "cyclic 1" in out  # the fixed-point passes are exercised
     _check(checker, tmp_path, CASES[name](), mean, (1 << 32) - 300, 601)
+
+
+@pytest.mark.parametrize("mean", [300_000, 3_000_000])
+@pytest.mark.parametrize("name", sorted(MODE_B_CASES))
+def test_restatement_mode_b(checker, tmp_path, name, mean):
+    """Mode B: the walks draw errors, a failed call step ends its script (no
+    later step, sleep or call), the worker hold stays the service's sleep
+    total; the oracle's walk records where each script
+    stops and its simulation responds there."""
+    _check(checker, tmp_path, MODE_B_CASES[name](), mean, 1000, 1500, isim.MODE_B)
+    _check(checker, tmp_path, MODE_B_CASES[name](), mean, (1 << 32) - 300, 601, isim.MODE_B)

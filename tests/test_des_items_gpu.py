@@ -1,5 +1,6 @@
 """GPU parity of the DES item engine: dynamic walks —
-probabilistic calls (shouldSkipRequest, executable.go:84-90), mode A — under
+probabilistic calls (shouldSkipRequest, executable.go:84-90), and mode-B
+aborts (a failed call step ends its script, handler.go:66-75) — under
 per-replica worker-pool contention, through the C ABI, against the
 sequential event-driven C oracle (oracle/des_oracle.c: its pre-walk fixes the
 executed calls and hop ids) — records, stats and the per-service DES table,
@@ -85,6 +86,33 @@ CASES = {
 }
 
 
+def _err(doc, rate):
+    doc = json.loads(json.dumps(doc))
+    for i, s in enumerate(doc["services"]):
+        s["errorRate"] = rate if not isinstance(rate, list) else rate[i % len(rate)]
+    return doc
+
+
+# mode B (EXT): a callee's 500 fails its call step and ends the caller's
+# script (handler.go:66-75 with the 500 propagated); a call step or sleep
+# after a step that can fail makes the walk dynamic even without
+# probabilities, so these run on the item engine
+MODE_B_CASES = {
+    # sequential steps with sleeps between and after: aborts skip both
+    "seq_tree_abort": lambda: _err(_sleepy(tree_topology(3, 3, sequential=True)), [0.15, 0.0, 0.3]),
+    # concurrent steps: the step waits for every callee, then the script ends
+    "conc_tree_abort": lambda: _err(_sleepy_tree(3, 4, reps_leaves=2), [0.2, 0.0, 0.05]),
+    "canonical_p50_b": lambda: _err(_sleepy(_prob_canonical()), 0.1),
+    "zero_hold_mix_b": lambda: _err(_zero_hold_mix(), [0.0, 0.3, 0.2, 0.5, 0.25]),
+    "real300p60_b": CASES["real300p60"],
+    "real300seq_b": CASES["real300seq_p75"],
+    "real300seq_t64_b": CASES["real300seq_t64"],
+    # rare errors: most traces run every step, a few abort deep in the tree
+    "real300seq_lo_b": lambda: realistic_topology(300, sleep_ms=(1, 5), error_rate=(0.0, 0.004), probability=75),
+    "mesh_des_b": lambda: _err(mesh_des_topology(4000, 6, 3, 40), [0.0, 0.02, 0.1]),
+}
+
+
 @pytest.mark.parametrize("mean", [300_000, 3_000_000])
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_items_match_event_oracle(gpu, name, mean):
@@ -92,6 +120,16 @@ def test_items_match_event_oracle(gpu, name, mean):
     assert c.d.info.items == 1
     recs, _, rows = c.compare(1000, 3000)
     assert 0 < int(recs["hops"].sum()) < 3000 * int(c.h.info.hops_upper) or c.h.info.hops_upper == 1
+    c.compare((1 << 32) - 500, 1001)
+
+
+@pytest.mark.parametrize("mean", [300_000, 3_000_000])
+@pytest.mark.parametrize("name", sorted(MODE_B_CASES))
+def test_items_mode_b(gpu, name, mean):
+    c = DesCase(MODE_B_CASES[name](), mean, error_mode=isim.MODE_B)
+    assert c.d.info.items == 1
+    recs, _, _ = c.compare(1000, 3000)
+    assert int((recs["status_err"] >> 31).sum()) > 0  # some trace's entry responded 500
     c.compare((1 << 32) - 500, 1001)
 
 
