@@ -135,10 +135,11 @@ struct K {
   uint32_t *ipos, *ipar, *itr, *ihop;
   uint8_t *iown;
   uint32_t *troot;                 // per trace: its entry item (items are renumbered position-major)
-  // the pre-walk's items in trace order, before the renumbering: position,
-  // and caller item | (trace | own error << 31) << 32; duration without contention
-  uint32_t *epos, *eT;
-  unsigned long long *erec;
+  // the pre-walk's items in trace order, before the renumbering: one 16-byte
+  // record each (one line touched per item, not one per field) — x: position
+  // | hop << 16, y: duration without contention (saturated), z: caller hop
+  // (kNone: the entry), w: trace | status << 31
+  uint4 *erec;
   uint64_t *IA, *IS, *IF, *acc, *bk;
   const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
   const uint64_t *row_hold;        // per duration-table row: the service's worker hold
@@ -215,25 +216,23 @@ struct CountSink {
   template <typename TT>
   __device__ __forceinline__ void resp(uint32_t, uint32_t, TT, bool) {}
 };
+// records of the current trace go to rec[base + hop]
 template <bool MB>
 struct EmitSink : CountSink {
-  uint32_t *epos, *eT;
-  unsigned long long *erec;
+  uint4 *rec;
   uint64_t base;
   uint32_t t;
   __device__ __forceinline__ void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
-    const uint64_t i = base + hop;
-    epos[i] = p;
-    const uint32_t par = caller == tw::kNoCaller ? kNone : (uint32_t)(base + caller);
-    erec[i] = (unsigned long long)par | (unsigned long long)(t | (own ? 0x80000000u : 0u)) << 32;
+    rec[base + hop] = uint4{p | hop << 16, 0u, caller == tw::kNoCaller ? kNone : caller, t | (own ? 0x80000000u : 0u)};
   }
   // (a lower bound is all k_relmax needs: u64 durations saturate at 2^32 - 1)
   // mode B: the response status (a failed step, or the own error) into bit
-  // 63 of the record exec wrote; mode A draws the own errors afterwards (k_own)
+  // 31 of w; mode A draws the own errors afterwards (k_own)
   template <typename TT>
   __device__ __forceinline__ void dur(uint32_t hop, TT T, bool st) {
-    eT[base + hop] = (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
-    if (MB && st) erec[base + hop] |= 1ull << 63;
+    const uint64_t i = base + hop;
+    rec[i].y = (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
+    if (MB && st) rec[i].w |= 0x80000000u;
   }
 };
 
@@ -268,9 +267,7 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   bool dry = false, active = false;
   uint32_t t = 0;
   EmitSink<MB> s;
-  s.epos = k.epos;
-  s.eT = k.eT;
-  s.erec = k.erec;
+  s.rec = k.erec;
   s.base = 0;
   s.t = 0;
   CountSink cs;
@@ -278,7 +275,7 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
     if (active && L.done) {
       if constexpr (!EMIT) k.cnt[t] = L.hops();
       if constexpr (EMIT && MB) {  // the entry's status (its response ends the walk: no dur call)
-        if (L.root500) k.erec[s.base] |= 1ull << 63;
+        if (L.root500) s.rec[s.base].w |= 0x80000000u;
       }
       active = false;
     }
@@ -335,26 +332,29 @@ __global__ void __launch_bounds__(LDSN ? 1024 : kT) k_prewalk(K k, unsigned long
 // (hop & 3) of Philox (t, hop >> 2, 0, 0) against the callee's threshold, as
 // the walk draws it (tree_walk.h own_error); the trace's 500 count by atomics
 // (errors are rare), its entry status below.  Mode B: the walk wrote each
-// item's status (EmitSink::dur), only counted here
-__global__ void __launch_bounds__(kT) k_own(K k) {
+// item's status (EmitSink::dur), only counted here.  Runs in trace order
+// after the renumbering's inverse (inv) is known: the caller hop becomes the
+// caller's NEW index here, where the caller's inv entry is a near read (same
+// trace), so k_perm_apply gathers nothing but the record
+__global__ void __launch_bounds__(kT) k_own(K k, const uint32_t *inv) {
   for (uint64_t i = gid(); i < k.M; i += nthreads()) {
-    const unsigned long long r = k.erec[i];
-    const uint32_t t = (uint32_t)(r >> 32) & 0x7FFFFFFFu;
-    const uint32_t hop = (uint32_t)(i - item_off(k, t));
-    const DesPos P = k.pos[k.epos[i]];
-    bool own = k.modeb ? (r >> 63) != 0 : (P.flags & kDesFlagAlways) != 0;
+    const uint4 r = k.erec[i];
+    const uint32_t t = r.w & 0x7FFFFFFFu;
+    const uint32_t hop = r.x >> 16;
+    const DesPos P = k.pos[r.x & 0xFFFFu];
+    bool own = k.modeb ? (r.w >> 31) != 0 : (P.flags & kDesFlagAlways) != 0;
     if (!k.modeb && !own && P.thr) {
       uint32_t a = (uint32_t)(k.trace_begin + t), b = (uint32_t)((k.trace_begin + t) >> 32), c = hop >> 2, d = 0;
       tw::philox10(a, b, c, d, k.k0, k.k1);
       own = tw::word4(hop & 3u, a, b, c, d) < P.thr;
     }
-    k.erec[i] = (r & ~(1ull << 63)) | ((unsigned long long)own << 63);
+    k.erec[i] = uint4{r.x, r.y, r.z == kNone ? kNone : inv[i - hop + r.z], t | (own ? 0x80000000u : 0u)};
     if (own) atomicAdd(k.terr + t, 1u);
   }
 }
 __global__ void __launch_bounds__(kT) k_root500(K k) {
   for (uint64_t t = gid(); t < k.n; t += nthreads())
-    if (k.erec[item_off(k, t)] >> 63) k.terr[t] |= 0x80000000u;
+    if (k.erec[item_off(k, t)].w >> 31) k.terr[t] |= 0x80000000u;
 }
 
 // ---- 2b. renumbering: items in (position, trace) order (a stable radix
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(kT) k_root500(K k) {
 // position), read the per-item arrays nearly in sequence
 __global__ void __launch_bounds__(kT) k_perm_keys(K k, uint32_t *key, uint32_t *val) {
   for (uint64_t i = gid(); i < k.M; i += nthreads()) {
-    key[i] = k.epos[i];
+    key[i] = k.erec[i].x & 0xFFFFu;
     val[i] = (uint32_t)i;
   }
 }
@@ -371,15 +371,13 @@ __global__ void __launch_bounds__(kT) k_perm_keys(K k, uint32_t *key, uint32_t *
 __global__ void __launch_bounds__(kT) k_perm_inv(K k, const uint32_t *perm, uint32_t *inv) {
   for (uint64_t j = gid(); j < k.M; j += nthreads()) inv[perm[j]] = (uint32_t)j;
 }
-__global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm, const uint32_t *inv) {
+__global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm) {
   for (uint64_t j = gid(); j < k.M; j += nthreads()) {
-    const uint32_t i = perm[j];
-    const unsigned long long r = k.erec[i];
-    const uint32_t par = (uint32_t)r, t = (uint32_t)(r >> 32) & 0x7FFFFFFFu;
-    k.itr[j] = t;
-    k.iown[j] = (uint8_t)(r >> 63);
-    k.ihop[j] = (uint32_t)(i - item_off(k, t));
-    k.ipar[j] = par == kNone ? kNone : inv[par];
+    const uint4 r = k.erec[perm[j]];
+    k.itr[j] = r.w & 0x7FFFFFFFu;
+    k.iown[j] = (uint8_t)(r.w >> 31);
+    k.ihop[j] = r.x >> 16;
+    k.ipar[j] = r.z;  // the caller's new index (k_own)
   }
 }
 // mode B: an item with a callee that responded 500 failed at that callee's
@@ -407,7 +405,7 @@ __global__ void __launch_bounds__(kT) k_relmax(K k, const uint32_t *perm, unsign
     if (pp.nsteps < 2) continue;  // no step begins: nothing reads it
     // off = H, except in the first call step: pre + H relative to the start (the step begins at start + pre)
     const uint64_t h = k.pos[v].off - (p.kstep == 0 ? k.steps[pp.bk_first].add : 0ull);
-    atomicMax(rel + (uint64_t)par * k.aw + p.kstep, (unsigned long long)(h + k.eT[perm[j]]));
+    atomicMax(rel + (uint64_t)par * k.aw + p.kstep, (unsigned long long)(h + k.erec[perm[j]].y));
   }
 }
 
@@ -1226,8 +1224,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   if (rocprim::inclusive_scan(scan_tmp, b, k.cnt, k.tend, (size_t)n, rocprim::plus<uint64_t>(), s) != hipSuccess)
     return fail("item offset scan");
   uint64_t M = 0;
-  if (hipMemcpyAsync(&M, k.tend + (n - 1), 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      sync_s() != hipSuccess)
+  if (hipMemcpyAsync(&M, k.tend + (n - 1), 8, hipMemcpyDeviceToHost, s) != hipSuccess || sync_s() != hipSuccess)
     return fail("item count read-back");
   if (M >= 0xFFFFFFFFull) {
     err = "DES items: a batch of more than 2^32 - 1 executed invocations (use smaller batches)";
@@ -1270,7 +1267,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       96,                                                      // two arrival-range slots; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
-      M * 4, n * 4, M * 4, M * 8, M * 4, 8, M * 4,             // ihop troot; epos erec eT (1 spare); inverse
+      M * 4, n * 4, M * 16, 4, 4, 8, M * 4,                    // ihop troot; erec (3 spare); inverse
       (uint64_t)(pl.pos.size() + 1) * 4, (uint64_t)pl.pos.size() * 4, (uint64_t)pl.pos.size() * 4,  // poff qdst fdst
       tmp_bytes,
       M * 2, (n >> chunk_shift(n)) + 1, (n >> chunk_shift(n)) + 1,  // replicas; the two chunk-change maps
@@ -1320,9 +1317,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint64_t *d_row_hold = (uint64_t *)carve(parts[36]);
   k.ihop = (uint32_t *)carve(parts[37]);
   k.troot = (uint32_t *)carve(parts[38]);
-  k.epos = (uint32_t *)carve(parts[39]);
-  k.erec = (unsigned long long *)carve(parts[40]);
-  k.eT = (uint32_t *)carve(parts[41]);
+  k.erec = (uint4 *)carve(parts[39]);
+  (void)carve(parts[40]);
+  (void)carve(parts[41]);
   (void)carve(parts[42]);
   uint32_t *inv = (uint32_t *)carve(parts[43]);
   uint32_t *d_poff = (uint32_t *)carve(parts[44]);
@@ -1350,8 +1347,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       rc = fail("memset");
       break;
     }
-    hipLaunchKernelGGL(k_own, dim3(grid_for(M)), dim3(kT), 0, s, k);
-    hipLaunchKernelGGL(k_root500, dim3(grid_for(n)), dim3(kT), 0, s, k);
     // 2b. renumber position-major: ipos = the sorted keys, the rest gathered
     hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, ids);
     {
@@ -1362,7 +1357,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       }
     }
     hipLaunchKernelGGL(k_perm_inv, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
-    hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids, inv);
+    hipLaunchKernelGGL(k_own, dim3(grid_for(M)), dim3(kT), 0, s, k, (const uint32_t *)inv);
+    hipLaunchKernelGGL(k_root500, dim3(grid_for(n)), dim3(kT), 0, s, k);
+    hipLaunchKernelGGL(k_perm_apply, dim3(grid_for(M)), dim3(kT), 0, s, k, qids);
     if (pl.modeb) {
       if (hipMemsetAsync(ifst, 0xFF, M * 4, s) != hipSuccess) {
         rc = fail("memset");
