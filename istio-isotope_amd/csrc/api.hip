@@ -228,14 +228,16 @@ int build_device(isim_handler *h, int device, DevState &st) {
   // dynamic walks: the lane tree walk (kind 7) when the unrolled tree was
   // built and its LDS layout placed (program.cpp place_tree); else the wave walk
   bool tree = false;
-  if (!p.static_walk && !p.tree_nodes.empty() && !(h->params.flags & ISIM_FLAG_WAVE_WALK) &&
+  if (!p.static_walk && p.has_tree() && !(h->params.flags & ISIM_FLAG_WAVE_WALK) &&
       p.tree_layout.bytes <= lds_max) {
     tree = true;
     st.kind = 7;
     st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames,
                                   p.tree_frames > isim::kTreeRegFrames, p.tree_layout.nodes_lds != 0,
                                   (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
-                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"), p.tree_t64);
+                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"), p.tree_t64,
+                                  p.tree_wide);
+    if (!st.kernel) return fail(ISIM_EHIP, "no lane-tree-walk kernel for this tree");
     st.lds_bytes = p.tree_layout.bytes;
     st.lds_counters = 1;
     // the workgroup size with the most resident waves per CU (registers and
@@ -299,10 +301,12 @@ int build_device(isim_handler *h, int device, DevState &st) {
   st.per_cu = (uint32_t)per_cu;
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
   const void *src = is_stream(st.kind) ? (const void *)p.stream.data()
-                    : tree                ? (const void *)p.tree_nodes.data()
+                    : tree                ? (p.tree_wide ? (const void *)p.tree_nodes_w.data()
+                                                         : (const void *)p.tree_nodes.data())
                                           : (const void *)p.code.data();
   const size_t bytes = is_stream(st.kind) ? p.stream.size() * sizeof(isim::Node)
-                       : tree             ? p.tree_nodes.size() * sizeof(isim::TreeNode)
+                       : tree             ? (p.tree_wide ? p.tree_nodes_w.size() * sizeof(isim::TreeNodeW)
+                                                         : p.tree_nodes.size() * sizeof(isim::TreeNode))
                                           : p.code.size() * sizeof(isim::Ins);
   // the draw-stream kernel prefetches group g+1 unconditionally: two zero
   // groups (32 B each) of tail padding keep those reads inside the buffer
@@ -371,7 +375,9 @@ int build_device(isim_handler *h, int device, DevState &st) {
       // (launch_walk_one)
       st.spill_lanes = st.max_blocks * st.threads;
       st.spill_words = (size_t)(p.tree_frames - 8u) *
-                       (p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) * st.spill_lanes;
+                       ((p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) +
+                        (p.tree_wide ? isim::kTreeSpillWide : 0u)) *
+                       st.spill_lanes;
       HIPCHK(hipMalloc(&st.d_spill, st.spill_words * isim::kSpillAreas * sizeof(uint32_t)));
       for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
@@ -621,7 +627,7 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.sum_row = st->d_sum_row;
   kp.slot_tc = st->d_slot_tc;
   kp.spill_lanes = st->spill_lanes;
-  kp.n_pos = (uint32_t)h->prog.tree_nodes.size();
+  kp.n_pos = h->prog.tree_positions();
   kp.n_rows = (uint32_t)h->prog.row_svc.size();
   kp.n_dyn = (uint32_t)h->prog.tree_dyn.size();
   kp.dyn_words = h->prog.tree_dyn_words;
@@ -877,7 +883,8 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
       return fail(ISIM_EHIP, "DES item pool creation failed");
     if (!up(&st->d_des_ipos, d.item_pos.data(), d.item_pos.size() * sizeof(isim::DesItemPos)) ||
         !up((void **)&st->d_des_sround, d.step_round.data(), d.step_round.size() * 4) ||
-        !up(&st->d_des_nodes, p.tree_nodes.data(), p.tree_nodes.size() * sizeof(isim::TreeNode)) ||
+        !(p.tree_wide ? up(&st->d_des_nodes, p.tree_nodes_w.data(), p.tree_nodes_w.size() * sizeof(isim::TreeNodeW))
+                      : up(&st->d_des_nodes, p.tree_nodes.data(), p.tree_nodes.size() * sizeof(isim::TreeNode))) ||
         !up(&st->d_des_text, p.tree_ext.data(), p.tree_ext.size() * sizeof(isim::TreeExt)) ||
         !up(&st->d_des_tstep, p.tree_step.data(), p.tree_step.size() * sizeof(isim::TreeStep)))
       return fail(ISIM_EHIP, "DES plan upload failed");
@@ -957,7 +964,8 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.tree_frames = h->prog.tree_frames;
     L.tree_t64 = h->prog.tree_t64 ? 1u : 0u;
     L.tree_flags = h->prog.tree_flags;
-    L.n_nodes = (uint32_t)h->prog.tree_nodes.size();
+    L.n_nodes = h->prog.tree_positions();
+    L.tree_wide = h->prog.tree_wide ? 1u : 0u;
     L.workspace = d_workspace;
     L.d_stats = d_stats;
     L.d_table = d_des_table;

@@ -224,6 +224,7 @@ struct DesItemsLaunch {
   const void *d_nodes, *d_ext, *d_tstep;     // the lane tree walk's TreeNode/TreeExt/TreeStep
   uint32_t tree_frames, tree_flags, n_nodes;
   uint32_t tree_t64;  // the walk keeps u64 time (Program::tree_t64)
+  uint32_t tree_wide;  // a wide tree: 16-byte nodes (Program::tree_wide)
   void *workspace;
   uint64_t *d_stats, *d_table;
   isim_trace_rec *d_records;

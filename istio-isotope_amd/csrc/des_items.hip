@@ -137,8 +137,9 @@ struct K {
   uint32_t *troot;                 // per trace: its entry item (items are renumbered position-major)
   // the pre-walk's items in trace order, before the renumbering: one 16-byte
   // record each (one line touched per item, not one per field) — x: position
-  // | hop << 16, y: duration without contention (saturated), z: caller hop
-  // (kNone: the entry), w: trace | status << 31
+  // (k_own replaces it with the hop), y: duration without contention
+  // (saturated), z: caller hop (k_own: the caller's new index; kNone: the
+  // entry), w: trace | status << 31
   uint4 *erec;
   uint64_t *IA, *IS, *IF, *acc, *bk;
   const uint64_t *acc_prev;        // cyclic schedules: the previous pass's callee maxima
@@ -210,6 +211,14 @@ struct GNodes {
     return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
   }
 };
+// a wide tree's 16-byte nodes
+struct GNodesW {
+  const uint4 *__restrict__ p;
+  __device__ __forceinline__ tw::NodeW4 load(uint32_t i) const {
+    const uint4 v = p[i];
+    return tw::NodeW4{v.x, v.y, v.z, v.w};
+  }
+};
 struct CountSink {
   __device__ __forceinline__ void call(uint32_t) {}
   __device__ __forceinline__ void resp_leaf(uint32_t, bool) {}
@@ -223,7 +232,7 @@ struct EmitSink : CountSink {
   uint64_t base;
   uint32_t t;
   __device__ __forceinline__ void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
-    rec[base + hop] = uint4{p | hop << 16, 0u, caller == tw::kNoCaller ? kNone : caller, t | (own ? 0x80000000u : 0u)};
+    rec[base + hop] = uint4{p, 0u, caller == tw::kNoCaller ? kNone : caller, t | (own ? 0x80000000u : 0u)};
   }
   // (a lower bound is all k_relmax needs: u64 durations saturate at 2^32 - 1)
   // mode B: the response status (a failed step, or the own error) into bit
@@ -250,13 +259,13 @@ struct LNodes {
   }
 };
 
-template <int FR, bool SPILL, bool EMIT, bool T64, bool MB, class Nodes>
+template <int FR, bool SPILL, bool EMIT, bool T64, bool MB, bool W, class Nodes>
 __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *work, const Nodes &nodes) {
   // mode A: no error draws in the walk (DRAW = false): an invocation's own
   // error changes no skip, so the walks only need the skip residues; the
   // errors are drawn per item afterwards (k_own), fully parallel.  Mode B:
   // the errors decide which steps run, so the walk draws them (MODEB, DRAW)
-  tw::Lane<FR, MB, true, SPILL, MB, std::conditional_t<T64, uint64_t, uint32_t>> L;
+  tw::Lane<FR, MB, true, SPILL, MB, std::conditional_t<T64, uint64_t, uint32_t>, W> L;
   if constexpr (SPILL) {
     L.sp = k.spill + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
     L.sp_stride = gridDim.x * blockDim.x;
@@ -315,16 +324,19 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   }
 }
 
-template <int FR, bool SPILL, bool EMIT, bool LDSN, bool T64, bool MB>
+// (W: a wide tree — 16-byte nodes in global memory)
+template <int FR, bool SPILL, bool EMIT, bool LDSN, bool T64, bool MB, bool W = false>
 __global__ void __launch_bounds__(LDSN ? 1024 : kT) k_prewalk(K k, unsigned long long *work) {
-  if constexpr (LDSN) {
+  if constexpr (W) {
+    prewalk_body<FR, SPILL, EMIT, T64, MB, true>(k, work, GNodesW{(const uint4 *)k.nodes});
+  } else if constexpr (LDSN) {
     extern __shared__ unsigned long long s_nodes[];
     for (uint32_t i = threadIdx.x; i < k.n_nodes; i += blockDim.x) s_nodes[i] = k.nodes[i];
     __syncthreads();
-    prewalk_body<FR, SPILL, EMIT, T64, MB>(
+    prewalk_body<FR, SPILL, EMIT, T64, MB, false>(
         k, work, LNodes{(const __attribute__((address_space(3))) unsigned long long *)s_nodes});
   } else {
-    prewalk_body<FR, SPILL, EMIT, T64, MB>(k, work, GNodes{k.nodes});
+    prewalk_body<FR, SPILL, EMIT, T64, MB, false>(k, work, GNodes{k.nodes});
   }
 }
 
@@ -340,15 +352,15 @@ __global__ void __launch_bounds__(kT) k_own(K k, const uint32_t *inv) {
   for (uint64_t i = gid(); i < k.M; i += nthreads()) {
     const uint4 r = k.erec[i];
     const uint32_t t = r.w & 0x7FFFFFFFu;
-    const uint32_t hop = r.x >> 16;
-    const DesPos P = k.pos[r.x & 0xFFFFu];
+    const uint32_t hop = (uint32_t)(i - item_off(k, t));  // (a near read: t advances with i)
+    const DesPos P = k.pos[r.x];
     bool own = k.modeb ? (r.w >> 31) != 0 : (P.flags & kDesFlagAlways) != 0;
     if (!k.modeb && !own && P.thr) {
       uint32_t a = (uint32_t)(k.trace_begin + t), b = (uint32_t)((k.trace_begin + t) >> 32), c = hop >> 2, d = 0;
       tw::philox10(a, b, c, d, k.k0, k.k1);
       own = tw::word4(hop & 3u, a, b, c, d) < P.thr;
     }
-    k.erec[i] = uint4{r.x, r.y, r.z == kNone ? kNone : inv[i - hop + r.z], t | (own ? 0x80000000u : 0u)};
+    k.erec[i] = uint4{hop, r.y, r.z == kNone ? kNone : inv[i - hop + r.z], t | (own ? 0x80000000u : 0u)};
     if (own) atomicAdd(k.terr + t, 1u);
   }
 }
@@ -363,7 +375,7 @@ __global__ void __launch_bounds__(kT) k_root500(K k) {
 // position), read the per-item arrays nearly in sequence
 __global__ void __launch_bounds__(kT) k_perm_keys(K k, uint32_t *key, uint32_t *val) {
   for (uint64_t i = gid(); i < k.M; i += nthreads()) {
-    key[i] = k.erec[i].x & 0xFFFFu;
+    key[i] = k.erec[i].x;
     val[i] = (uint32_t)i;
   }
 }
@@ -376,7 +388,7 @@ __global__ void __launch_bounds__(kT) k_perm_apply(K k, const uint32_t *perm) {
     const uint4 r = k.erec[perm[j]];
     k.itr[j] = r.w & 0x7FFFFFFFu;
     k.iown[j] = (uint8_t)(r.w >> 31);
-    k.ihop[j] = r.x >> 16;
+    k.ihop[j] = r.x;  // the hop (k_own)
     k.ipar[j] = r.z;  // the caller's new index (k_own)
   }
 }
@@ -1173,7 +1185,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *spill_buf = nullptr;
   const uint64_t pw_threads = (uint64_t)kPrewalkBlocks * kT;
   if (spill) {
-    const uint64_t words = (uint64_t)(fr - 8 + 1) * (L.tree_t64 ? kTreeSpillWords64 : kTreeSpillWords) * pw_threads;
+    const uint64_t words = (uint64_t)(fr - 8 + 1) *
+                           ((L.tree_t64 ? kTreeSpillWords64 : kTreeSpillWords) + (L.tree_wide ? kTreeSpillWide : 0u)) *
+                           pw_threads;
     if (!pool_alloc(spill_mem, words * 4)) return fail("spill allocation");
     spill_buf = (uint32_t *)spill_mem.p;
   }
@@ -1182,7 +1196,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   // counts) when they fit in 96 KB; ISIM_DES_ITEMS_GLOBAL_NODES: always global
   k.n_nodes = L.n_nodes;
   const uint32_t lds_nodes = L.n_nodes * 8u;
-  const bool ldsn = lds_nodes <= 96u * 1024u && !std::getenv("ISIM_DES_ITEMS_GLOBAL_NODES");
+  const bool ldsn = !L.tree_wide && lds_nodes <= 96u * 1024u && !std::getenv("ISIM_DES_ITEMS_GLOBAL_NODES");
   auto launch = [&](auto kern, unsigned long long *w) {
     if (ldsn) {
       (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_nodes);
@@ -1197,7 +1211,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     constexpr int FRc = decltype(fr_c)::value;
     constexpr bool SP = decltype(spill_c)::value, T6 = decltype(t64_c)::value, MB = decltype(mb_c)::value;
     unsigned long long *w = work + (emit ? 1 : 0);
-    if (ldsn) {
+    if (L.tree_wide) {
+      if (emit) launch(k_prewalk<FRc, SP, true, false, T6, MB, true>, w);
+      else launch(k_prewalk<FRc, SP, false, false, T6, MB, true>, w);
+    } else if (ldsn) {
       if (emit) launch(k_prewalk<FRc, SP, true, true, T6, MB>, w);
       else launch(k_prewalk<FRc, SP, false, true, T6, MB>, w);
     } else {
@@ -1351,7 +1368,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, ids);
     {
       size_t tb0 = tmp_bytes;
-      if (rocprim::radix_sort_pairs(tmp, tb0, qk, k.ipos, ids, qids, (size_t)M, 0, 16, s) != hipSuccess) {
+      if (rocprim::radix_sort_pairs(tmp, tb0, qk, k.ipos, ids, qids, (size_t)M, 0,
+                                    bits_for(std::max<size_t>(1, pl.pos.size()) - 1), s) != hipSuccess) {
         rc = fail("position sort");
         break;
       }

@@ -120,12 +120,12 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
       stack.push_back(i);
       for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
     }
-  } else if (!p.static_walk && !p.tree_nodes.empty()) {
+  } else if (!p.static_walk && p.has_tree()) {
     out.items = true;
     std::vector<std::pair<uint32_t, uint32_t>> stack;  // (position, end of its subtree)
-    for (uint32_t i = 0; i < (uint32_t)p.tree_nodes.size(); ++i) {
+    for (uint32_t i = 0; i < p.tree_positions(); ++i) {
       while (!stack.empty() && i >= stack.back().second) stack.pop_back();
-      const TreeNode &nd = p.tree_nodes[i];
+      const TreeNodeW &nd = p.tree_nodes_w[i];
       src.push_back({i ? (uint32_t)nd.slot : kSlotRoot, stack.empty() ? kDesNoParent : stack.back().first,
                      p.tree_ext[i].thr, (nd.flags & TF_ERR_ALWAYS) != 0});
       stack.push_back({i, i + std::max<uint32_t>(1, nd.size)});

@@ -103,6 +103,19 @@ struct TreeNode {
   uint16_t slot;   // stats slot of the call site
 };
 static_assert(sizeof(TreeNode) == 8, "TreeNode must be 8 bytes");
+// WIDE trees (round 5): more than 65,535 potential invocations, call sites
+// or rows, or per-slot counters that do not fit in LDS — 32-bit sizes and
+// slots (16 B per position, read from global memory), every statistic by
+// global atomics (tree.hip WideSink), the row index whole in TreeExt.row
+struct TreeNodeW {
+  uint32_t size;   // positions in the subtree (itself included)
+  uint32_t k;      // index of the call command in the caller's script
+  uint8_t prob;    // 1..99: draw to skip; 0: always called
+  uint8_t flags;   // TF_*
+  uint16_t pad;
+  uint32_t slot;   // stats slot of the call site
+};
+static_assert(sizeof(TreeNodeW) == 16, "TreeNodeW must be 16 bytes");
 struct TreeExt {
   uint32_t H;      // hop cost of the call
   uint32_t tc;     // leaf callee: its latency; else the time after its last call step (mode A: + the
@@ -143,6 +156,7 @@ constexpr uint32_t kTreeRegFrames = 16;          // deepest register stack; deep
 constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations below the current one
 constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
 constexpr uint32_t kTreeSpillWords64 = 7;        // ... with u64 time (acc and step max take two words each)
+constexpr uint32_t kTreeSpillWide = 2;           // ... + position end and hop id of a wide tree's frame
 constexpr uint32_t kSpillAreas = 4;              // spill areas per (handler, device): launches in flight
 // LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
 // workgroups per CU, and the whole CU.
@@ -223,19 +237,19 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters);
 // kind 7 variant (tree.hip, compiled once per mode and concurrency):
 // register-stack depth (4, 6, 8, 12, 16; `spill`: 8 registers + the rest in
 // global memory), nodes in LDS or global, the error-block cache.
-void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
-void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
-void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
-void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64);
+void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
+void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
+void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
+void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
 // occ2: the LDS layout fits two workgroups per CU (kernels built for 80 VGPRs);
-// t64: u64 time (Program::tree_t64)
+// t64: u64 time (Program::tree_t64); wide: a wide tree (Program::tree_wide)
 inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw, bool occ2,
-                         bool t64) {
+                         bool t64, bool wide = false) {
   if (modeb)
-    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2, t64)
-                : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2, t64);
-  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64)
-              : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64);
+    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2, t64, wide)
+                : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2, t64, wide);
+  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64, wide)
+              : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide);
 }
 void *stream_calls_kernel();
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

@@ -90,7 +90,7 @@ static uint32_t row_lds_bytes(uint32_t bw, bool compact) {
 
 static bool place_tree(Program &out, const std::vector<double> &row_heat, const std::vector<uint32_t> &row_bw,
                        const std::vector<char> &row_nonleaf) {
-  const uint32_t P = (uint32_t)out.tree_nodes.size(), S = (uint32_t)out.n_slots;
+  const uint32_t P = (uint32_t)out.tree_nodes_w.size(), S = (uint32_t)out.n_slots;
   const uint32_t R = (uint32_t)out.row_svc.size();
   const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;  // + the duration-bucket LUT
   // per-slot counters: guarded 16-bit pairs (4 B per slot; ISIM_TREE_CNT32 set: two u32, A/B measurements)
@@ -181,25 +181,34 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
 }
 
 // The unrolled tree of potential invocations for the lane tree walk
-// (kernel_abi.h TreeNode/TreeExt, tree_walk.h); leaves out.tree_nodes empty
-// with the reason in out.tree_why when the walk does not fit it.
+// (kernel_abi.h TreeNode/TreeExt, tree_walk.h); leaves the trees empty with
+// the reason in out.tree_why when the walk does not fit it.  A tree past the
+// 8-byte nodes' 16-bit fields (positions, call sites, rows) or whose per-slot
+// counters do not fit in LDS is built WIDE (kernel_abi.h TreeNodeW;
+// ISIM_TREE_FORCE_WIDE set: always, for tests and A/B measurements).
+constexpr uint32_t kTreeMaxWidePositions = 1u << 24;
 static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Site> &sites,
                        const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
                        const std::vector<uint64_t> &tmin, const std::vector<char> &leaf, bool modeb) {
   out.tree_nodes.clear();
+  out.tree_nodes_w.clear();
   out.tree_ext.clear();
   out.tree_step.clear();
+  out.tree_wide = false;
   auto give_up = [&](const char *why) {
     out.tree_nodes.clear();
+    out.tree_nodes_w.clear();
     out.tree_ext.clear();
     out.tree_step.clear();
+    out.tree_wide = false;
     out.tree_why = why;
   };
   // u64 time when the latency bound reaches 2^32 ns; each position's own
   // figures (hop cost, callee time, step facts, leaf latency) stay 32-bit
   out.tree_t64 = out.max_latency >= (1ull << 32);
   constexpr uint64_t k32 = 1ull << 32;
-  if (out.n_slots > (int32_t)kTreeMaxPositions) return give_up("more than 65535 call sites");
+  bool wide = std::getenv("ISIM_TREE_FORCE_WIDE") != nullptr || out.n_slots > (int32_t)kTreeMaxPositions;
+  if ((uint32_t)out.n_slots >= kSlotRoot) return give_up("more than 2^24 call sites");
   const int32_t n = (int32_t)g.services.size();
   std::vector<ScriptTimes> shape(n);
   std::vector<char> shaped(n, 0);
@@ -211,7 +220,8 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     return shape[s];
   };
   const uint32_t R = (uint32_t)out.row_svc.size();
-  if (R > kTreeGlobalStatic) return give_up("more than 65532 reachable services");
+  if (R > kTreeGlobalStatic) wide = true;
+  if (R >= kTreeLeafSlot) return give_up("more than 2^23 reachable services");
   // per row: bucket range of the durations (a table when it spans several buckets), non-leaf
   std::vector<uint32_t> row_bw(R, 0);
   std::vector<char> row_nonleaf(R, 0);
@@ -257,14 +267,14 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   };
   std::vector<Frame> stack;
   const int32_t e = out.entry;
-  TreeNode root{};
+  TreeNodeW root{};
   root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e) | (probk0[e] ? TF_PROBK0 : 0));
   if (root.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
   TreeExt rx{};
   if (own_time(e) >= k32) return give_up("a script whose time outside its call steps is >= 2^32 ns");
   rx.tc = (uint32_t)own_time(e);
   rx.thr = thr[e] >= (1ull << 32) ? 0u : (uint32_t)thr[e];
-  out.tree_nodes.push_back(root);
+  out.tree_nodes_w.push_back(root);
   out.tree_ext.push_back(rx);
   out.tree_step.push_back(TreeStep{});
   pos_callee.push_back(e);
@@ -277,10 +287,10 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       const Site &st = sites[svc_sites[top.svc][j]];
       const CallShape &cs = shape_of(top.svc).calls[j];
       const int32_t c = st.callee;
-      if (out.tree_nodes.size() >= kTreeMaxPositions) return give_up("more than 65535 potential invocations");
-      if (st.k > 0xFFFFu) return give_up("a script with more than 65536 calls");
-      TreeNode nd{};
-      nd.k = (uint16_t)st.k;
+      if (out.tree_nodes_w.size() >= kTreeMaxPositions) wide = true;
+      if (out.tree_nodes_w.size() >= kTreeMaxWidePositions) return give_up("more than 2^24 potential invocations");
+      TreeNodeW nd{};
+      nd.k = st.k;
       nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
       const bool xpre = modeb && cs.step_first && cs.pre != 0;
       const bool xcmax = cs.step_first && cs.conc && cs.cmax0 != 0;
@@ -291,7 +301,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       if (nd.flags & TF_CONC) out.tree_flags |= kTreeAnyConc;
       if (nd.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
       const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
-      nd.slot = (uint16_t)slot;
+      nd.slot = (uint32_t)slot;
       through[slot] += 1;
       const uint32_t row = (uint32_t)out.svc_row[c];
       if (row_bw[row]) row_through[row] += 1;
@@ -303,8 +313,8 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       x.H = (uint32_t)st.hop;
       x.tc = (uint32_t)own_time(c);
       x.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
-      const uint32_t pos = (uint32_t)out.tree_nodes.size();
-      out.tree_nodes.push_back(nd);
+      const uint32_t pos = (uint32_t)out.tree_nodes_w.size();
+      out.tree_nodes_w.push_back(nd);
       out.tree_ext.push_back(x);
       out.tree_step.push_back(TreeStep{(uint32_t)cs.pre, (uint32_t)cs.cmax0});
       pos_callee.push_back(c);
@@ -313,24 +323,47 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
         max_open = std::max<uint32_t>(max_open, (uint32_t)stack.size());
       }
     } else {
-      out.tree_nodes[top.pos].size = (uint16_t)(out.tree_nodes.size() - top.pos);
+      out.tree_nodes_w[top.pos].size = (uint32_t)(out.tree_nodes_w.size() - top.pos);
       stack.pop_back();
     }
   }
-  if (out.tree_nodes.size() == 1) out.tree_nodes[0].size = 1;
-  for (size_t i = 0; i < out.tree_nodes.size(); ++i)
-    if (out.tree_nodes[i].size == 0) out.tree_nodes[i].size = 1;  // leaf positions
+  if (out.tree_nodes_w.size() == 1) out.tree_nodes_w[0].size = 1;
+  for (size_t i = 0; i < out.tree_nodes_w.size(); ++i)
+    if (out.tree_nodes_w[i].size == 0) out.tree_nodes_w[i].size = 1;  // leaf positions
   out.tree_frames = max_open ? max_open - 1 : 0;
   if (out.tree_frames > kTreeMaxFrames) return give_up("more than 65 nested calling invocations");
-  if (!place_tree(out, row_heat, row_bw, row_nonleaf)) return give_up("the per-slot counters do not fit in LDS");
+  if (!wide) {  // the 8-byte device nodes and the LDS layout
+    out.tree_nodes.resize(out.tree_nodes_w.size());
+    for (size_t i = 0; i < out.tree_nodes_w.size(); ++i) {
+      const TreeNodeW &w = out.tree_nodes_w[i];
+      out.tree_nodes[i] = TreeNode{(uint16_t)w.size, (uint16_t)w.k, w.prob, w.flags, (uint16_t)w.slot};
+    }
+    if (!place_tree(out, row_heat, row_bw, row_nonleaf)) {  // the per-slot counters do not fit in LDS
+      wide = true;
+      out.tree_nodes.clear();
+    }
+  }
+  out.tree_wide = wide;
+  if (wide) {  // no LDS tables: the accumulators, histograms and bucket LUT only
+    TreeLayout &L = out.tree_layout;
+    L = TreeLayout{};
+    const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;
+    L.off_cnt = L.off_sums = L.off_dyn = L.off_nodes = L.bytes = head;
+    L.wg_per_cu = 1;
+    out.sum_row.clear();
+    out.tree_dyn.clear();
+    out.tree_dyn_words = 0;
+    out.tree_row_place.assign(R, kTreeGlobalDyn);
+    out.tree_row_index.assign(R, 0);
+  }
   // the row words of the non-leaf callees (the entry's row is filled from the histograms)
-  for (size_t i = 1; i < out.tree_nodes.size(); ++i) {
+  for (size_t i = 1; i < out.tree_nodes_w.size(); ++i) {
     const int32_t c = pos_callee[i];
     if (leaf[c]) continue;
     const uint32_t r = (uint32_t)out.svc_row[c];
-    out.tree_ext[i].row = out.tree_row_index[r] | (out.tree_row_place[r] << 16);
+    out.tree_ext[i].row = wide ? r : out.tree_row_index[r] | (out.tree_row_place[r] << 16);
   }
-  out.tree_ext[0].row = kTreeStaticRow << 16;
+  out.tree_ext[0].row = wide ? 0u : kTreeStaticRow << 16;
   // per slot: the callee's row, its static bucket (kTreeDynBucket when it varies), leaf flag and latency
   out.slot_tbkt.assign(out.n_slots, 0);
   out.slot_tc.assign(out.n_slots, 0);
@@ -342,10 +375,12 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     if (leaf[s] && out.svc_time[s] >= k32) return give_up("a leaf latency >= 2^32 ns");
     out.slot_tc[sl] = leaf[s] ? (uint32_t)out.svc_time[s] : 0u;
   }
-  out.tree_mult = 1;
-  for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
-  for (uint32_t r = 0; r < R; ++r)
-    if (out.tree_row_place[r] < kTreeGlobalStatic) out.tree_mult = std::max(out.tree_mult, row_through[r]);
+  out.tree_mult = 1;  // (a wide tree's statistics are u64 global atomics: nothing to guard)
+  if (!wide) {
+    for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
+    for (uint32_t r = 0; r < R; ++r)
+      if (out.tree_row_place[r] < kTreeGlobalStatic) out.tree_mult = std::max(out.tree_mult, row_through[r]);
+  }
   out.tree_why.clear();
 }
 

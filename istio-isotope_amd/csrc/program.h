@@ -47,7 +47,11 @@ struct Program {
   uint32_t root_dur = 0;            // the entry: row 0 | bucket << 24 when the entry is a leaf
   // lane tree walk (kernel kind 7, dynamic walks): the unrolled tree of potential
   // invocations when it fits (tree_nodes empty otherwise; tree_why says why)
+  // (tree_nodes_w: every tree in the wide format — the host-side view the DES
+  // plan reads; tree_nodes: the 8-byte device nodes, empty for a wide tree)
   std::vector<TreeNode> tree_nodes;
+  std::vector<TreeNodeW> tree_nodes_w;
+  bool tree_wide = false;           // a wide tree (kernel_abi.h TreeNodeW): 32-bit fields, global statistics
   std::vector<TreeExt> tree_ext;
   std::vector<TreeStep> tree_step;
   std::vector<uint32_t> slot_tbkt;  // per slot: callee row | kTreeLeafSlot | static duration bucket << 24
@@ -64,6 +68,8 @@ struct Program {
                                     // counter overflow guard)
   uint32_t tree_flags = 0;          // kTreeAnyProb | kTreeAnyDraw | kTreeAnyConc
   std::string tree_why;
+  bool has_tree() const { return !tree_nodes_w.empty(); }
+  uint32_t tree_positions() const { return (uint32_t)tree_nodes_w.size(); }
 };
 
 // Bucket of an invocation duration on the service_request_duration_seconds

@@ -93,6 +93,50 @@ struct GlobalNodes {
     return tw::NodeW{(uint32_t)v, (uint32_t)(v >> 32)};
   }
 };
+// a wide tree's 16-byte nodes (global_load_dwordx4)
+struct GlobalNodesW {
+  const uint4 *__restrict__ p;
+  __device__ __forceinline__ tw::NodeW4 load(uint32_t i) const {
+    const uint4 v = p[i];
+    return tw::NodeW4{v.x, v.y, v.z, v.w};
+  }
+};
+
+// A wide tree's statistics (Program::tree_wide: call sites, rows or
+// positions past 16 bits, or counters that do not fit in LDS): every event
+// by a global u64 atomic — calls and callee 500s per slot, each response's
+// duration bucket and sum in its row (a leaf callee's from its slot: static
+// bucket and latency).  No LDS tables, no flush beyond the histograms.
+__device__ __forceinline__ uint32_t wide_row(uint32_t w) {
+  uint32_t r = w & (kTreeLeafSlot - 1u);
+  asm volatile("" : "+v"(r));  // (as dur_row: keep the mask out of the address arithmetic)
+  return r;
+}
+struct WideSink {
+  const uint8_t *lut;
+  uint64_t *svc_tab;
+  uint32_t n_slots;
+  unsigned long long *sites;
+  const uint32_t *slot_tbkt, *slot_tc;
+  __device__ __forceinline__ void call(uint32_t slot) { atomicAdd(sites + slot, 1ull); }
+  __device__ __forceinline__ void resp_leaf(uint32_t slot, bool st) {
+    if (st) atomicAdd(sites + n_slots + slot, 1ull);
+    if (!svc_tab) return;
+    const uint32_t w = slot_tbkt[slot];
+    unsigned long long *row = (unsigned long long *)(svc_tab + (uint64_t)wide_row(w) * ISIM_SVC_DUR_WORDS);
+    atomicAdd(row + (st ? ISIM_N_PROM : 0u) + (w >> 24), 1ull);
+    const uint32_t tc = slot_tc[slot];
+    if (tc) atomicAdd(row + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)tc);
+  }
+  template <typename TT>
+  __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, TT T, bool st) {
+    if (st) atomicAdd(sites + n_slots + slot, 1ull);
+    if (!svc_tab) return;
+    unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)wide_row(roww) * ISIM_SVC_DUR_WORDS);
+    atomicAdd(r + (st ? ISIM_N_PROM : 0u) + lut_bucket(lut, T), 1ull);
+    atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
+  }
+};
 
 struct TreeSink {
   uint32_t *cnt;                // LDS: per slot calls | 500s << 16 (cnt16), else [2][n_slots] u32
@@ -236,7 +280,9 @@ struct TreeSink {
 // 768-thread workgroups per CU) when the LDS layout fits half the CU, else 4
 // (one 1024-thread workgroup per CU: up to 128 VGPRs, no spills).
 // T64: u64 time (a latency bound of 2^32 ns or more; tree_walk.h Lane TT).
-template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE, bool T64 = false>
+// WIDE: a wide tree (16-byte nodes in global memory, WideSink).
+template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE, bool T64 = false,
+          bool WIDE = false>
 __global__ void __launch_bounds__(kWgThreads, WPE)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
@@ -274,16 +320,24 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     dyn[d.off] = d.b_lo | (d.width << 8);
   }
   __syncthreads();
-  TreeSink sink{c.cnt, lut, sum200, dyn, lay.compact != 0, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
-                reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
+  auto sink = [&]() {
+    if constexpr (WIDE)
+      return WideSink{lut, c.svc_tab, S, reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt,
+                      kp.slot_tc};
+    else
+      return TreeSink{c.cnt, lut, sum200, dyn, lay.compact != 0, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
+                      reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
+  }();
 #ifdef ISIM_TREE_DEBUG
   sink.n_pos = P;
   sink.n_rows = kp.n_rows;
   sink.dbg = reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_DES_RETRY);
 #endif
-  using Nodes = std::conditional_t<NLDS, LdsNodes, GlobalNodes>;
+  using Nodes = std::conditional_t<WIDE, GlobalNodesW, std::conditional_t<NLDS, LdsNodes, GlobalNodes>>;
   Nodes nodes;
-  if constexpr (NLDS)
+  if constexpr (WIDE)
+    nodes.p = reinterpret_cast<const uint4 *>(gnodes);
+  else if constexpr (NLDS)
     nodes.p = (const __attribute__((address_space(3))) unsigned long long *)(lds + lay.off_nodes);
   else
     nodes.p = reinterpret_cast<const unsigned long long *>(gnodes);
@@ -313,7 +367,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   bool dry = b >= n_batches;
   uint64_t nxt = dry ? 0 : b * 64, lim = dry ? 0 : (b * 64 + 64 < n ? b * 64 + 64 : n);
   const uint64_t lt = ((uint64_t)1 << lane_id()) - 1;  // lanes below this one
-  tw::Lane<FRAMES, MODEB, CONC, SPILL, DRAW, TT> L;
+  tw::Lane<FRAMES, MODEB, CONC, SPILL, DRAW, TT, WIDE> L;
   if constexpr (SPILL) {
     L.sp = kp.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     L.sp_stride = kp.spill_lanes;
@@ -431,6 +485,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
   // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
+  if constexpr (!WIDE) {  // (a wide tree counted every event in HBM)
   auto calls_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] & 0xFFFFu) : c.cnt[s]; };
   auto errs_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] >> 16) : c.cnt[S + s]; };
   for (uint32_t i = threadIdx.x; i < 2u * S; i += blockDim.x) {
@@ -463,6 +518,10 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
           lay.compact ? (unsigned long long)((uint32_t *)sum200)[r] : ((unsigned long long *)sum200)[r];
       if (v) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
     }
+  }
+  }  // !WIDE
+  if (c.svc_tab) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
     // the varying LDS rows' bucket tables: one thread per (row, word)
     for (uint32_t i = threadIdx.x; i < kp.dyn_words; i += blockDim.x) {
       const uint32_t v = dyn[i];
@@ -486,6 +545,9 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
         atomicAdd(row + code * ISIM_N_PROM + b, (unsigned long long)v);
       }
     }
+  }
+  if (c.svc_tab) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
     // the entry's row: its invocations are the traces (end-to-end histogram and sums)
     unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;
     for (uint32_t i = threadIdx.x; i < 2u * ISIM_N_PROM; i += blockDim.x)
@@ -525,9 +587,18 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
 #define TREE_WPE2 6
 #endif
 template <bool NLDS, bool DRAW>
-static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64) {
+static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wide) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
+  if (wide) {  // a wide tree: nodes in global memory; 16 register frames, or 8 + the spill; 4 waves per SIMD
+    if constexpr (!NLDS) {
+      if (t64) return spill ? (void *)&isim_tree<M, 8, true, false, C, DRAW, 4, true, true>
+                            : (void *)&isim_tree<M, 16, false, false, C, DRAW, 4, true, true>;
+      return spill ? (void *)&isim_tree<M, 8, true, false, C, DRAW, 4, false, true>
+                   : (void *)&isim_tree<M, 16, false, false, C, DRAW, 4, false, true>;
+    }
+    return nullptr;
+  }
   if (t64) {  // u64 time: register stacks of 8 or 16 frames, or 8 + the spill; 4 waves per SIMD
     if (spill) return (void *)&isim_tree<M, 8, true, NLDS, C, DRAW, 4, true>;
     if (frames <= 8) return (void *)&isim_tree<M, 8, false, NLDS, C, DRAW, 4, true>;
@@ -549,10 +620,12 @@ static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64) {
 #define TREE_CAT2(a, b, c) a##b##c
 #define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
 void *TREE_CAT(tree_kernel_m, TREE_MODEB, TREE_CAT(c, TREE_CONC, ))(uint32_t frames, bool spill, bool nodes_lds,
-                                                                      bool draw, bool occ2, bool t64) {
-  if (nodes_lds)
-    return draw ? tree_pick<true, true>(frames, spill, occ2, t64) : tree_pick<true, false>(frames, spill, occ2, t64);
-  return draw ? tree_pick<false, true>(frames, spill, occ2, t64) : tree_pick<false, false>(frames, spill, occ2, t64);
+                                                                      bool draw, bool occ2, bool t64, bool wide) {
+  if (nodes_lds && !wide)
+    return draw ? tree_pick<true, true>(frames, spill, occ2, t64, false)
+                : tree_pick<true, false>(frames, spill, occ2, t64, false);
+  return draw ? tree_pick<false, true>(frames, spill, occ2, t64, wide)
+              : tree_pick<false, false>(frames, spill, occ2, t64, wide);
 }
 
 }  // namespace isim

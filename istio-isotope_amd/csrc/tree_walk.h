@@ -99,6 +99,24 @@ struct CpuNodes {
     return n;
   }
 };
+// A wide tree's TreeNodeW (kernel_abi.h): the same accessors on 32-bit fields
+struct NodeW4 {
+  uint32_t sz, kk, pf, sl;  // size, k, prob | flags << 8, slot
+  ISIM_TW uint32_t size() const { return sz; }
+  ISIM_TW uint32_t k() const { return kk; }
+  ISIM_TW uint32_t prob() const { return pf & 0xFFu; }
+  ISIM_TW uint32_t flags() const { return (pf >> 8) & 0xFFu; }
+  ISIM_TW uint32_t slot() const { return sl; }
+};
+static_assert(sizeof(TreeNodeW) == sizeof(NodeW4), "TreeNodeW is four words");
+struct CpuNodesW {
+  const TreeNodeW *p;
+  ISIM_TW NodeW4 load(uint32_t i) const {
+    NodeW4 n;
+    __builtin_memcpy(&n, p + i, sizeof n);
+    return n;
+  }
+};
 ISIM_TW TreeExt load_ext(const TreeExt *ext, uint32_t p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint4 v = reinterpret_cast<const uint4 *>(ext)[p];
@@ -162,27 +180,41 @@ struct has_exec<S, decltype((void)&S::exec)> {
 // TT: the time type — uint32_t when the walk's latency bound is below 2^32
 // ns, else uint64_t (round 5: a sequential 10k-service tree's bound is ~30 s;
 // every position's own H, tc and step facts still fit 32 bits, program.cpp)
-template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true, typename TT = uint32_t>
+// W: a wide tree (kernel_abi.h TreeNodeW): positions and hop ids take 32 bits,
+// so a frame keeps its position and end, and its hop and flags, in separate
+// words (two more registers per frame; the nodes come as NodeW4)
+template <int FRAMES, bool MODEB, bool CONC = true, bool SPILL = false, bool DRAW = true, typename TT = uint32_t,
+          bool W = false>
 struct Lane {
-  // u32 words of a spilled frame: pos|end, hop|flags, residues, time, step max
-  static constexpr uint32_t kSW = sizeof(TT) == 8 ? kTreeSpillWords64 : kTreeSpillWords;
+  // u32 words of a spilled frame: pos|end, hop|flags, residues, time, step max (+ end, hop when wide)
+  static constexpr uint32_t kSW0 = sizeof(TT) == 8 ? kTreeSpillWords64 : kTreeSpillWords;
+  static constexpr uint32_t kSW = kSW0 + (W ? kTreeSpillWide : 0u);
+  static constexpr uint32_t kWF = W && FRAMES > 0 ? FRAMES : 1;
   uint32_t t_lo = 0, t_hi = 0;
   uint32_t p = 0, d = 0, end = 0;
   uint32_t he = 0;  // executed invocations (hop ids handed out) | invocations that responded 500 << 16
+  uint32_t he_err = 0;  // W: the 500s (he counts the hops alone)
   bool done = true;
   TT lat = 0;
   bool root500 = false;
   // current invocation: f_hf = hop | fl << 16 (fl: FL_* | call block of f_res << KB_SHIFT), packed
-  // as its frame is (one register fewer; HF() shifts a flag into place)
-  uint32_t f_pos = 0, f_hf = 0, f_res = 0;
+  // as its frame is (one register fewer; HF() shifts a flag into place); W: f_hf = fl, hop in f_hop
+  uint32_t f_pos = 0, f_hf = 0, f_res = 0, f_hop = 0;
   TT f_acc = 0, f_cmax = 0;
-  static constexpr uint32_t HF(uint32_t fl) { return fl << 16; }
-  ISIM_TW uint32_t hops() const { return he & 0xFFFFu; }
-  ISIM_TW uint32_t errs() const { return he >> 16; }
-  ISIM_TW uint32_t f_kb() const { return (f_hf >> (16 + KB_SHIFT)) & KB_NONE; }
+  static constexpr uint32_t kHFS = W ? 0u : 16u;
+  static constexpr uint32_t HF(uint32_t fl) { return fl << kHFS; }
+  ISIM_TW uint32_t hops() const { return W ? he : he & 0xFFFFu; }
+  ISIM_TW uint32_t errs() const { return W ? he_err : he >> 16; }
+  ISIM_TW void add_err(bool e) {
+    if (W) he_err += e ? 1u : 0u;
+    else he += e ? 0x10000u : 0u;
+  }
+  ISIM_TW uint32_t cur_hop() const { return W ? f_hop : f_hf & 0xFFFFu; }
+  ISIM_TW uint32_t f_kb() const { return (f_hf >> (kHFS + KB_SHIFT)) & KB_NONE; }
   ISIM_TW void set_kb(uint32_t kb) { f_hf = (f_hf & ~HF(KB_NONE << KB_SHIFT)) | HF(kb << KB_SHIFT); }
-  // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time
+  // calling invocations below it: pos | end << 16, hop | fl << 16, residues, time (W: + end, hop)
   uint32_t s_pe[FRAMES > 0 ? FRAMES : 1], s_hf[FRAMES > 0 ? FRAMES : 1], s_res[FRAMES > 0 ? FRAMES : 1];
+  uint32_t s_end[kWF], s_hop[kWF];
   TT s_acc[FRAMES > 0 ? FRAMES : 1], s_cmax[CONC && FRAMES > 0 ? FRAMES : 1];
   uint32_t *sp = nullptr;  // SPILL: this lane's column of the spill area
   uint32_t sp_stride = 1;
@@ -222,6 +254,7 @@ struct Lane {
     t_hi = (uint32_t)(trace >> 32);
     done = false;
     he = 0;
+    he_err = 0;
     d = 0;
     ek_blk = 0xFFFFFFFFu;  // the error block belongs to the previous trace of the lane
     p = 0;
@@ -240,7 +273,7 @@ struct Lane {
   }
 
   ISIM_TW void push() {
-    const uint32_t pe = f_pos | (end << 16), hf = f_hf;
+    const uint32_t pe = W ? f_pos : f_pos | (end << 16), hf = f_hf;
     if (SPILL && d >= (uint32_t)FRAMES) {
       uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
       q[0] = pe;
@@ -252,6 +285,10 @@ struct Lane {
         q[5 * sp_stride] = (uint32_t)((uint64_t)f_acc >> 32);
         q[6 * sp_stride] = (uint32_t)((uint64_t)f_cmax >> 32);
       }
+      if constexpr (W) {
+        q[kSW0 * sp_stride] = end;
+        q[(kSW0 + 1) * sp_stride] = f_hop;
+      }
     } else {
 TW_PRAGMA_UNROLL
       for (int i = 0; i < FRAMES; ++i) {
@@ -261,6 +298,10 @@ TW_PRAGMA_UNROLL
         s_res[i] = m ? f_res : s_res[i];
         s_acc[i] = m ? f_acc : s_acc[i];
         if (CONC) s_cmax[i] = m ? f_cmax : s_cmax[i];
+        if (W) {
+          s_end[i] = m ? end : s_end[i];
+          s_hop[i] = m ? f_hop : s_hop[i];
+        }
       }
     }
     ++d;
@@ -268,7 +309,7 @@ TW_PRAGMA_UNROLL
 
   ISIM_TW void pop() {
     --d;
-    uint32_t pe = 0, hf = 0, r = 0;
+    uint32_t pe = 0, hf = 0, r = 0, en = 0, hp = 0;
     TT a = 0, c = 0;
     if (SPILL && d >= (uint32_t)FRAMES) {
       const uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
@@ -281,6 +322,10 @@ TW_PRAGMA_UNROLL
         a |= (TT)((uint64_t)q[5 * sp_stride] << 32);
         c |= (TT)((uint64_t)q[6 * sp_stride] << 32);
       }
+      if constexpr (W) {
+        en = q[kSW0 * sp_stride];
+        hp = q[(kSW0 + 1) * sp_stride];
+      }
     } else {
 TW_PRAGMA_UNROLL
       for (int i = 0; i < FRAMES; ++i) {
@@ -290,10 +335,20 @@ TW_PRAGMA_UNROLL
         r = m ? s_res[i] : r;
         a = m ? s_acc[i] : a;
         if (CONC) c = m ? s_cmax[i] : c;
+        if (W) {
+          en = m ? s_end[i] : en;
+          hp = m ? s_hop[i] : hp;
+        }
       }
     }
-    f_pos = pe & 0xFFFFu;
-    end = pe >> 16;
+    if constexpr (W) {
+      f_pos = pe;
+      end = en;
+      f_hop = hp;
+    } else {
+      f_pos = pe & 0xFFFFu;
+      end = pe >> 16;
+    }
     f_hf = hf;
     f_res = r;
     f_acc = a;
@@ -305,7 +360,8 @@ TW_PRAGMA_UNROLL
   // only, TF_XPRE: mode A folds it into the caller's tc —, a concurrent step
   // starts) on copies of the frame's time and flags; returns false when the
   // script has failed (mode B: it runs no further step).
-  ISIM_TW bool step_begin(const NodeW &n, const TreeStep *stp, TT &acc, uint32_t &fl, TT &cm) const {
+  template <class N>
+  ISIM_TW bool step_begin(const N &n, const TreeStep *stp, TT &acc, uint32_t &fl, TT &cm) const {
     if (!(n.flags() & TF_STEP)) return true;
     if (CONC && (fl & HF(FL_INCONC))) {
       acc += cm;
@@ -325,7 +381,8 @@ TW_PRAGMA_UNROLL
   }
 
   // the skip draw of call n (its block's residues are in f_res)
-  ISIM_TW bool skipped(const NodeW &n) const {
+  template <class N>
+  ISIM_TW bool skipped(const N &n) const {
     return ((f_res >> (7u * (n.k() & 3u))) & 0x7Fu) < 100u - n.prob();
   }
 
@@ -342,7 +399,7 @@ TW_PRAGMA_UNROLL
     const bool failed = MODEB && (fl & HF(FL_FAILED));
     if (!failed) T += x.tc;
     const bool st = failed || (fl & HF(FL_OWN));
-    he += st ? 0x10000u : 0u;
+    add_err(st);
     if (f_pos == 0) {
       done = true;
       lat = T;
@@ -350,7 +407,7 @@ TW_PRAGMA_UNROLL
       return false;
     }
     sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
-    if constexpr (has_exec<Sink>::value) sink.dur(f_hf & 0xFFFFu, T, st);
+    if constexpr (has_exec<Sink>::value) sink.dur(cur_hop(), T, st);
     const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
     pop();
@@ -362,7 +419,7 @@ TW_PRAGMA_UNROLL
   template <class Nodes, class Sink>
   ISIM_TW void process(const Nodes &nodes, const TreeExt *ext, const TreeStep *stp, Sink &sink, uint32_t k0,
                        uint32_t k1) {
-    const NodeW n = nodes.load(p);
+    const auto n = nodes.load(p);
     if (!step_begin(n, stp, f_acc, f_hf, f_cmax)) {  // mode B: the script stops, close at the subtree's end
       p = end;
       return;
@@ -370,7 +427,7 @@ TW_PRAGMA_UNROLL
     if (n.prob()) {  // shouldSkipRequest: word (k & 3) of Philox((t, caller hop, 1 + k/4, 0)) % 100 < 100 - p
       const uint32_t kb = (uint32_t)n.k() >> 2;
       if (f_kb() != kb) {  // a call block past the first four calls
-        f_res = residues(f_hf & 0xFFFFu, kb, k0, k1);
+        f_res = residues(cur_hop(), kb, k0, k1);
         set_kb(kb);
       }
       if (skipped(n)) {
@@ -378,7 +435,7 @@ TW_PRAGMA_UNROLL
         return;
       }
     }
-    const uint32_t hop = he & 0xFFFFu;
+    const uint32_t hop = hops();
     he += 1u;
     const uint32_t fl = n.flags();
     const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
@@ -386,8 +443,8 @@ TW_PRAGMA_UNROLL
     if (fl & TF_LEAF) {
       const TreeExt x = load_ext(ext, p);
       const bool own = own_error(hop, fl, x.thr, k0, k1);
-      he += own ? 0x10000u : 0u;
-      if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : (f_hf & 0xFFFFu), own);
+      add_err(own);
+      if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : cur_hop(), own);
       if (entry) {
         done = true;
         lat = x.tc;
@@ -402,14 +459,15 @@ TW_PRAGMA_UNROLL
     }
     const bool own =
         (DRAW && (fl & TF_ERR_DRAW)) ? own_error(hop, fl, load_ext(ext, p).thr, k0, k1) : (fl & TF_ERR_ALWAYS) != 0;
-    if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : (f_hf & 0xFFFFu), own);
+    if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : cur_hop(), own);
     if (!entry) push();
     f_pos = p;
     f_acc = 0;
     f_cmax = 0;
     const bool pk = (fl & TF_PROBK0) != 0;
     f_res = pk ? residues(hop, 0, k0, k1) : 0u;
-    f_hf = hop | HF((own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT));
+    f_hf = (W ? 0u : hop) | HF((own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT));
+    if (W) f_hop = hop;
     end = p + n.size();
     p += 1;
   }
@@ -417,7 +475,7 @@ TW_PRAGMA_UNROLL
   // pass call position p if its skip draw (already in f_res) says skip
   template <class Nodes>
   ISIM_TW bool scan(const Nodes &nodes, const TreeStep *stp) {
-    const NodeW n = nodes.load(p);
+    const auto n = nodes.load(p);
     if (!n.prob() || f_kb() != ((uint32_t)n.k() >> 2) || !skipped(n)) return false;
     TT acc = f_acc, cm = f_cmax;
     uint32_t fl = f_hf;

@@ -75,11 +75,11 @@ struct Sink {
   }
 };
 
-template <bool MB>
-void walk_all(const Program &prog, uint64_t seed, uint64_t begin, uint64_t n, std::vector<Item> &items,
-              std::vector<uint64_t> &dur_of, std::vector<uint64_t> &toff, std::vector<uint32_t> &terr) {
-  tw::Lane<kTreeMaxFrames + 1, MB, true, false, true, uint64_t> L;
-  const tw::CpuNodes nodes{prog.tree_nodes.data()};
+template <bool MB, bool W, class Nodes>
+void walk_all(const Program &prog, const Nodes &nodes, uint64_t seed, uint64_t begin, uint64_t n,
+              std::vector<Item> &items, std::vector<uint64_t> &dur_of, std::vector<uint64_t> &toff,
+              std::vector<uint32_t> &terr) {
+  tw::Lane<kTreeMaxFrames + 1, MB, true, false, true, uint64_t, W> L;
   for (uint64_t t = 0; t < n; ++t) {
     Sink s{&items, &dur_of, toff[t], (uint32_t)t};
     L.start(begin + t);
@@ -142,8 +142,15 @@ int main(int argc, char **argv) {
   std::vector<uint64_t> dur_of;
   std::vector<uint64_t> toff(n + 1, 0);
   std::vector<uint32_t> terr(n);
-  if (modeb) walk_all<true>(prog, seed, begin, n, items, dur_of, toff, terr);
-  else walk_all<false>(prog, seed, begin, n, items, dur_of, toff, terr);
+  const tw::CpuNodes nodes{prog.tree_nodes.data()};
+  const tw::CpuNodesW nodes_w{prog.tree_nodes_w.data()};
+  if (prog.tree_wide) {  // a wide tree (ISIM_TREE_FORCE_WIDE): 16-byte nodes, 32-bit frames
+    if (modeb) walk_all<true, true>(prog, nodes_w, seed, begin, n, items, dur_of, toff, terr);
+    else walk_all<false, true>(prog, nodes_w, seed, begin, n, items, dur_of, toff, terr);
+  } else {
+    if (modeb) walk_all<true, false>(prog, nodes, seed, begin, n, items, dur_of, toff, terr);
+    else walk_all<false, false>(prog, nodes, seed, begin, n, items, dur_of, toff, terr);
+  }
   const uint64_t M = items.size();
   // mode B: an invocation with a callee that responded 500 failed at that
   // callee's call step (the last one it ran: no later step has callees)

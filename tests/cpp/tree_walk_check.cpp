@@ -35,11 +35,22 @@ struct Sink {
   std::map<uint32_t, std::vector<uint64_t>> dyn;    // the LDS code-200 bucket tables, by header offset
   std::map<uint32_t, uint32_t> hdr;                 // their header words (b_lo | width << 8)
   bool out_of_table = false;
+  bool wide = false;  // a wide tree (tree.hip WideSink): every response's bucket and sum at once
   void call(uint32_t slot) { calls[slot] += 1; }
   void resp_leaf(uint32_t slot, bool st) {
     if (st) errs[slot] += 1;
+    if (!wide) return;
+    const uint32_t w = prog->slot_tbkt[slot], r = w & (kTreeLeafSlot - 1u);
+    gbucket[r][(st ? ISIM_N_PROM : 0) + (w >> 24)] += 1;
+    (st ? sum500 : sum200)[r] += prog->slot_tc[slot];
   }
   void resp(uint32_t slot, uint32_t roww, uint64_t T, bool st) {
+    if (wide) {
+      if (st) errs[slot] += 1;
+      gbucket[roww][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;
+      (st ? sum500 : sum200)[roww] += T;
+      return;
+    }
     const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
     if (st) errs[slot] += 1;
     if (place == kTreeGlobalDyn || place == kTreeGlobalStatic) {  // as tree.hip TreeSink::resp: a row in global memory
@@ -88,16 +99,17 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "compile: %s\n", err.c_str());
     return 2;
   }
-  if (prog.tree_nodes.empty()) {
+  if (!prog.has_tree()) {
     std::printf("why %s\n", prog.tree_why.c_str());
     return 3;
   }
-  std::fprintf(stderr, "positions %zu frames %u lds %u nodes_lds %u wg_per_cu %u lds_rows %u\n", prog.tree_nodes.size(),
-               prog.tree_frames, prog.tree_layout.bytes, prog.tree_layout.nodes_lds, prog.tree_layout.wg_per_cu,
-               prog.tree_layout.n_sum);
+  std::fprintf(stderr, "positions %u frames %u lds %u nodes_lds %u wg_per_cu %u lds_rows %u wide %d\n",
+               prog.tree_positions(), prog.tree_frames, prog.tree_layout.bytes, prog.tree_layout.nodes_lds,
+               prog.tree_layout.wg_per_cu, prog.tree_layout.n_sum, prog.tree_wide ? 1 : 0);
   const uint32_t S = (uint32_t)prog.n_slots, R = (uint32_t)prog.row_svc.size();
   Sink sk;
   sk.prog = &prog;
+  sk.wide = prog.tree_wide;
   sk.calls.assign(S, 0);
   sk.errs.assign(S, 0);
   sk.sum200.assign(R, 0);
@@ -131,14 +143,31 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> spill64((size_t)kTreeMaxFrames * kTreeSpillWords64, 0);
   bs.sp = as.sp = spill.data();
   cs.sp = ds.sp = spill64.data();
+  // wide trees (Program::tree_wide): the kernel's 16-frame and spilling variants, u32 and u64 time
+  tw::Lane<16, true, true, false, true, uint32_t, true> wb16;
+  tw::Lane<8, true, true, true, true, uint32_t, true> wbs;
+  tw::Lane<16, false, true, false, true, uint32_t, true> wa16;
+  tw::Lane<8, false, true, true, true, uint32_t, true> was;
+  tw::Lane<16, true, true, false, true, uint64_t, true> wc16;
+  tw::Lane<8, true, true, true, true, uint64_t, true> wcs;
+  tw::Lane<16, false, true, false, true, uint64_t, true> wd16;
+  tw::Lane<8, false, true, true, true, uint64_t, true> wds;
+  std::vector<uint32_t> spillw((size_t)kTreeMaxFrames * (kTreeSpillWords64 + kTreeSpillWide), 0);
+  wbs.sp = was.sp = wcs.sp = wds.sp = spillw.data();
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
+  const tw::CpuNodesW nodes_w{prog.tree_nodes_w.data()};
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t lat = 0;
     uint32_t hops = 0, errh = 0;
     bool r500 = false;
     auto run = [&](auto &L) {
       L.start(begin + i);
-      while (!L.done) L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      while (!L.done) {
+        if (prog.tree_wide)
+          L.step(nodes_w, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        else
+          L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+      }
       lat = L.lat;
       hops = L.hops();
       errh = L.errs();
@@ -147,7 +176,16 @@ int main(int argc, char **argv) {
     // the register-stack depth the device compiles for this graph (tree.hip tree_kernel)
     const uint32_t fr = prog.tree_frames;
     const bool spills = fr > kTreeRegFrames || std::getenv("ISIM_TW_SPILL") != nullptr;
-    if (prog.tree_t64) {
+    if (prog.tree_wide) {
+      const bool sp = fr > 16 || std::getenv("ISIM_TW_SPILL") != nullptr;
+      if (prog.tree_t64) {
+        if (modeb) sp ? run(wcs) : run(wc16);
+        else sp ? run(wds) : run(wd16);
+      } else {
+        if (modeb) sp ? run(wbs) : run(wb16);
+        else sp ? run(was) : run(wa16);
+      }
+    } else if (prog.tree_t64) {
       if (modeb) {
         if (spills) run(cs);
         else if (fr <= 8) run(c8);
@@ -203,7 +241,7 @@ int main(int argc, char **argv) {
   }
   for (const TreeDynRow &d : prog.tree_dyn)
     for (uint32_t j = 0; j < d.width; ++j) row[d.row][d.b_lo + j] += sk.dyn[d.off][j];
-  for (uint32_t s = 0; s < S; ++s) {  // the kernel's flush: static buckets and leaf sums from the counters
+  for (uint32_t s = 0; s < S && !prog.tree_wide; ++s) {  // the kernel's flush: static buckets and leaf sums from the counters
     const uint32_t w = prog.slot_tbkt[s], r = w & kTreeRowMask, b = w >> 24;
     if (b != kTreeDynBucket) {
       row[r][b] += sk.calls[s] - sk.errs[s];

@@ -112,12 +112,19 @@ def test_des_class():
         sv["errorRate"] = 0.1
     assert isim.DesHandler(_handler(seq), 1_000_000).info.items == 0
     assert isim.DesHandler(_handler(seq, error_mode=isim.MODE_B), 1_000_000).info.items == 1
-    # a dynamic walk needs the lane tree walk's tree (at most 65,535 potential invocations)
-    # (a chain of 17 services each calling the next twice: 2^17 - 1 positions)
-    big = {"services": [{"name": f"s{i}", "isEntrypoint": i == 0,
-                         "script": [{"call": {"service": f"s{i + 1}", "probability": 50}}] * 2 if i < 16 else []}
-                        for i in range(17)]}
-    _rejects(_handler(big), "unrolled tree")
+    # more than 65,535 potential invocations: a wide tree (round 5) — a chain of
+    # 17 services each calling the next twice: 2^17 - 1 positions
+    def chain(conc):
+        call = {"call": {"service": None, "probability": 50}}
+        out = []
+        for i in range(17):
+            c = [json.loads(json.dumps(call).replace("null", f'"s{i + 1}"')) for _ in range(2)] if i < 16 else []
+            out.append({"name": f"s{i}", "isEntrypoint": i == 0, "script": ([c] if conc else c) if c else []})
+        return {"services": out}
+    dw = isim.DesHandler(_handler(chain(True)), 1_000_000)
+    assert dw.info.items == 1 and dw.info.n_positions == (1 << 17) - 1
+    # sequential: every call step after the previous one's subtree — 131,071 rounds
+    _rejects(_handler(chain(False)), "rounds")
     doc = tree_topology(3, 3)
     doc["services"][-1]["numReplicas"] = 65
     isim.DesHandler(_handler(doc), 1_000_000)  # no sleeps: never queues, replicas do not matter

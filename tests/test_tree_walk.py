@@ -51,7 +51,7 @@ def run_check(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80,
     if r.returncode == 3:
         return None
     assert r.returncode == 0, r.stderr + r.stdout
-    recs, out = [], {"dur": {}}
+    recs, out = [], {"dur": {}, "stderr": r.stderr}
     for line in r.stdout.splitlines():
         f = line.split()
         if f[0] == "rec":
@@ -63,11 +63,14 @@ def run_check(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80,
     return recs, out
 
 
-def compare(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80, resp=80, begin=0, n=500):
+def compare(checker, tmp_path, j, mode=0, seed=0x15070BE, hop=250_000, req=80, resp=80, begin=0, n=500,
+            wide=None):
     got = run_check(checker, tmp_path, j, mode, seed, hop, req, resp, begin, n)
     if got is None:
         return False
     recs, out = got
+    if wide is not None:  # the tree format the program compiler chose
+        assert (" wide 1" in out["stderr"]) == wide, out["stderr"]
     sg = SimGraph(gr.unmarshal_service_graph(j))
     p = SimParams(seed, hop, req, resp, mode)
     orec, ost = oc.run(sg, p, sg.entry(), begin, n, records=True, n_threads=1)
@@ -223,3 +226,29 @@ def test_u64_time(checker, tmp_path, mode):
     got = run_check(checker, tmp_path, json.dumps({"services": svcs}), mode, n=50)
     assert got is not None and max(r[0] for r in got[0]) > 1 << 32
     assert compare(checker, tmp_path, json.dumps({"services": svcs}), mode, n=400)
+
+
+# ---- wide trees (round 5, kernel_abi.h TreeNodeW): more than 65,535
+# potential invocations, call sites or rows, or per-slot counters past the
+# LDS — 32-bit node fields and frames, statistics by global atomics
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_forced_wide(checker, tmp_path, monkeypatch, mode):
+    """Every tree shape in the wide format (ISIM_TREE_FORCE_WIDE): meshes,
+    concurrent and sequential realistic graphs, the spilling depths, u64 time."""
+    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
+    assert compare(checker, tmp_path, with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
+                   mode, n=1000, wide=True)
+    deep = realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2), probability=70)
+    assert compare(checker, tmp_path, obj_to_json(deep), mode, n=600, wide=True)
+    seq = realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.1), probability=75)  # u64 time
+    assert compare(checker, tmp_path, obj_to_json(seq), mode, n=300, wide=True)
+    monkeypatch.setenv("ISIM_TW_SPILL", "1")
+    assert compare(checker, tmp_path, obj_to_json(deep), mode, n=300, wide=True)
+
+
+def test_wide_by_size(checker, tmp_path):
+    """A graph past the 8-byte nodes: 70,000 services with probabilistic calls
+    (70,000 positions and call sites) — wide without forcing, bit-exact."""
+    doc = realistic_topology(70000, concurrent=True, sleep_ms=(1, 3), error_rate=(0.0, 0.01), probability=40)
+    assert compare(checker, tmp_path, obj_to_json(doc), 0, n=60, wide=True)
