@@ -326,3 +326,13 @@ def test_items_c3s_u64_walk(gpu):
     c = DesCase(j, 6_000_000)
     assert c.d.info.items == 1 and c.h.info.time_bits == 64
     c.compare(1 << 20, 4000)
+
+
+@pytest.mark.parametrize("name", ["real300p60", "canonical_p50", "mesh_des"])
+def test_items_wide_tree(gpu, monkeypatch, name):
+    """The item engine over a wide tree (ISIM_TREE_FORCE_WIDE: 16-byte nodes,
+    32-bit frames in the pre-walk; positions past 16 bits in the records and
+    the renumbering sort), modes A and B, against the oracle."""
+    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
+    DesCase(CASES[name](), 300_000).compare(1000, 3000)
+    DesCase(MODE_B_CASES["seq_tree_abort"](), 300_000, error_mode=isim.MODE_B).compare(9, 2000)

@@ -387,3 +387,40 @@ def test_tree_u64_time(gpu, mode):
     w = Case(j, None, isim.SimParams(error_mode=mode, flags=isim.native.FLAG_WAVE_WALK))
     assert w.handler.launch_info(0)["kernel_kind"] == 3
     w.compare(7, 1000)
+
+
+# ---- wide trees (round 5): past 65,535 positions, call sites or rows, or
+# per-slot counters that do not fit in LDS — 16-byte nodes, 32-bit frames,
+# every statistic by a global atomic (tree.hip WideSink; its LDS holds the
+# histograms and accumulators only)
+WIDE_LDS = 2048
+
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_tree_wide_forced(gpu, monkeypatch, mode):
+    """Every tree shape in the wide format (ISIM_TREE_FORCE_WIDE): a mesh,
+    a deep concurrent realistic graph, a 40-deep chain (spilled frames), u64
+    time — bit-exact against the oracle on windows across 2^32."""
+    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
+    docs = [with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
+            obj_to_json(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2),
+                                           probability=70)),
+            _prob_chain(40),
+            obj_to_json(realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.1), probability=75))]
+    for j in docs:
+        c = Case(j, None, isim.SimParams(error_mode=mode))
+        li = c.handler.launch_info(0)
+        assert li["kernel_kind"] == 7 and li["lds_bytes"] < WIDE_LDS
+        c.compare(1000, 3000)
+        c.compare((1 << 32) - 700, 1400)
+
+
+def test_tree_wide_by_size(gpu):
+    """70,000 services with probabilistic calls: 70,000 positions and call
+    sites, past the 8-byte nodes — the wide kernel without forcing."""
+    j = obj_to_json(realistic_topology(70000, concurrent=True, sleep_ms=(1, 3), error_rate=(0.0, 0.01),
+                                       probability=40))
+    c = Case(j, None, isim.SimParams())
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7 and li["lds_bytes"] < WIDE_LDS
+    c.compare(77, 2000)
