@@ -176,10 +176,12 @@ typedef struct {
                                 5 draw stream with the mode-B bit stack (call depth <= 32),
                                 6 draw stream with the mode-B close list (the default in mode B),
                                 7 lane tree walk (dynamic walks whose unrolled tree of potential
-                                invocations and LDS tables fit; else 2/3) */
+                                invocations has at most 2^24 positions; else 2/3) */
   int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
-  int32_t reserved;          /* 0 */
+  int32_t tree_wide;         /* kind 7 on a wide tree (more than 65,535 positions, call sites or rows, or
+                                per-site counters past the LDS): 16-byte nodes, the hottest sites counted
+                                in LDS, the rest by global atomics; else 0 */
   uint64_t max_launch_traces; /* isim_serve_device splits a batch into launches of at most this many traces
                                  (per-workgroup u32 LDS counters must not wrap) */
 } isim_launch_info;

@@ -83,6 +83,7 @@ struct DevState {
   isim::TreeDynRow *d_tree_dyn = nullptr;  // kind 7: the LDS bucket tables' rows
   uint32_t *d_sum_row = nullptr;        // kind 7: per LDS sum index, its row
   uint32_t *d_slot_tc = nullptr;        // kind 7: per slot, the leaf callee's latency
+  uint32_t *d_lds_slot = nullptr;       // kind 7, wide tree: per LDS counter its slot
   uint32_t *d_spill = nullptr;          // kind 7: frames below the register stack, kSpillAreas areas
   uint32_t spill_lanes = 0;
   size_t spill_words = 0;               // u32 words of one area
@@ -101,7 +102,7 @@ void free_dev(DevState &d) {
                   (void *)d.d_des_pipe,
                   d.d_des_ext, d.d_des_steps, d.d_des_ipos, d.d_des_nodes, d.d_des_text, d.d_des_tstep,
                   (void *)d.d_des_sround, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
-                  (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill})
+                  (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill, (void *)d.d_lds_slot})
     if (q) (void)hipFree(q);
   for (hipEvent_t e : d.spill_ev)
     if (e) (void)hipEventDestroy(e);
@@ -325,6 +326,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
     if (const int rc = up(st.d_tree_step, p.tree_step)) return rc;
     if (const int rc = up(st.d_sum_row, p.sum_row)) return rc;
     if (const int rc = up(st.d_slot_tc, p.slot_tc)) return rc;
+    if (const int rc = up(st.d_lds_slot, p.tree_lds_slot)) return rc;
     HIPCHK(hipMalloc(&st.d_tree_dyn, std::max<size_t>(1, p.tree_dyn.size()) * sizeof(isim::TreeDynRow)));
     if (!p.tree_dyn.empty())
       HIPCHK(hipMemcpy(st.d_tree_dyn, p.tree_dyn.data(), p.tree_dyn.size() * sizeof(isim::TreeDynRow),
@@ -562,7 +564,7 @@ int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out)
   out->max_blocks = (int32_t)st->max_blocks;
   out->kernel_kind = (int32_t)st->kind;
   out->fill = st->draw_free && !(h->params.flags & ISIM_FLAG_WALK_ALL) ? 1 : 0;
-  out->reserved = 0;
+  out->tree_wide = st->kind == 7 && h->prog.tree_wide ? 1 : 0;
   out->max_launch_traces = max_launch_traces(st);
   return ISIM_OK;
 }
@@ -633,6 +635,8 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   kp.dyn_words = h->prog.tree_dyn_words;
   kp.tree_flags = h->prog.tree_flags;
   kp.lay = h->prog.tree_layout;
+  kp.lds_slot = st->d_lds_slot;
+  kp.n_lds_slots = (uint32_t)h->prog.tree_lds_slot.size();
   const uint64_t per_wave = is_stream(st->kind) ? isim::stream_traces_per_wave() : 64u;
   const uint64_t batches = (n_traces + per_wave - 1) / per_wave;
   const uint64_t waves = st->threads / 64;

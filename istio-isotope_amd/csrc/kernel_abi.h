@@ -112,7 +112,7 @@ struct TreeNodeW {
   uint32_t k;      // index of the call command in the caller's script
   uint8_t prob;    // 1..99: draw to skip; 0: always called
   uint8_t flags;   // TF_*
-  uint16_t pad;
+  uint16_t lidx;   // the call site's LDS counter (0xFFFF: global atomics; program.cpp: the hottest sites)
   uint32_t slot;   // stats slot of the call site
 };
 static_assert(sizeof(TreeNodeW) == 16, "TreeNodeW must be 16 bytes");
@@ -210,6 +210,8 @@ struct KParams {
   uint32_t dyn_words;            // kind 7: LDS words of the bucket tables
   uint32_t tree_flags;           // kind 7: kTreeAny*
   TreeLayout lay;                // kind 7: LDS layout
+  const uint32_t *lds_slot;      // kind 7, wide tree: per LDS counter its slot (lay.off_cnt .. off_sums)
+  uint32_t n_lds_slots;          // kind 7, wide tree: LDS counters
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to

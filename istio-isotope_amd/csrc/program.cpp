@@ -256,6 +256,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     }
   out.tree_flags = 0;
   std::vector<uint32_t> through(out.n_slots, 0);
+  std::vector<double> slot_heat(out.n_slots, 0.0);  // expected calls per trace (a wide tree's LDS counters)
   std::vector<uint32_t> row_through(R, 0);
   std::vector<int32_t> pos_callee;  // per position: the callee service
   // preorder DFS over call sites; frame = (service, next call index, position, path probability)
@@ -307,6 +308,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       if (row_bw[row]) row_through[row] += 1;
       const double heat = top.heat * (nd.prob ? nd.prob / 100.0 : 1.0);
       row_heat[row] += heat;
+      slot_heat[slot] += heat;
       if (st.hop >= k32 || own_time(c) >= k32 || cs.pre >= k32 || cs.cmax0 >= k32)
         return give_up("a hop cost, script time or step sleep >= 2^32 ns");
       TreeExt x{};
@@ -344,11 +346,25 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     }
   }
   out.tree_wide = wide;
-  if (wide) {  // no LDS tables: the accumulators, histograms and bucket LUT only
+  if (wide) {  // no duration rows in LDS: the accumulators, histograms, bucket LUT, hot slots' counters
     TreeLayout &L = out.tree_layout;
     L = TreeLayout{};
     const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;
-    L.off_cnt = L.off_sums = L.off_dyn = L.off_nodes = L.bytes = head;
+    // the hottest call sites (expected calls per trace) keep guarded 16-bit
+    // counter pairs in LDS, as the 8-byte kernel's (one word each, up to the
+    // whole CU); the index rides in TreeNodeW.pad (0xFFFF: global atomics)
+    std::vector<uint32_t> order(out.n_slots);
+    for (uint32_t i = 0; i < (uint32_t)out.n_slots; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return slot_heat[a] > slot_heat[b]; });
+    const uint32_t K = std::min<uint32_t>({(uint32_t)out.n_slots, (kTreeLdsFull - head) / 4u, 0xFFFEu});
+    out.tree_slot_lds.assign(out.n_slots, 0xFFFFu);
+    out.tree_lds_slot.assign(order.begin(), order.begin() + K);
+    for (uint32_t i = 0; i < K; ++i) out.tree_slot_lds[order[i]] = (uint16_t)i;
+    for (TreeNodeW &nd : out.tree_nodes_w) nd.lidx = out.tree_slot_lds.empty() ? 0xFFFFu : out.tree_slot_lds[nd.slot];
+    out.tree_nodes_w[0].lidx = 0xFFFFu;  // the entry has no call site
+    L.off_cnt = head;
+    L.cnt16 = 1;
+    L.off_sums = L.off_dyn = L.off_nodes = L.bytes = head + 4u * K;
     L.wg_per_cu = 1;
     out.sum_row.clear();
     out.tree_dyn.clear();

@@ -52,6 +52,8 @@ struct Program {
   std::vector<TreeNode> tree_nodes;
   std::vector<TreeNodeW> tree_nodes_w;
   bool tree_wide = false;           // a wide tree (kernel_abi.h TreeNodeW): 32-bit fields, global statistics
+  std::vector<uint16_t> tree_slot_lds;  // wide: per slot its LDS counter (0xFFFF: global atomics)
+  std::vector<uint32_t> tree_lds_slot;  // wide: per LDS counter its slot
   std::vector<TreeExt> tree_ext;
   std::vector<TreeStep> tree_step;
   std::vector<uint32_t> slot_tbkt;  // per slot: callee row | kTreeLeafSlot | static duration bucket << 24

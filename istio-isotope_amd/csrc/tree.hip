@@ -103,10 +103,13 @@ struct GlobalNodesW {
 };
 
 // A wide tree's statistics (Program::tree_wide: call sites, rows or
-// positions past 16 bits, or counters that do not fit in LDS): every event
-// by a global u64 atomic — calls and callee 500s per slot, each response's
-// duration bucket and sum in its row (a leaf callee's from its slot: static
-// bucket and latency).  No LDS tables, no flush beyond the histograms.
+// positions past 16 bits, or counters that do not fit in LDS): the hottest
+// call sites (program.cpp, by expected calls per trace) count calls and
+// callee 500s in guarded 16-bit LDS pairs as the 8-byte kernel does, their
+// leaf callees' durations following from those counts at the flush; every
+// other event is a global u64 atomic — a cold site's calls and 500s, each
+// calling callee's duration bucket and sum in its row, a cold leaf callee's
+// (static bucket and latency, from its slot).
 __device__ __forceinline__ uint32_t wide_row(uint32_t w) {
   uint32_t r = w & (kTreeLeafSlot - 1u);
   asm volatile("" : "+v"(r));  // (as dur_row: keep the mask out of the address arithmetic)
@@ -118,19 +121,45 @@ struct WideSink {
   uint32_t n_slots;
   unsigned long long *sites;
   const uint32_t *slot_tbkt, *slot_tc;
-  __device__ __forceinline__ void call(uint32_t slot) { atomicAdd(sites + slot, 1ull); }
-  __device__ __forceinline__ void resp_leaf(uint32_t slot, bool st) {
-    if (st) atomicAdd(sites + n_slots + slot, 1ull);
-    if (!svc_tab) return;
+  uint32_t *cnt;               // LDS: per hot site calls | 500s << 16 (guarded 16-bit fields)
+  const uint32_t *lds_slot;    // per LDS counter: its slot
+  // a leaf callee's durations, n of them (static bucket and latency)
+  __device__ __forceinline__ void leaf_dur(uint32_t slot, bool st, unsigned long long n) {
     const uint32_t w = slot_tbkt[slot];
     unsigned long long *row = (unsigned long long *)(svc_tab + (uint64_t)wide_row(w) * ISIM_SVC_DUR_WORDS);
-    atomicAdd(row + (st ? ISIM_N_PROM : 0u) + (w >> 24), 1ull);
+    atomicAdd(row + (st ? ISIM_N_PROM : 0u) + (w >> 24), n);
     const uint32_t tc = slot_tc[slot];
-    if (tc) atomicAdd(row + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)tc);
+    if (tc) atomicAdd(row + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)tc * n);
+  }
+  // a hot site's 16-bit field reached 2^15: 2^15 of its events to the stats
+  // (and, a leaf callee's, their durations; a 500 moves from code 200 to 500)
+  __device__ __forceinline__ void move(uint32_t li, bool err) {
+    constexpr unsigned long long K = 0x8000ull;
+    const uint32_t slot = lds_slot[li];
+    atomicAdd(sites + (err ? n_slots : 0u) + slot, K);
+    lds_add(cnt + li, err ? 0x80000000u : 0xFFFF8000u);  // the field less 2^15 (no borrow: it is >= 2^15)
+    if (svc_tab && (slot_tbkt[slot] & kTreeLeafSlot)) {
+      if (err) leaf_dur(slot, false, 0ull - K);
+      leaf_dur(slot, err, K);
+    }
+  }
+  __device__ __forceinline__ void count(uint32_t site, bool err) {
+    if (site & tw::kSiteLds) {
+      const uint32_t li = site & 0xFFFFu;
+      const uint32_t old = lds_add_rtn(cnt + li, err ? 0x10000u : 1u);
+      if (((old >> (err ? 16 : 0)) & 0xFFFFu) == 0x7FFFu) move(li, err);
+    } else {
+      atomicAdd(sites + (err ? n_slots : 0u) + site, 1ull);
+    }
+  }
+  __device__ __forceinline__ void call(uint32_t site) { count(site, false); }
+  __device__ __forceinline__ void resp_leaf(uint32_t site, bool st) {
+    if (st) count(site, true);
+    if (svc_tab && !(site & tw::kSiteLds)) leaf_dur(site, st, 1ull);  // (hot sites: at the flush)
   }
   template <typename TT>
-  __device__ __forceinline__ void resp(uint32_t slot, uint32_t roww, TT T, bool st) {
-    if (st) atomicAdd(sites + n_slots + slot, 1ull);
+  __device__ __forceinline__ void resp(uint32_t site, uint32_t roww, TT T, bool st) {
+    if (st) count(site, true);
     if (!svc_tab) return;
     unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)wide_row(roww) * ISIM_SVC_DUR_WORDS);
     atomicAdd(r + (st ? ISIM_N_PROM : 0u) + lut_bucket(lut, T), 1ull);
@@ -322,8 +351,8 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   __syncthreads();
   auto sink = [&]() {
     if constexpr (WIDE)
-      return WideSink{lut, c.svc_tab, S, reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt,
-                      kp.slot_tc};
+      return WideSink{lut,       c.svc_tab,  S, reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES),
+                      slot_tbkt, kp.slot_tc, c.cnt, kp.lds_slot};
     else
       return TreeSink{c.cnt, lut, sum200, dyn, lay.compact != 0, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
                       reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
@@ -485,7 +514,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
   // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
-  if constexpr (!WIDE) {  // (a wide tree counted every event in HBM)
+  if constexpr (!WIDE) {
   auto calls_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] & 0xFFFFu) : c.cnt[s]; };
   auto errs_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] >> 16) : c.cnt[S + s]; };
   for (uint32_t i = threadIdx.x; i < 2u * S; i += blockDim.x) {
@@ -519,6 +548,26 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       if (v) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
     }
   }
+  } else {  // a wide tree: the hot sites' LDS counters (the cold ones counted in HBM as they came)
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
+    for (uint32_t i = threadIdx.x; i < kp.n_lds_slots; i += blockDim.x) {
+      const uint32_t v = c.cnt[i], calls = v & 0xFFFFu, errs = v >> 16;
+      if (!v) continue;
+      const uint32_t s = kp.lds_slot[i];
+      if (calls) atomicAdd(st + ISIM_ST_SITES + s, (unsigned long long)calls);
+      if (errs) atomicAdd(st + ISIM_ST_SITES + S + s, (unsigned long long)errs);
+      const uint32_t w = slot_tbkt[s];
+      if (!tab || !(w & kTreeLeafSlot)) continue;  // (a calling callee's durations came per response)
+      // code-200 events = calls - 500s, in u64 wrap-around arithmetic (the guarded fields, as above)
+      const unsigned long long ok = (unsigned long long)calls - (unsigned long long)errs;
+      unsigned long long *row = tab + (uint64_t)wide_row(w) * ISIM_SVC_DUR_WORDS;
+      const uint32_t bk = w >> 24;
+      const unsigned long long tc = kp.slot_tc[s];
+      if (ok) atomicAdd(row + bk, ok);
+      if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
+      if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
+      if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
+    }
   }  // !WIDE
   if (c.svc_tab) {
     unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);

@@ -89,6 +89,7 @@ struct NodeW {
   ISIM_TW uint32_t prob() const { return w1 & 0xFFu; }
   ISIM_TW uint32_t flags() const { return (w1 >> 8) & 0xFFu; }
   ISIM_TW uint32_t slot() const { return w1 >> 16; }
+  ISIM_TW uint32_t site() const { return slot(); }  // what the sink counts the call under
 };
 static_assert(sizeof(TreeNode) == sizeof(NodeW), "TreeNode is two words");
 struct CpuNodes {
@@ -100,13 +101,16 @@ struct CpuNodes {
   }
 };
 // A wide tree's TreeNodeW (kernel_abi.h): the same accessors on 32-bit fields
+constexpr uint32_t kSiteLds = 0x80000000u;
 struct NodeW4 {
-  uint32_t sz, kk, pf, sl;  // size, k, prob | flags << 8, slot
+  uint32_t sz, kk, pf, sl;  // size, k, prob | flags << 8 | LDS counter << 16, slot
   ISIM_TW uint32_t size() const { return sz; }
   ISIM_TW uint32_t k() const { return kk; }
   ISIM_TW uint32_t prob() const { return pf & 0xFFu; }
   ISIM_TW uint32_t flags() const { return (pf >> 8) & 0xFFu; }
   ISIM_TW uint32_t slot() const { return sl; }
+  // a hot site's LDS counter | kSiteLds, else the slot (global atomics)
+  ISIM_TW uint32_t site() const { return (pf >> 16) != 0xFFFFu ? kSiteLds | (pf >> 16) : sl; }
 };
 static_assert(sizeof(TreeNodeW) == sizeof(NodeW4), "TreeNodeW is four words");
 struct CpuNodesW {
@@ -406,7 +410,7 @@ TW_PRAGMA_UNROLL
       root500 = st;
       return false;
     }
-    sink.resp(nodes.load(f_pos).slot(), x.row, T, st);
+    sink.resp(nodes.load(f_pos).site(), x.row, T, st);
     if constexpr (has_exec<Sink>::value) sink.dur(cur_hop(), T, st);
     const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
@@ -439,7 +443,7 @@ TW_PRAGMA_UNROLL
     he += 1u;
     const uint32_t fl = n.flags();
     const bool entry = p == 0;  // the trace's first step: the entry (no call site, no caller)
-    if (!entry) sink.call(n.slot());
+    if (!entry) sink.call(n.site());
     if (fl & TF_LEAF) {
       const TreeExt x = load_ext(ext, p);
       const bool own = own_error(hop, fl, x.thr, k0, k1);
@@ -451,7 +455,7 @@ TW_PRAGMA_UNROLL
         root500 = own;
         return;
       }
-      sink.resp_leaf(n.slot(), own);
+      sink.resp_leaf(n.site(), own);
       if constexpr (has_exec<Sink>::value) sink.dur(hop, x.tc, own);
       fold((TT)x.H + x.tc, own, (fl & TF_CONC) != 0);
       p += 1;

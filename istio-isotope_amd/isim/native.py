@@ -76,7 +76,7 @@ class HandlerInfo(C.Structure):
 class LaunchInfo(C.Structure):
     _fields_ = [("wg_threads", C.c_int32), ("lds_bytes", C.c_int32), ("lds_counters", C.c_int32),
                 ("blocks_per_cu", C.c_int32), ("max_blocks", C.c_int32), ("kernel_kind", C.c_int32),
-                ("fill", C.c_int32), ("reserved", C.c_int32), ("max_launch_traces", C.c_uint64)]
+                ("fill", C.c_int32), ("tree_wide", C.c_int32), ("max_launch_traces", C.c_uint64)]
 
 
 class DesParams(C.Structure):

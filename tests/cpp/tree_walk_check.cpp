@@ -36,15 +36,21 @@ struct Sink {
   std::map<uint32_t, uint32_t> hdr;                 // their header words (b_lo | width << 8)
   bool out_of_table = false;
   bool wide = false;  // a wide tree (tree.hip WideSink): every response's bucket and sum at once
-  void call(uint32_t slot) { calls[slot] += 1; }
-  void resp_leaf(uint32_t slot, bool st) {
+  // a wide tree's node gives a hot site's LDS counter | kSiteLds (tree_walk.h NodeW4::site)
+  uint32_t slot_of(uint32_t site) const {
+    return (wide && (site & tw::kSiteLds)) ? prog->tree_lds_slot[site & 0xFFFFu] : site;
+  }
+  void call(uint32_t site) { calls[slot_of(site)] += 1; }
+  void resp_leaf(uint32_t site, bool st) {
+    const uint32_t slot = slot_of(site);
     if (st) errs[slot] += 1;
     if (!wide) return;
     const uint32_t w = prog->slot_tbkt[slot], r = w & (kTreeLeafSlot - 1u);
     gbucket[r][(st ? ISIM_N_PROM : 0) + (w >> 24)] += 1;
     (st ? sum500 : sum200)[r] += prog->slot_tc[slot];
   }
-  void resp(uint32_t slot, uint32_t roww, uint64_t T, bool st) {
+  void resp(uint32_t site, uint32_t roww, uint64_t T, bool st) {
+    const uint32_t slot = slot_of(site);
     if (wide) {
       if (st) errs[slot] += 1;
       gbucket[roww][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;

@@ -391,11 +391,8 @@ def test_tree_u64_time(gpu, mode):
 
 # ---- wide trees (round 5): past 65,535 positions, call sites or rows, or
 # per-slot counters that do not fit in LDS — 16-byte nodes, 32-bit frames,
-# every statistic by a global atomic (tree.hip WideSink; its LDS holds the
-# histograms and accumulators only)
-WIDE_LDS = 2048
-
-
+# the hottest call sites counted in LDS, the rest by global atomics (tree.hip
+# WideSink; isim_launch_info.tree_wide)
 @pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
 def test_tree_wide_forced(gpu, monkeypatch, mode):
     """Every tree shape in the wide format (ISIM_TREE_FORCE_WIDE): a mesh,
@@ -410,7 +407,7 @@ def test_tree_wide_forced(gpu, monkeypatch, mode):
     for j in docs:
         c = Case(j, None, isim.SimParams(error_mode=mode))
         li = c.handler.launch_info(0)
-        assert li["kernel_kind"] == 7 and li["lds_bytes"] < WIDE_LDS
+        assert li["kernel_kind"] == 7 and li["tree_wide"] == 1
         c.compare(1000, 3000)
         c.compare((1 << 32) - 700, 1400)
 
@@ -422,5 +419,5 @@ def test_tree_wide_by_size(gpu):
                                        probability=40))
     c = Case(j, None, isim.SimParams())
     li = c.handler.launch_info(0)
-    assert li["kernel_kind"] == 7 and li["lds_bytes"] < WIDE_LDS
+    assert li["kernel_kind"] == 7 and li["tree_wide"] == 1
     c.compare(77, 2000)
