@@ -25,6 +25,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -139,8 +140,16 @@ def build_graph(config: str, prob: int = 50):
                             "~30 s latency bound, lane tree walk with u64 time",
                 "services": 10000, "probability": prob}
     elif config == "c4w":
-        j = obj_to_json(realistic_topology(100000, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.01),
-                                           probability=prob))
+        # (the 100k-node generator takes ~40 s: the JSON is cached per probability under the temp dir)
+        cache = os.path.join(tempfile.gettempdir(), f"isim_c4w_p{prob}.json")
+        if os.path.exists(cache):
+            j = open(cache).read()
+        else:
+            j = obj_to_json(realistic_topology(100000, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.01),
+                                               probability=prob))
+            with open(cache + f".{os.getpid()}", "w") as f:
+                f.write(j)
+            os.replace(cache + f".{os.getpid()}", cache)
         desc = {"workload": f"create_realistic_topology.py multitier Barabasi 100k services (restated generator, "
                             f"seed 42), concurrent fan-out, sleep U{{1..5}}ms, errorRate U[0,1%], probability {prob} "
                             "on every call: a wide tree (100,000 positions and call sites), lane tree walk",
