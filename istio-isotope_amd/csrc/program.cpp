@@ -346,17 +346,45 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     }
   }
   out.tree_wide = wide;
-  if (wide) {  // no duration rows in LDS: the accumulators, histograms, bucket LUT, hot slots' counters
+  if (wide) {  // LDS: the accumulators, histograms, bucket LUT, then the hottest rows and call sites
     TreeLayout &L = out.tree_layout;
     L = TreeLayout{};
     const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;
+    // the hottest calling rows (expected invocations per trace) in up to half
+    // the CU's LDS, as the 8-byte kernel's wide rows (a u64 code-200 sum and
+    // a [2][width] bucket table — width 1 for a static bucket, so every hot
+    // row counts its buckets in LDS); the rest by global atomics
+    std::vector<uint32_t> rorder;
+    for (uint32_t r = 1; r < R; ++r)
+      if (row_nonleaf[r]) rorder.push_back(r);
+    std::stable_sort(rorder.begin(), rorder.end(), [&](uint32_t a, uint32_t b) { return row_heat[a] > row_heat[b]; });
+    out.sum_row.clear();
+    out.tree_dyn.clear();
+    out.tree_dyn_words = 0;
+    out.tree_row_place.assign(R, kTreeGlobalDyn);
+    out.tree_row_index.assign(R, 0);
+    uint32_t room = kTreeLdsHalf - head;
+    for (uint32_t r : rorder) {
+      const uint32_t w = std::max<uint32_t>(1u, row_bw[r]);
+      const uint32_t need = row_lds_bytes(w, false);
+      if (need > room || out.sum_row.size() >= 0x7FFFu || out.tree_dyn_words + 1u + 2u * w >= 0xFFF0u) continue;
+      room -= need;
+      out.tree_row_index[r] = (uint32_t)out.sum_row.size();
+      out.tree_row_place[r] = out.tree_dyn_words;
+      out.sum_row.push_back(r);
+      out.tree_dyn.push_back(TreeDynRow{r, out.tree_dyn_words, out.tree_row_blo[r], w});
+      out.tree_dyn_words += 1u + 2u * w;
+    }
+    L.n_sum = (uint32_t)out.sum_row.size();
     // the hottest call sites (expected calls per trace) keep guarded 16-bit
-    // counter pairs in LDS, as the 8-byte kernel's (one word each, up to the
-    // whole CU); the index rides in TreeNodeW.pad (0xFFFF: global atomics)
+    // counter pairs in LDS, as the 8-byte kernel's (one word each, the rest
+    // of the CU); the index rides in TreeNodeW.lidx (0xFFFF: global atomics)
+    const uint32_t rows_bytes = 8u * L.n_sum + 4u * out.tree_dyn_words;
     std::vector<uint32_t> order(out.n_slots);
     for (uint32_t i = 0; i < (uint32_t)out.n_slots; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return slot_heat[a] > slot_heat[b]; });
-    const uint32_t K = std::min<uint32_t>({(uint32_t)out.n_slots, (kTreeLdsFull - head) / 4u, 0xFFFEu});
+    const uint32_t K =
+        std::min<uint32_t>({(uint32_t)out.n_slots, (kTreeLdsFull - head - rows_bytes - 8u) / 4u, 0xFFFEu});
     out.tree_slot_lds.assign(out.n_slots, 0xFFFFu);
     out.tree_lds_slot.assign(order.begin(), order.begin() + K);
     for (uint32_t i = 0; i < K; ++i) out.tree_slot_lds[order[i]] = (uint16_t)i;
@@ -364,20 +392,21 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     out.tree_nodes_w[0].lidx = 0xFFFFu;  // the entry has no call site
     L.off_cnt = head;
     L.cnt16 = 1;
-    L.off_sums = L.off_dyn = L.off_nodes = L.bytes = head + 4u * K;
+    L.off_sums = (head + 4u * K + 7u) & ~7u;
+    L.off_dyn = L.off_sums + 8u * L.n_sum;
+    L.off_nodes = L.bytes = L.off_dyn + 4u * out.tree_dyn_words;
     L.wg_per_cu = 1;
-    out.sum_row.clear();
-    out.tree_dyn.clear();
-    out.tree_dyn_words = 0;
-    out.tree_row_place.assign(R, kTreeGlobalDyn);
-    out.tree_row_index.assign(R, 0);
   }
   // the row words of the non-leaf callees (the entry's row is filled from the histograms)
   for (size_t i = 1; i < out.tree_nodes_w.size(); ++i) {
     const int32_t c = pos_callee[i];
     if (leaf[c]) continue;
     const uint32_t r = (uint32_t)out.svc_row[c];
-    out.tree_ext[i].row = wide ? r : out.tree_row_index[r] | (out.tree_row_place[r] << 16);
+    // (a wide tree: a hot row's sum index << 16 | its table's LDS offset, flagged by bit 31; else the row)
+    out.tree_ext[i].row = !wide                                  ? out.tree_row_index[r] | (out.tree_row_place[r] << 16)
+                          : out.tree_row_place[r] != kTreeGlobalDyn ? 0x80000000u | (out.tree_row_index[r] << 16) |
+                                                                          out.tree_row_place[r]
+                                                                    : r;
   }
   out.tree_ext[0].row = wide ? 0u : kTreeStaticRow << 16;
   // per slot: the callee's row, its static bucket (kTreeDynBucket when it varies), leaf flag and latency
@@ -391,8 +420,12 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     if (leaf[s] && out.svc_time[s] >= k32) return give_up("a leaf latency >= 2^32 ns");
     out.slot_tc[sl] = leaf[s] ? (uint32_t)out.svc_time[s] : 0u;
   }
-  out.tree_mult = 1;  // (a wide tree's statistics are u64 global atomics: nothing to guard)
-  if (!wide) {
+  out.tree_mult = 1;
+  if (wide) {  // a hot row's u32 LDS bucket counts: the positions into it (the launch split's guard)
+    std::vector<uint32_t> into(R, 0);
+    for (size_t i = 1; i < out.tree_nodes_w.size(); ++i) into[(uint32_t)out.svc_row[pos_callee[i]]] += 1;
+    for (uint32_t r : out.sum_row) out.tree_mult = std::max(out.tree_mult, into[r]);
+  } else {
     for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
     for (uint32_t r = 0; r < R; ++r)
       if (out.tree_row_place[r] < kTreeGlobalStatic) out.tree_mult = std::max(out.tree_mult, row_through[r]);

@@ -123,6 +123,9 @@ struct WideSink {
   const uint32_t *slot_tbkt, *slot_tc;
   uint32_t *cnt;               // LDS: per hot site calls | 500s << 16 (guarded 16-bit fields)
   const uint32_t *lds_slot;    // per LDS counter: its slot
+  unsigned long long *sum200;  // LDS: the hot rows' code-200 duration sums
+  uint32_t *dyn;               // LDS: the hot rows' bucket tables (header b_lo | width << 8, [2][width] u32)
+  const uint32_t *sum_row;     // per hot row: its row
   // a leaf callee's durations, n of them (static bucket and latency)
   __device__ __forceinline__ void leaf_dur(uint32_t slot, bool st, unsigned long long n) {
     const uint32_t w = slot_tbkt[slot];
@@ -161,6 +164,20 @@ struct WideSink {
   __device__ __forceinline__ void resp(uint32_t site, uint32_t roww, TT T, bool st) {
     if (st) count(site, true);
     if (!svc_tab) return;
+    if (roww & 0x80000000u) {  // a hot row: sum index << 16 | its bucket table's LDS offset
+      const uint32_t idx = (roww >> 16) & 0x7FFFu, place = roww & 0xFFFFu;
+      const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
+      uint32_t b = lut_bucket(lut, T) - lo;
+      b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
+      lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
+      if (st)
+        atomicAdd((unsigned long long *)(svc_tab + (uint64_t)wide_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS) +
+                      2 * ISIM_N_PROM + 1,
+                  (unsigned long long)T);
+      else
+        lds_add(sum200 + idx, (unsigned long long)T);
+      return;
+    }
     unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)wide_row(roww) * ISIM_SVC_DUR_WORDS);
     atomicAdd(r + (st ? ISIM_N_PROM : 0u) + lut_bucket(lut, T), 1ull);
     atomicAdd(r + 2 * ISIM_N_PROM + (st ? 1u : 0u), (unsigned long long)T);
@@ -351,8 +368,9 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   __syncthreads();
   auto sink = [&]() {
     if constexpr (WIDE)
-      return WideSink{lut,       c.svc_tab,  S, reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES),
-                      slot_tbkt, kp.slot_tc, c.cnt, kp.lds_slot};
+      return WideSink{lut,       c.svc_tab,  S,           reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES),
+                      slot_tbkt, kp.slot_tc, c.cnt,       kp.lds_slot,
+                      reinterpret_cast<unsigned long long *>(sum200), dyn, kp.sum_row};
     else
       return TreeSink{c.cnt, lut, sum200, dyn, lay.compact != 0, c.svc_tab, kp.sum_row, S, lay.cnt16 != 0,
                       reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES), slot_tbkt, kp.slot_tc};
@@ -568,6 +586,10 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
       if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
     }
+    for (uint32_t r = threadIdx.x; r < lay.n_sum && tab; r += blockDim.x) {  // the hot rows' code-200 sums
+      const unsigned long long v = ((unsigned long long *)sum200)[r];
+      if (v) atomicAdd(tab + (uint64_t)wide_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
+    }
   }  // !WIDE
   if (c.svc_tab) {
     unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
@@ -584,7 +606,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       }
       const TreeDynRow d = kp.tree_dyn[lo];
       if (i == d.off) continue;  // the header
-      unsigned long long *row = tab + (uint64_t)dur_row(d.row) * ISIM_SVC_DUR_WORDS;
+      unsigned long long *row = tab + (uint64_t)(WIDE ? wide_row(d.row) : dur_row(d.row)) * ISIM_SVC_DUR_WORDS;
       if (lay.compact) {  // code-200 u16 pairs
         const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
         if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));

@@ -51,10 +51,11 @@ struct Sink {
   }
   void resp(uint32_t site, uint32_t roww, uint64_t T, bool st) {
     const uint32_t slot = slot_of(site);
-    if (wide) {
+    if (wide) {  // (a hot row: bit 31 | its sum index << 16 | table offset — counted in LDS, same totals)
+      const uint32_t r = (roww & 0x80000000u) ? prog->sum_row[(roww >> 16) & 0x7FFFu] : roww;
       if (st) errs[slot] += 1;
-      gbucket[roww][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;
-      (st ? sum500 : sum200)[roww] += T;
+      gbucket[r][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;
+      (st ? sum500 : sum200)[r] += T;
       return;
     }
     const uint32_t idx = roww & 0xFFFFu, place = roww >> 16;
