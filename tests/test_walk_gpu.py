@@ -421,3 +421,21 @@ def test_tree_wide_by_size(gpu):
     li = c.handler.launch_info(0)
     assert li["kernel_kind"] == 7 and li["tree_wide"] == 1
     c.compare(77, 2000)
+
+
+def test_tree_wide_equals_narrow(gpu, monkeypatch):
+    """2^24 traces of one graph on the 8-byte kernel and forced wide: equal
+    records and statistics word for word — at that size a workgroup counts
+    more than 2^15 calls at the hot sites, so the wide sink's guarded LDS
+    fields move 2^15 events (and their leaf durations) to HBM mid-launch."""
+    j = obj_to_json(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2), probability=70))
+    n = 1 << 24
+    narrow = Case(j, None, isim.SimParams())
+    assert narrow.handler.launch_info(0)["tree_wide"] == 0
+    r1, s1 = narrow.gpu(12345, n)
+    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
+    wide = Case(j, None, isim.SimParams())
+    assert wide.handler.launch_info(0)["tree_wide"] == 1
+    r2, s2 = wide.gpu(12345, n)
+    assert np.array_equal(r1, r2)
+    assert np.array_equal(s1, s2)
