@@ -40,11 +40,16 @@ struct Sink {
   uint32_t slot_of(uint32_t site) const {
     return (wide && (site & tw::kSiteLds)) ? prog->tree_lds_slot[site & 0xFFFFu] : site;
   }
-  void call(uint32_t site) { calls[slot_of(site)] += 1; }
+  uint64_t ev_hot = 0, ev_cold = 0, row_hot = 0, row_cold = 0, leaf_cold = 0;  // wide: event kinds (stderr)
+  void call(uint32_t site) {
+    calls[slot_of(site)] += 1;
+    ((wide && (site & tw::kSiteLds)) ? ev_hot : ev_cold) += 1;
+  }
   void resp_leaf(uint32_t site, bool st) {
     const uint32_t slot = slot_of(site);
     if (st) errs[slot] += 1;
     if (!wide) return;
+    if (!(site & tw::kSiteLds)) leaf_cold += 1;
     const uint32_t w = prog->slot_tbkt[slot], r = w & (kTreeLeafSlot - 1u);
     gbucket[r][(st ? ISIM_N_PROM : 0) + (w >> 24)] += 1;
     (st ? sum500 : sum200)[r] += prog->slot_tc[slot];
@@ -53,6 +58,7 @@ struct Sink {
     const uint32_t slot = slot_of(site);
     if (wide) {  // (a hot row: bit 31 | its sum index << 16 | table offset — counted in LDS, same totals)
       const uint32_t r = (roww & 0x80000000u) ? prog->sum_row[(roww >> 16) & 0x7FFFu] : roww;
+      ((roww & 0x80000000u) ? row_hot : row_cold) += 1;
       if (st) errs[slot] += 1;
       gbucket[r][(st ? ISIM_N_PROM : 0) + prom_bucket_ns(T)] += 1;
       (st ? sum500 : sum200)[r] += T;
@@ -131,7 +137,7 @@ int main(int argc, char **argv) {
   // one Lane per depth variant, reused trace after trace as a GPU lane is
   // (tree.hip hands a lane its next trace as soon as one responds); the
   // spilling variant keeps its deep frames in a vector, one column (stride 1)
-  std::vector<uint32_t> spill((size_t)kTreeMaxFrames * kTreeSpillWords, 0);
+  std::vector<uint32_t> spill((size_t)kTreeMaxFrames * 12, 0);  // (rows of 16-B aligned frames)
   tw::Lane<4, true> b4;
   tw::Lane<8, true> b8;
   tw::Lane<16, true> b16;
@@ -147,7 +153,7 @@ int main(int argc, char **argv) {
   tw::Lane<8, false, true, false, true, uint64_t> d8;
   tw::Lane<16, false, true, false, true, uint64_t> d16;
   tw::Lane<8, false, true, true, true, uint64_t> ds;
-  std::vector<uint32_t> spill64((size_t)kTreeMaxFrames * kTreeSpillWords64, 0);
+  std::vector<uint32_t> spill64((size_t)kTreeMaxFrames * 12, 0);
   bs.sp = as.sp = spill.data();
   cs.sp = ds.sp = spill64.data();
   // wide trees (Program::tree_wide): the kernel's 16-frame and spilling variants, u32 and u64 time
@@ -159,7 +165,7 @@ int main(int argc, char **argv) {
   tw::Lane<8, true, true, true, true, uint64_t, true> wcs;
   tw::Lane<16, false, true, false, true, uint64_t, true> wd16;
   tw::Lane<8, false, true, true, true, uint64_t, true> wds;
-  std::vector<uint32_t> spillw((size_t)kTreeMaxFrames * (kTreeSpillWords64 + kTreeSpillWide), 0);
+  std::vector<uint32_t> spillw((size_t)kTreeMaxFrames * 12, 0);
   wbs.sp = was.sp = wcs.sp = wds.sp = spillw.data();
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
   const tw::CpuNodesW nodes_w{prog.tree_nodes_w.data()};
@@ -217,6 +223,11 @@ int main(int argc, char **argv) {
     root_hist[(r500 ? ISIM_N_PROM : 0) + prom_bucket_ns(lat)] += 1;
     root_sum[r500 ? 1 : 0] += lat;
   }
+  if (sk.wide)
+    std::fprintf(stderr, "wide events per trace: calls hot %.2f cold %.2f, rows hot %.2f cold %.2f, cold leaves %.2f "
+                 "(hot sites %zu, hot rows %zu)\n", (double)sk.ev_hot / n, (double)sk.ev_cold / n,
+                 (double)sk.row_hot / n, (double)sk.row_cold / n, (double)sk.leaf_cold / n, prog.tree_lds_slot.size(),
+                 prog.sum_row.size());
   // per call site and per service, as isim_stats_fold
   std::vector<uint64_t> site(prog.n_sites, 0), svc_calls(prog.n_services, 0), svc_errs(prog.n_services, 0);
   for (uint32_t s = 0; s < S; ++s) {
