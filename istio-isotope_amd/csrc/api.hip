@@ -234,7 +234,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
     tree = true;
     st.kind = 7;
     st.kernel = isim::tree_kernel(h->params.error_mode == ISIM_MODE_B, p.tree_frames,
-                                  p.tree_frames > isim::kTreeRegFrames, p.tree_layout.nodes_lds != 0,
+                                  p.tree_frames > isim::tree_reg_frames(p.tree_frames, p.tree_t64, p.tree_wide),
+                                  p.tree_layout.nodes_lds != 0,
                                   (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
                                   p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"), p.tree_t64,
                                   p.tree_wide);
@@ -371,12 +372,13 @@ int build_device(isim_handler *h, int device, DevState &st) {
   st.max_mult = std::max<uint64_t>(1, p.hops_upper);
   if (tree) {
     st.max_mult = std::max<uint32_t>(1, p.tree_mult);
-    if (p.tree_frames > isim::kTreeRegFrames) {
-      // the spill areas: frames below the 8 register frames, one column per
+    const uint32_t regf = isim::tree_reg_frames(p.tree_frames, p.tree_t64, p.tree_wide);
+    if (p.tree_frames > regf) {
+      // the spill areas: frames below the register frames, one column per
       // lane of a full grid; a launch waits for the area's previous launch
       // (launch_walk_one)
       st.spill_lanes = st.max_blocks * st.threads;
-      st.spill_words = (size_t)(p.tree_frames - 8u) *
+      st.spill_words = (size_t)(p.tree_frames - regf) *
                        ((p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) +
                         (p.tree_wide ? isim::kTreeSpillWide : 0u)) *
                        st.spill_lanes;

@@ -157,6 +157,15 @@ constexpr uint32_t kTreeMaxFrames = 64;          // open calling invocations bel
 constexpr uint32_t kTreeSpillWords = 5;          // u32 words of a spilled frame
 constexpr uint32_t kTreeSpillWords64 = 7;        // ... with u64 time (acc and step max take two words each)
 constexpr uint32_t kTreeSpillWide = 2;           // ... + position end and hop id of a wide tree's frame
+// a wide tree's kernels keep fewer frames in registers (7 or 9 words each):
+// 6 with u32 time, 4 with u64, the rest always in the spill area — at 8 the
+// 1024-thread kernels ran out of their 128 VGPRs into scratch (32-144 B per lane)
+inline uint32_t tree_wide_reg_frames(bool t64) { return t64 ? 4u : 6u; }
+// register frames of the kind-7 kernel for a tree: the spill area holds the rest
+inline uint32_t tree_reg_frames(uint32_t frames, bool t64, bool wide) {
+  if (wide) return tree_wide_reg_frames(t64);
+  return frames > kTreeRegFrames ? 8u : frames;
+}
 constexpr uint32_t kSpillAreas = 4;              // spill areas per (handler, device): launches in flight
 // LDS of the kind-7 kernel, per workgroup: the budget for two 1024-thread
 // workgroups per CU, and the whole CU.

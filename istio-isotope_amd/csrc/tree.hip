@@ -661,12 +661,12 @@ template <bool NLDS, bool DRAW>
 static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wide) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
-  if (wide) {  // a wide tree: nodes in global memory; 16 register frames, or 8 + the spill; 4 waves per SIMD
+  if (wide) {  // a wide tree: nodes in global memory; tree_wide_reg_frames register frames (+ the spill)
     if constexpr (!NLDS) {
-      if (t64) return spill ? (void *)&isim_tree<M, 8, true, false, C, DRAW, 4, true, true>
-                            : (void *)&isim_tree<M, 16, false, false, C, DRAW, 4, true, true>;
-      return spill ? (void *)&isim_tree<M, 8, true, false, C, DRAW, 4, false, true>
-                   : (void *)&isim_tree<M, 16, false, false, C, DRAW, 4, false, true>;
+      if (t64) return spill ? (void *)&isim_tree<M, 4, true, false, C, DRAW, 4, true, true>
+                            : (void *)&isim_tree<M, 4, false, false, C, DRAW, 4, true, true>;
+      return spill ? (void *)&isim_tree<M, 6, true, false, C, DRAW, 4, false, true>
+                   : (void *)&isim_tree<M, 6, false, false, C, DRAW, 4, false, true>;
     }
     return nullptr;
   }

@@ -156,15 +156,16 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> spill64((size_t)kTreeMaxFrames * 12, 0);
   bs.sp = as.sp = spill.data();
   cs.sp = ds.sp = spill64.data();
-  // wide trees (Program::tree_wide): the kernel's 16-frame and spilling variants, u32 and u64 time
-  tw::Lane<16, true, true, false, true, uint32_t, true> wb16;
-  tw::Lane<8, true, true, true, true, uint32_t, true> wbs;
-  tw::Lane<16, false, true, false, true, uint32_t, true> wa16;
-  tw::Lane<8, false, true, true, true, uint32_t, true> was;
-  tw::Lane<16, true, true, false, true, uint64_t, true> wc16;
-  tw::Lane<8, true, true, true, true, uint64_t, true> wcs;
-  tw::Lane<16, false, true, false, true, uint64_t, true> wd16;
-  tw::Lane<8, false, true, true, true, uint64_t, true> wds;
+  // wide trees (Program::tree_wide): the kernel's variants — 6 register frames (u32 time) or 4 (u64),
+  // and the same + the spill (kernel_abi.h tree_wide_reg_frames)
+  tw::Lane<6, true, true, false, true, uint32_t, true> wb16;
+  tw::Lane<6, true, true, true, true, uint32_t, true> wbs;
+  tw::Lane<6, false, true, false, true, uint32_t, true> wa16;
+  tw::Lane<6, false, true, true, true, uint32_t, true> was;
+  tw::Lane<4, true, true, false, true, uint64_t, true> wc16;
+  tw::Lane<4, true, true, true, true, uint64_t, true> wcs;
+  tw::Lane<4, false, true, false, true, uint64_t, true> wd16;
+  tw::Lane<4, false, true, true, true, uint64_t, true> wds;
   std::vector<uint32_t> spillw((size_t)kTreeMaxFrames * 12, 0);
   wbs.sp = was.sp = wcs.sp = wds.sp = spillw.data();
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
@@ -190,7 +191,7 @@ int main(int argc, char **argv) {
     const uint32_t fr = prog.tree_frames;
     const bool spills = fr > kTreeRegFrames || std::getenv("ISIM_TW_SPILL") != nullptr;
     if (prog.tree_wide) {
-      const bool sp = fr > 16 || std::getenv("ISIM_TW_SPILL") != nullptr;
+      const bool sp = fr > tree_wide_reg_frames(prog.tree_t64) || std::getenv("ISIM_TW_SPILL") != nullptr;
       if (prog.tree_t64) {
         if (modeb) sp ? run(wcs) : run(wc16);
         else sp ? run(wds) : run(wd16);
