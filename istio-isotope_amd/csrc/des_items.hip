@@ -862,6 +862,214 @@ __global__ void __launch_bounds__(kT) k_qout(K k, uint64_t m, const uint32_t *rk
   }
 }
 
+// ---- 4b'. the scan and k_qout in one pass.  The FIFO of one replica with a
+// constant hold h (a segment: a run of one (row, replica) in the round's
+// order; a zero-hold item is a segment of its own) starts its j-th item at
+//   S_j = max over the segment's items i <= j of a_i + (j - i) h
+//       = j h + max(a_i - i h),
+// a segmented prefix maximum of the keys a_i - i h (i, j: list indices; the
+// offset cancels within a segment; the host keeps j h below 2^62).  A
+// workgroup takes a tile of kT x IPT items by ticket; tiles are chained by a
+// decoupled look-back (des.hip chain_body's hand-off: sc1 stores drained
+// before the flag store, sc1 loads).  The flag word carries the launch's
+// epoch, so the states are cleared once per batch, not per launch.
+struct QState {
+  uint64_t agg, inc;  // the max after the tile's last segment start (flag >= 1); with the prefix (flag 2)
+  uint32_t flag, pad[3];
+};
+static_assert(sizeof(QState) == 32, "QState is 32 bytes");
+constexpr uint32_t kQAgg = 1, kQInc = 2, kQEpochShift = 2;
+constexpr int64_t kQMin = INT64_MIN;
+__device__ __forceinline__ int64_t qmax(int64_t a, int64_t b) { return a > b ? a : b; }
+
+// P0: a round that needs no sort (k_pairs0's order) read straight from its
+// list: the item, its position (the segment; a zero-hold item alone), row,
+// hold and arrival, instead of k_pairs0's arrays (segk, rowk, sid, mp unused)
+template <uint32_t IPT, bool P0>
+__global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *ids, const uint32_t *segk,
+                                              const uint32_t *rowk, const uint32_t *sid, const MP *mp, QState *qs,
+                                              uint32_t *ticket, uint32_t tbase, uint32_t epoch) {
+  constexpr uint32_t NW = kT / 64;
+  __shared__ uint32_t s_tile, s_row;
+  __shared__ int64_t w_v[NW], s_cin;
+  __shared__ uint32_t w_f[NW];
+  __shared__ unsigned long long s_n, s_sw, s_mw, s_sh;
+  if (threadIdx.x == 0) {
+    const uint32_t t = atomicAdd(ticket, 1u) - tbase;
+    s_tile = t;
+    const uint64_t j0 = (uint64_t)t * kT * IPT;
+    s_row = P0 ? k.pos[k.ipos[ids[j0]]].row : rowk[j0];
+    s_n = s_sw = s_mw = s_sh = 0;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t w0 = (uint64_t)tile * kT * IPT + (uint64_t)wave * 64 * IPT;
+  // the wave's rows of 64 items: a segmented max over the lanes, then over
+  // the rows (cf, cv: the wave's items so far)
+  int64_t v[IPT];
+  bool f[IPT];
+  uint64_t a[IPT], h[IPT];
+  uint32_t it[IPT], rw[IPT];  // P0: the item and its row
+  bool cf = false;
+  int64_t cv = kQMin;
+#pragma unroll
+  for (uint32_t r = 0; r < IPT; ++r) {
+    const uint64_t j = w0 + r * 64 + lane;
+    bool s = false;
+    int64_t x = kQMin;
+    a[r] = h[r] = 0;
+    if constexpr (P0) {
+      // the previous item's position: the lane below's, lane 0 reads it
+      uint32_t pv = kNone, vv = kNone;
+      if (j < m) {
+        it[r] = ids[j];
+        vv = k.ipos[it[r]];
+        rw[r] = k.pos[vv].row;
+        h[r] = k.row_hold[rw[r]];
+        a[r] = k.IA[it[r]];
+        if (lane == 0 && j > 0) pv = k.ipos[ids[j - 1]];
+      }
+      const uint32_t up = __shfl_up(vv, 1, 64);
+      if (lane > 0) pv = up;
+      if (j < m) {
+        s = j == 0 || h[r] == 0 || pv != vv;
+        x = (int64_t)(a[r] - j * h[r]);
+      }
+    } else if (j < m) {
+      s = j == 0 || segk[j - 1] != segk[j];
+      const MP p = mp[j];
+      h[r] = p.B;
+      a[r] = p.C - p.B;
+      x = (int64_t)(a[r] - j * h[r]);
+    }
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const int64_t ox = __shfl_up(x, d, 64);
+      const int os = __shfl_up((int)s, d, 64);
+      if (lane >= d) {
+        if (!s) x = qmax(x, ox);
+        s = s || os;
+      }
+    }
+    v[r] = s ? x : qmax(cv, x);
+    f[r] = s || cf;
+    cv = __shfl(v[r], 63, 64);
+    cf = __shfl((int)f[r], 63, 64);
+  }
+  if (lane == 0) {
+    w_v[wave] = cv;
+    w_f[wave] = cf;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    bool bf = false;
+    int64_t bv = kQMin;
+    for (uint32_t w = 0; w < NW; ++w) {
+      bv = w_f[w] ? w_v[w] : qmax(bv, w_v[w]);
+      bf = bf || w_f[w];
+    }
+    QState *me = qs + tile;
+    const uint32_t ep = epoch << kQEpochShift;
+    if (lane == 0 && (bf || tile > 0)) {  // a tile with a segment start knows its prefix already
+      __hip_atomic_store(&me->agg, (uint64_t)bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (bf) __hip_atomic_store(&me->inc, (uint64_t)bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&me->flag, ep | (bf ? kQAgg | kQInc : kQAgg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the open segment's max before the tile, unless its first item starts one
+    int64_t cin = kQMin;
+    if (tile > 0 && !__shfl((int)f[0], 0, 64)) {
+      int64_t top = (int64_t)tile - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t jt = top - (int64_t)lane;  // lane 0: the nearest tile
+        uint32_t fl = kQInc;                    // before tile 0: an empty prefix
+        if (jt >= 0) {
+          fl = __hip_atomic_load(&qs[jt].flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fl = (fl >> kQEpochShift) == epoch ? fl & (kQAgg | kQInc) : 0u;
+        }
+        const uint64_t m0 = __ballot(fl == 0), mi = __ballot((fl & kQInc) != 0);
+        const uint32_t fi = mi ? (uint32_t)__builtin_ctzll(mi) : 64u;
+        const uint64_t upto = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1);
+        if (m0 & upto) {  // a tile this one needs has not published yet
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 26)) break;  // never expected: tickets order the tiles
+          continue;
+        }
+        int64_t x = kQMin;
+        if (jt >= 0 && lane <= fi)
+          x = (int64_t)__hip_atomic_load(lane == fi ? &qs[jt].inc : &qs[jt].agg, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t d = 32; d > 0; d >>= 1) x = qmax(x, __shfl_xor(x, d, 64));
+        cin = qmax(cin, x);
+        if (fi < 64) break;
+        top -= 64;
+      }
+    }
+    if (lane == 0) {
+      if (!bf && tile > 0) {
+        __hip_atomic_store(&me->inc, (uint64_t)qmax(cin, bv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&me->flag, ep | kQAgg | kQInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_cin = cin;
+    }
+  }
+  __syncthreads();
+  int64_t c = s_cin;
+  for (uint32_t w = 0; w < wave; ++w) c = w_f[w] ? w_v[w] : qmax(c, w_v[w]);
+  // starts; the queue figures as k_qout sums them
+  const uint32_t hrow = k.quiet ? kNone : s_row;
+  uint32_t row = kNone;
+  unsigned long long n = 0, sw = 0, mw = 0, sh = 0;
+  auto flush = [&]() {
+    if (row == kNone || !n) return;
+    if (row == hrow) {
+      atomicAdd(&s_n, n);
+      if (sw) atomicAdd(&s_sw, sw);
+      if (mw) atomicMax(&s_mw, mw);
+      if (sh) atomicAdd(&s_sh, sh);
+      return;
+    }
+    unsigned long long *tr = k.table + (uint64_t)row * ISIM_DES_ROW_WORDS;
+    atomicAdd(tr + ISIM_DES_COUNT, n);
+    if (sw) atomicAdd(tr + ISIM_DES_SUM_WAIT, sw);
+    if (mw) atomicMax(tr + ISIM_DES_MAX_WAIT, mw);
+    if (sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, sh);
+  };
+#pragma unroll
+  for (uint32_t r = 0; r < IPT; ++r) {
+    const uint64_t j = w0 + r * 64 + lane;
+    if (j >= m) break;
+    const uint64_t S = (uint64_t)(f[r] ? v[r] : qmax(c, v[r])) + j * h[r];
+    const uint32_t i = P0 ? it[r] : sid[j];
+    store_tracked(k, k.IS + i, S, i);
+    if (k.quiet) continue;
+    const uint32_t rj = P0 ? rw[r] : rowk[j];
+    if (rj != row) {
+      flush();
+      row = rj;
+      n = sw = mw = sh = 0;
+    }
+    const uint64_t w = S - a[r];
+    n += 1;
+    sw += w;
+    mw = w > mw ? w : mw;
+    sh += h[r];
+  }
+  if (k.quiet) return;
+  flush();
+  __syncthreads();
+  if (threadIdx.x == 0 && s_n) {
+    unsigned long long *tr = k.table + (uint64_t)hrow * ISIM_DES_ROW_WORDS;
+    atomicAdd(tr + ISIM_DES_COUNT, s_n);
+    if (s_sw) atomicAdd(tr + ISIM_DES_SUM_WAIT, s_sw);
+    if (s_mw) atomicMax(tr + ISIM_DES_MAX_WAIT, s_mw);
+    if (s_sh) atomicAdd(tr + ISIM_DES_SUM_HOLD, s_sh);
+  }
+}
+
 // ---- 4c. finishes of one group (its items position by position): per
 // item the finish and its callee maximum into the caller's slot; the
 // statistics summed over a thread's run of one position (and one bucket for
@@ -1279,7 +1487,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 4, pl.cyclic ? M * 4 : 4, M * 4, 4, M * 4, M * 4,    // qk ord ids (spare) qids fids
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
-      4, 4, 16,                                                // (spare, spare); ovf: key overflow, no fixed
+      4, 4, 16,                                                // (k_qscan ticket, spare); ovf: key overflow, no fixed
                                                                // point, (unused), step-op count
       96,                                                      // two arrival-range slots; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
@@ -1322,7 +1530,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *rv_a = (uint32_t *)carve(parts[24]), *rv_b = (uint32_t *)carve(parts[25]);
   MP *mp_in = (MP *)carve(parts[26]), *mp_out = (MP *)carve(parts[27]);
   uint32_t *sid = (uint32_t *)carve(parts[28]);
-  (void)carve(parts[29]);
+  uint32_t *qticket = (uint32_t *)carve(parts[29]);  // k_qscan's tile tickets (its states: mp_out)
   (void)carve(parts[30]);
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
   uint64_t *mm = (uint64_t *)carve(parts[32]);
@@ -1350,6 +1558,14 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint16_t *ordc = (uint16_t *)carve(parts[51]);
   uint32_t *ifst = (uint32_t *)carve(parts[52]);
   k.ifst = pl.modeb ? ifst : nullptr;
+  // the rounds' queues by k_qscan (its keys a - j h need j h < 2^62), else
+  // rocPRIM's scan by key over the maps and k_qout (A/B: ISIM_DES_ITEMS_SCAN_BY_KEY)
+  uint64_t max_hold = 0;
+  for (uint64_t hv : row_hold) max_hold = std::max(max_hold, hv);
+  const bool qscan = std::getenv("ISIM_DES_ITEMS_SCAN_BY_KEY") == nullptr &&
+                     (max_hold == 0 || M <= (1ull << 62) / max_hold);
+  QState *qstate = (QState *)mp_out;  // mp_out's bytes: >= 32 B per 512 items
+  uint32_t qepoch = 0, qtbase = 0;
   int rc = 0;
   std::vector<uint32_t> qoff(R + 1), foff(G + 1);
   do {
@@ -1482,6 +1698,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     std::vector<uint64_t> rlo(R, ~0ull), rhi(R, 0);  // per sort round: its arrival range over the passes
     // A/B switch: every quiet pass recomputes every item
     const bool no_incr = std::getenv("ISIM_DES_ITEMS_NO_INCR") != nullptr;
+    // k_qscan's states (their epochs: 1, 2, ... per launch) and ticket
+    if (qscan && (hipMemsetAsync(qstate, 0, al256((M + 511) / 512 * sizeof(QState)), s) != hipSuccess ||
+                  hipMemsetAsync(qticket, 0, 4, s) != hipSuccess)) {
+      rc = fail("memset");
+      break;
+    }
     auto pass = [&](K &kk) {
     hipLaunchKernelGGL(k_acc_init, dim3(grid_for(M)), dim3(kT), 0, s, kk, pl.cyclic ? acc_b : nullptr, kk.acc);
     // items per lane of k_qout / k_fin: runs of one row / position summed
@@ -1535,8 +1757,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
                              (const uint32_t *)(qids + qoff[r]), rep_bits, rk_a, rk_b, mp_in, sid);
         } else if (nosort) {
-          hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b, mp_in,
-                             sid);
+          if (!qscan)  // k_qscan reads the list itself
+            hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b,
+                               mp_in, sid);
         } else if (!two_sorts && row_bits + rep_bits + ab <= 64) {
           hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, hmm[0], rep_bits, ab,
                              key_a, val_a);
@@ -1573,14 +1796,36 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           hipLaunchKernelGGL(k_pairs2, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, rk_b, rv_b, key_b, val_b, rep_bits,
                              rk_a, mp_in, sid);
         }
-        tb = tmp_bytes;
-        if (rocprim::inclusive_scan_by_key(tmp, tb, rk_a, mp_in, mp_out, (size_t)m, MPThen(),
-                                           rocprim::equal_to<uint32_t>(), s) != hipSuccess) {
-          rc = fail("queue scan");
-          break;
+        if (qscan) {
+          // 8 items per lane on a large round, 2 otherwise (more tiles to spread)
+          const bool big = m >= 2048ull * 512;
+          const uint32_t tiles = (uint32_t)((m + (big ? 2047 : 511)) / (big ? 2048 : 512));
+          if (qtbase > 0xFFFFFFFFu - tiles) {  // the ticket counter restarts
+            if (hipMemsetAsync(qticket, 0, 4, s) != hipSuccess) {
+              rc = fail("memset");
+              break;
+            }
+            qtbase = 0;
+          }
+          ++qepoch;
+          static void (*const qs_k[2][2])(K, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                                          const uint32_t *, const MP *, QState *, uint32_t *, uint32_t, uint32_t) = {
+              {k_qscan<2, false>, k_qscan<2, true>}, {k_qscan<8, false>, k_qscan<8, true>}};
+          const bool p0 = nosort && !chk;  // no k_pairs0: the round's list read directly
+          hipLaunchKernelGGL(qs_k[big][p0], dim3(tiles), dim3(kT), 0, s, kk, m, (const uint32_t *)(qids + qoff[r]),
+                             (const uint32_t *)rk_a, (const uint32_t *)rk_b, (const uint32_t *)sid,
+                             (const MP *)mp_in, qstate, qticket, qtbase, qepoch);
+          qtbase += tiles;
+        } else {
+          tb = tmp_bytes;
+          if (rocprim::inclusive_scan_by_key(tmp, tb, rk_a, mp_in, mp_out, (size_t)m, MPThen(),
+                                             rocprim::equal_to<uint32_t>(), s) != hipSuccess) {
+            rc = fail("queue scan");
+            break;
+          }
+          hipLaunchKernelGGL(k_qout, dim3(grid_for((m + span - 1) / span)), dim3(kT), 0, s, kk, m, rk_b, sid,
+                             mp_in, mp_out, span);
         }
-        hipLaunchKernelGGL(k_qout, dim3(grid_for((m + span - 1) / span)), dim3(kT), 0, s, kk, m, rk_b, sid,
-                           mp_in, mp_out, span);
       }
     finishes:
       for (uint32_t gi = pl.fin_round_off[r]; gi < pl.fin_round_off[r + 1]; ++gi) {
