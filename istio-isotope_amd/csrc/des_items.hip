@@ -49,6 +49,8 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 #include <rocprim/device/device_scan_by_key.hpp>
 
 #include "des.h"
@@ -373,12 +375,10 @@ __global__ void __launch_bounds__(kT) k_root500(K k) {
 // sort of the trace-ordered items by position) so that the passes, which
 // visit a position's items together (queues by service, finishes by
 // position), read the per-item arrays nearly in sequence
-__global__ void __launch_bounds__(kT) k_perm_keys(K k, uint32_t *key, uint32_t *val) {
-  for (uint64_t i = gid(); i < k.M; i += nthreads()) {
-    key[i] = k.erec[i].x;
-    val[i] = (uint32_t)i;
-  }
-}
+// (the sort reads its keys from the records: an item's position)
+struct PosOf {
+  __host__ __device__ uint32_t operator()(const uint4 &r) const { return r.x; }
+};
 // inv[old] = new
 __global__ void __launch_bounds__(kT) k_perm_inv(K k, const uint32_t *perm, uint32_t *inv) {
   for (uint64_t j = gid(); j < k.M; j += nthreads()) inv[perm[j]] = (uint32_t)j;
@@ -1473,7 +1473,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     (void)rocprim::radix_sort_pairs(nullptr, sop_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                     (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                     (size_t)(M * pl.item_bk), 0, 32);
-  const size_t tmp_bytes = std::max(std::max(std::max(sort32_bytes, sort64_bytes), sbk_bytes), sop_bytes);
+  size_t perm_bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, perm_bytes, rocprim::make_transform_iterator((const uint4 *)nullptr, PosOf()),
+                                  (uint32_t *)nullptr, rocprim::make_counting_iterator<uint32_t>(0u),
+                                  (uint32_t *)nullptr, (size_t)M, 0, 32);
+  const size_t tmp_bytes =
+      std::max({sort32_bytes, sort64_bytes, sbk_bytes, sop_bytes, perm_bytes});
   // per duration-table row: the service's worker hold (the queue kernels read no item's position)
   std::vector<uint64_t> row_hold(std::max<size_t>(1, max_row + 1), 0);
   for (const DesPos &q : pl.pos) row_hold[q.row] = q.hold;
@@ -1484,7 +1489,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 8 * k.aw, M * 8 * std::max<uint32_t>(1, k.bw),       // acc bk
       pl.cyclic ? M * 8 * k.aw : 8,                            // acc of the previous pass
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops: rounds, (item, step)
-      M * 4, pl.cyclic ? M * 4 : 4, M * 4, 4, M * 4, M * 4,    // qk ord ids (spare) qids fids
+      4, pl.cyclic ? M * 4 : 4, 4, 4, M * 4, M * 4,            // (spare) ord (spare spare) qids fids
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       4, 4, 16,                                                // (k_qscan ticket, spare); ovf: key overflow, no fixed
@@ -1519,9 +1524,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint64_t *acc_b = (uint64_t *)carve(parts[9]);
   uint32_t *op_k = (uint32_t *)carve(parts[10]);
   unsigned long long *op_v = (unsigned long long *)carve(parts[11]);
-  uint32_t *qk = (uint32_t *)carve(parts[12]);
+  (void)carve(parts[12]);
   uint32_t *ord = (uint32_t *)carve(parts[13]);  // per sort round: the last sorted order (list indices)
-  uint32_t *ids = (uint32_t *)carve(parts[14]);
+  (void)carve(parts[14]);
   (void)carve(parts[15]);
   uint32_t *qids = (uint32_t *)carve(parts[16]), *fids = (uint32_t *)carve(parts[17]);
   uint64_t *key_a = (uint64_t *)carve(parts[18]), *key_b = (uint64_t *)carve(parts[19]);
@@ -1581,10 +1586,11 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       break;
     }
     // 2b. renumber position-major: ipos = the sorted keys, the rest gathered
-    hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(M)), dim3(kT), 0, s, k, qk, ids);
+    // (keys read from the records, values counted: no key / index arrays)
     {
       size_t tb0 = tmp_bytes;
-      if (rocprim::radix_sort_pairs(tmp, tb0, qk, k.ipos, ids, qids, (size_t)M, 0,
+      if (rocprim::radix_sort_pairs(tmp, tb0, rocprim::make_transform_iterator((const uint4 *)k.erec, PosOf()),
+                                    k.ipos, rocprim::make_counting_iterator<uint32_t>(0u), qids, (size_t)M, 0,
                                     bits_for(std::max<size_t>(1, pl.pos.size()) - 1), s) != hipSuccess) {
         rc = fail("position sort");
         break;
