@@ -1872,7 +1872,15 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           break;
         }
         rep.passes = p + 2;  // the quiet passes so far and the recording pass
-        if (debug) std::fprintf(stderr, "isim des items: pass %u changed %u values\n", p + 1, changed[1]);
+        if (debug) {
+          // and the trace chunks the next pass recomputes
+          std::vector<uint8_t> ch(n_chunks);
+          uint64_t live_n = 0;
+          if (hipMemcpy(ch.data(), chg_a, n_chunks, hipMemcpyDeviceToHost) == hipSuccess)
+            for (uint8_t c : ch) live_n += c != 0;
+          std::fprintf(stderr, "isim des items: pass %u changed %u values, %llu of %llu trace chunks live\n", p + 1,
+                       changed[1], (unsigned long long)live_n, (unsigned long long)n_chunks);
+        }
         if (!changed[0]) break;
       }
       if (debug)
