@@ -336,3 +336,28 @@ def test_items_wide_tree(gpu, monkeypatch, name):
     monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
     DesCase(CASES[name](), 300_000).compare(1000, 3000)
     DesCase(MODE_B_CASES["seq_tree_abort"](), 300_000, error_mode=isim.MODE_B).compare(9, 2000)
+
+
+@pytest.mark.parametrize("case", ["c5p", "c4d", "mesh_heavy"])
+def test_items_qscan_equals_scan_by_key(gpu, monkeypatch, case):
+    """The one-pass queue kernel (k_qscan: a segmented prefix max of
+    a_i - i*h with a decoupled look-back across thousands of tiles) against
+    the independent path it replaced (rocPRIM's scan by key over max-plus
+    maps, then k_qout; ISIM_DES_ITEMS_SCAN_BY_KEY) at sizes where the rounds
+    span thousands of tiles and queue segments span many of them: records,
+    statistics and the DES table identical.  c5p at its bench batch and gap,
+    c4d at 2^21 of its bench gap (cyclic, kept orders), and the mesh under
+    heavy contention (waits far above the holds: long carries)."""
+    if case == "mesh_heavy":
+        d, n = DesCase(CASES["mesh_des"](), 20_000).d, 300_000
+    else:
+        c, n = _bench_case(case)
+        d, n = c.d, (n if case == "c5p" else 1 << 21)
+    got = d.serve(1 << 22, n, device=0)
+    monkeypatch.setenv("ISIM_DES_ITEMS_SCAN_BY_KEY", "1")
+    ref = d.serve(1 << 22, n, device=0)
+    assert np.array_equal(got[0], ref[0])
+    assert np.array_equal(np.asarray(got[1]), np.asarray(ref[1]))
+    assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))
+    rows = d.fold(got[2])
+    assert int(rows[:, native.DES_SUM_WAIT].sum()) > 0
