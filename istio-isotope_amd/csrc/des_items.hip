@@ -882,13 +882,85 @@ constexpr uint32_t kQAgg = 1, kQInc = 2, kQEpochShift = 2;
 constexpr int64_t kQMin = INT64_MIN;
 __device__ __forceinline__ int64_t qmax(int64_t a, int64_t b) { return a > b ? a : b; }
 
-// P0: a round that needs no sort (k_pairs0's order) read straight from its
-// list: the item, its position (the segment; a zero-hold item alone), row,
-// hold and arrival, instead of k_pairs0's arrays (segk, rowk, sid, mp unused)
-template <uint32_t IPT, bool P0>
-__global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *ids, const uint32_t *segk,
-                                              const uint32_t *rowk, const uint32_t *sid, const MP *mp, QState *qs,
-                                              uint32_t *ticket, uint32_t tbase, uint32_t epoch) {
+// Where a round's queue order comes from (the kernel reads it directly, so
+// no k_pairs* arrays are written and read back, except for kQArrays):
+//   kQArrays  k_pairs2's arrays (segment key, row, item, (hold, a + hold))
+//   kQList    a round that needs no sort: its list in (position, trace)
+//             order; segment = the position (a zero-hold item alone); the
+//             arrival computed here as k_qarr would (no k_qarr launched)
+//   kQKept    a cyclic schedule's kept order that still sorts the round
+//             (list indices; k_ordchk checked it)
+//   kQSorted  the round's sorted keys row | replica | arrival - amin with
+//             their list indices
+constexpr int kQArrays = 0, kQList = 1, kQKept = 2, kQSorted = 3;
+struct QSrc {
+  const uint32_t *list;  // the round's item list
+  const uint32_t *ord;   // kQKept
+  const uint64_t *key;   // kQSorted
+  const uint32_t *val;   // kQSorted
+  uint64_t amin;         // kQSorted
+  uint32_t rb, ab;       // replica bits; kQSorted: arrival bits
+  const uint32_t *segk, *rowk, *sid;  // kQArrays
+  const MP *mp;                       // kQArrays
+};
+
+// item j of the order: its segment key (hold-free: kQList treats zero holds
+// itself), and with FULL its item, row, hold and arrival
+template <int SRC, bool FULL>
+__device__ __forceinline__ uint64_t qitem(const K &k, const QSrc &q, uint64_t j, uint32_t &i, uint32_t &row,
+                                          uint64_t &h, uint64_t &a) {
+  uint64_t sk;
+  if constexpr (SRC == kQArrays) {
+    sk = q.segk[j];
+    if (FULL) {
+      i = q.sid[j];
+      row = q.rowk[j];
+      const MP p = q.mp[j];
+      h = p.B;
+      a = p.C - p.B;
+    }
+  } else if constexpr (SRC == kQSorted) {
+    const uint64_t kk = q.key[j];
+    sk = kk >> q.ab;
+    if (FULL) {
+      i = q.list[q.val[j]];
+      row = (uint32_t)(kk >> (q.ab + q.rb));
+      h = k.row_hold[row];
+      a = (kk & ((1ull << q.ab) - 1ull)) + q.amin;
+    }
+  } else {
+    i = q.list[SRC == kQKept ? q.ord[j] : (uint32_t)j];
+    const uint32_t v = k.ipos[i];
+    if (SRC == kQList) {
+      sk = v;
+    } else {
+      row = k.pos[v].row;
+      sk = ((uint64_t)row << q.rb) | k.irep[i];
+    }
+    if (FULL) {
+      const DesPos P = k.pos[v];
+      row = P.row;
+      h = k.row_hold[row];
+      if (SRC == kQKept || !live(k, i)) {
+        a = k.IA[i];  // (kQList: an item a quiet pass does not recompute keeps its own)
+      } else {
+        const uint32_t par = k.ipar[i];
+        if (par == kNone) {
+          a = k.A[k.itr[i]];
+        } else {
+          const uint32_t ks = k.ip[v].kstep;
+          a = (ks == 0 ? k.IS[par] : k.bk[(uint64_t)par * k.bw + ks]) + P.off;
+        }
+        k.IA[i] = a;
+      }
+    }
+  }
+  return sk;
+}
+
+template <uint32_t IPT, int SRC>
+__global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, QSrc q, QState *qs, uint32_t *ticket, uint32_t tbase,
+                                              uint32_t epoch) {
   constexpr uint32_t NW = kT / 64;
   __shared__ uint32_t s_tile, s_row;
   __shared__ int64_t w_v[NW], s_cin;
@@ -898,7 +970,9 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *i
     const uint32_t t = atomicAdd(ticket, 1u) - tbase;
     s_tile = t;
     const uint64_t j0 = (uint64_t)t * kT * IPT;
-    s_row = P0 ? k.pos[k.ipos[ids[j0]]].row : rowk[j0];
+    if constexpr (SRC == kQArrays) s_row = q.rowk[j0];
+    else if constexpr (SRC == kQSorted) s_row = (uint32_t)(q.key[j0] >> (q.ab + q.rb));
+    else s_row = k.pos[k.ipos[q.list[SRC == kQKept ? q.ord[j0] : (uint32_t)j0]]].row;
     s_n = s_sw = s_mw = s_sh = 0;
   }
   __syncthreads();
@@ -910,7 +984,7 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *i
   int64_t v[IPT];
   bool f[IPT];
   uint64_t a[IPT], h[IPT];
-  uint32_t it[IPT], rw[IPT];  // P0: the item and its row
+  uint32_t it[IPT], rw[IPT];
   bool cf = false;
   int64_t cv = kQMin;
 #pragma unroll
@@ -919,28 +993,21 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *i
     bool s = false;
     int64_t x = kQMin;
     a[r] = h[r] = 0;
-    if constexpr (P0) {
-      // the previous item's position: the lane below's, lane 0 reads it
-      uint32_t pv = kNone, vv = kNone;
-      if (j < m) {
-        it[r] = ids[j];
-        vv = k.ipos[it[r]];
-        rw[r] = k.pos[vv].row;
-        h[r] = k.row_hold[rw[r]];
-        a[r] = k.IA[it[r]];
-        if (lane == 0 && j > 0) pv = k.ipos[ids[j - 1]];
+    it[r] = rw[r] = 0;
+    // the previous item's segment: the lane below's, lane 0 reads it
+    uint64_t sk = ~0ull, ps = ~0ull;
+    if (j < m) {
+      sk = qitem<SRC, true>(k, q, j, it[r], rw[r], h[r], a[r]);
+      if (lane == 0 && j > 0) {
+        uint32_t i1, r1;
+        uint64_t h1, a1;
+        ps = qitem<SRC, false>(k, q, j - 1, i1, r1, h1, a1);
       }
-      const uint32_t up = __shfl_up(vv, 1, 64);
-      if (lane > 0) pv = up;
-      if (j < m) {
-        s = j == 0 || h[r] == 0 || pv != vv;
-        x = (int64_t)(a[r] - j * h[r]);
-      }
-    } else if (j < m) {
-      s = j == 0 || segk[j - 1] != segk[j];
-      const MP p = mp[j];
-      h[r] = p.B;
-      a[r] = p.C - p.B;
+    }
+    const uint64_t up = __shfl_up(sk, 1, 64);
+    if (lane > 0) ps = up;
+    if (j < m) {
+      s = j == 0 || ps != sk || (SRC == kQList && h[r] == 0);
       x = (int64_t)(a[r] - j * h[r]);
     }
 #pragma unroll
@@ -1043,10 +1110,10 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, const uint32_t *i
     const uint64_t j = w0 + r * 64 + lane;
     if (j >= m) break;
     const uint64_t S = (uint64_t)(f[r] ? v[r] : qmax(c, v[r])) + j * h[r];
-    const uint32_t i = P0 ? it[r] : sid[j];
+    const uint32_t i = it[r];
     store_tracked(k, k.IS + i, S, i);
     if (k.quiet) continue;
-    const uint32_t rj = P0 ? rw[r] : rowk[j];
+    const uint32_t rj = rw[r];
     if (rj != row) {
       flush();
       row = rj;
@@ -1722,11 +1789,14 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
                            (uint64_t)(soff[r + 1] - soff[r]));
       const uint64_t m = qoff[r + 1] - qoff[r];
       if (m) {
-        uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
-        ++qn;
-        hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m,
-                           (unsigned long long *)slot, (unsigned long long *)slot_next, ordbad);
         const bool nosort = pl.round_nosort[r] && !two_sorts;
+        // (a no-sort round reads no arrival range back; k_qscan computes its arrivals)
+        uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
+        if (!(nosort && qscan)) {
+          ++qn;
+          hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m,
+                             (unsigned long long *)slot, (unsigned long long *)slot_next, ordbad);
+        }
         const bool chk = !nosort && have_ord[r];
         if (chk)
           hipLaunchKernelGGL(k_ordchk, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
@@ -1758,11 +1828,17 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         }
         const uint32_t ab = bits_for(hmm[1] - hmm[0]);
         tb = tmp_bytes;
+        // k_qscan's source of the round's order (k_pairs* only for the two-sort path)
+        QSrc qsrc{qids + qoff[r], ord + qoff[r], key_b, val_b, hmm[0], rep_bits, ab, rk_a, rk_b, sid, mp_in};
+        int qsk = kQArrays;
         if (chk && !bad) {  // the kept order holds: no sort
           ++reused;
-          hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
-                             (const uint32_t *)(qids + qoff[r]), rep_bits, rk_a, rk_b, mp_in, sid);
+          qsk = kQKept;
+          if (!qscan)
+            hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
+                               (const uint32_t *)(qids + qoff[r]), rep_bits, rk_a, rk_b, mp_in, sid);
         } else if (nosort) {
+          qsk = kQList;
           if (!qscan)  // k_qscan reads the list itself
             hipLaunchKernelGGL(k_pairs0, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, rk_a, rk_b,
                                mp_in, sid);
@@ -1781,8 +1857,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
                                (const uint32_t *)(qids + qoff[r]), m, ord + qoff[r], ordc + qoff[r]);
             have_ord[r] = 1;
           }
-          hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b,
-                             (const uint32_t *)(qids + qoff[r]), rep_bits, ab, hmm[0], rk_a, rk_b, mp_in, sid);
+          qsk = kQSorted;
+          if (!qscan)
+            hipLaunchKernelGGL(k_pairs1, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, key_b, val_b,
+                               (const uint32_t *)(qids + qoff[r]), rep_bits, ab, hmm[0], rk_a, rk_b, mp_in, sid);
         } else {
           hipLaunchKernelGGL(k_qkey2, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, hmm[0], rep_bits,
                              key_a, val_a, ovf);
@@ -1814,13 +1892,11 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
             qtbase = 0;
           }
           ++qepoch;
-          static void (*const qs_k[2][2])(K, uint64_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                                          const uint32_t *, const MP *, QState *, uint32_t *, uint32_t, uint32_t) = {
-              {k_qscan<2, false>, k_qscan<2, true>}, {k_qscan<8, false>, k_qscan<8, true>}};
-          const bool p0 = nosort && !chk;  // no k_pairs0: the round's list read directly
-          hipLaunchKernelGGL(qs_k[big][p0], dim3(tiles), dim3(kT), 0, s, kk, m, (const uint32_t *)(qids + qoff[r]),
-                             (const uint32_t *)rk_a, (const uint32_t *)rk_b, (const uint32_t *)sid,
-                             (const MP *)mp_in, qstate, qticket, qtbase, qepoch);
+          static void (*const qs_k[2][4])(K, uint64_t, QSrc, QState *, uint32_t *, uint32_t, uint32_t) = {
+              {k_qscan<2, kQArrays>, k_qscan<2, kQList>, k_qscan<2, kQKept>, k_qscan<2, kQSorted>},
+              {k_qscan<8, kQArrays>, k_qscan<8, kQList>, k_qscan<8, kQKept>, k_qscan<8, kQSorted>}};
+          hipLaunchKernelGGL(qs_k[big][qsk], dim3(tiles), dim3(kT), 0, s, kk, m, qsrc, qstate, qticket, qtbase,
+                             qepoch);
           qtbase += tiles;
         } else {
           tb = tmp_bytes;
