@@ -375,10 +375,6 @@ __global__ void __launch_bounds__(kT) k_root500(K k) {
 // sort of the trace-ordered items by position) so that the passes, which
 // visit a position's items together (queues by service, finishes by
 // position), read the per-item arrays nearly in sequence
-// an alternative configuration of the rounds' one-key sorts (A/B): onesweep
-// at every size (the default merge-sorts up to 2^20 items)
-using QSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                            rocprim::default_config, 0>;
 // (the sort reads its keys from the records: an item's position)
 struct PosOf {
   __host__ __device__ uint32_t operator()(const uint4 &r) const { return r.x; }
@@ -1584,17 +1580,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     (void)rocprim::radix_sort_pairs(nullptr, sop_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                     (const unsigned long long *)nullptr, (unsigned long long *)nullptr,
                                     (size_t)(M * pl.item_bk), 0, 32);
-  size_t qcfg_bytes = 0;
-  (void)rocprim::radix_sort_pairs<QSortCfg>(nullptr, qcfg_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                            (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)M, 0, 64);
-  // A/B: the rounds' one-key sorts with QSortCfg (ISIM_DES_ITEMS_SORT_CFG)
-  const bool qsort_cfg = std::getenv("ISIM_DES_ITEMS_SORT_CFG") != nullptr;
   size_t perm_bytes = 0;
   (void)rocprim::radix_sort_pairs(nullptr, perm_bytes, rocprim::make_transform_iterator((const uint4 *)nullptr, PosOf()),
                                   (uint32_t *)nullptr, rocprim::make_counting_iterator<uint32_t>(0u),
                                   (uint32_t *)nullptr, (size_t)M, 0, 32);
   const size_t tmp_bytes =
-      std::max({sort32_bytes, sort64_bytes, sbk_bytes, sop_bytes, perm_bytes, qcfg_bytes});
+      std::max({sort32_bytes, sort64_bytes, sbk_bytes, sop_bytes, perm_bytes});
   // per duration-table row: the service's worker hold (the queue kernels read no item's position)
   std::vector<uint64_t> row_hold(std::max<size_t>(1, max_row + 1), 0);
   for (const DesPos &q : pl.pos) row_hold[q.row] = q.hold;
@@ -1895,10 +1886,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         } else if (!two_sorts && row_bits + rep_bits + ab <= 64) {
           hipLaunchKernelGGL(k_qkey1, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m, hmm[0], rep_bits, ab,
                              key_a, val_a);
-          if ((qsort_cfg ? rocprim::radix_sort_pairs<QSortCfg>(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0,
-                                                                row_bits + rep_bits + ab, s)
-                         : rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0,
-                                                     row_bits + rep_bits + ab, s)) != hipSuccess) {
+          if (rocprim::radix_sort_pairs(tmp, tb, key_a, key_b, val_a, val_b, (size_t)m, 0, row_bits + rep_bits + ab,
+                                        s) != hipSuccess) {
             rc = fail("queue sort");
             break;
           }
