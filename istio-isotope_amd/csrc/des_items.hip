@@ -544,7 +544,7 @@ struct MPThen {
 // round's arrival range (mm[0..1]: one 64-bit atomic min / max per
 // workgroup); in a quiet pass of a cyclic schedule mm[2] flags an arrival
 // that differs from the previous pass's (none: the round's queues are as
-// they were and the pass skips them); mm[3]: k_qarr_ord's flag.  The words
+// they were and the pass skips them); mm[3]: k_ordchk's flag.  The words
 // alternate between two slots by launch; this launch empties the other slot
 // for the next one.
 // an item's arrival: its trace's, or its caller's start / step begin + off
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(kT) k_reps(K k) {
 // ONE sort key when the bits fit: row | replica | arrival - amin (equal keys
 // are put in (trace, hop) order afterwards: k_tiefix)
 // (the value is the list index j: a cyclic schedule keeps each round's sorted
-// order for the next pass, k_qarr_ord)
+// order for the next pass, k_ordchk)
 __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t m, uint64_t amin, uint32_t rb,
                                               uint32_t ab, uint64_t *key, uint32_t *val) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(kT) k_qkey1(K k, const uint32_t *ids, uint64_t
 // pass's (row, replica, arrival): when (row, replica, arrival, j) strictly
 // increases along it, it IS the stable sort of the round's queue keys, and
 // the sort is skipped (k_qscan reads it); any inversion raises mm[3]
-// (k_qarr_ord) and the host sorts (des_items_launch)
+// (k_ordchk) and the host sorts (des_items_launch)
 // the oracle's tie order of equal (row, replica, arrival): (trace, hop) —
 // the event heap pops the earlier trace first (des_oracle.c).  The rounds'
 // lists are position-major, so a stable sort alone would break such ties by
@@ -673,61 +673,30 @@ __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_
     }
   }
 }
-// k_qarr and the kept order's check in one pass over a round with a kept order: the
-// arrivals of the items in that order (each item once: the order is a
-// permutation of the round's list), the range and change flag as k_qarr,
-// and the order's check against the new arrivals — the previous
-// item's tuple from the lane below (lane 0 computes it), its flag in mm[3]
-// (this slot's, emptied by the launch before: no clear racing the sets)
-__global__ void __launch_bounds__(kT) k_qarr_ord(K k, const uint32_t *ids, const uint32_t *ord, const uint16_t *ordc,
-                                                 uint64_t m, unsigned long long *mm, unsigned long long *mm_next) {
-  qarr_reset(mm_next);
-  unsigned long long lo = ~0ull, hi = 0;
-  const uint32_t lane = threadIdx.x & 63u;
-  bool inv = false;
-  auto tuple = [&](uint64_t jj, uint32_t &i, uint64_t &h, uint64_t &a, bool own) {
-    i = ids[ord[jj]];
-    const uint32_t v = k.ipos[i];
-    const DesPos P = k.pos[v];
-    h = ((uint64_t)P.row << 32) | k.irep[i];
-    if (!live(k, i)) {
-      a = k.IA[i];  // the previous pass's (the host keeps the round's range)
-      return;
-    }
-    a = item_arrival(k, i, v, P.off);
-    if (own) {
-      if (k.changed) qarr_changed(k, k.IA[i] != a, mm);
-      k.IA[i] = a;
-      lo = a < lo ? a : lo;
-      hi = a > hi ? a : hi;
-    }
+// the kept order against this pass's arrivals (k_qarr's, in list order):
+// any inversion raises mm[3] (this slot's, emptied by the launch before)
+__global__ void __launch_bounds__(kT) k_ordchk(K k, const uint32_t *ids, const uint32_t *ord, const uint16_t *ordc,
+                                               uint64_t m, unsigned long long *mm) {
+  auto tuple = [&](uint32_t i, uint64_t &h, uint64_t &a) {
+    h = ((uint64_t)k.pos[k.ipos[i]].row << 32) | k.irep[i];
+    a = k.IA[i];
   };
-  for (uint64_t j0 = gid() - lane; j0 < m; j0 += nthreads()) {  // whole waves: the lane below's tuple
-    const uint64_t jj = j0 + lane;
-    uint32_t i = 0, ip = 0;
-    uint64_t h = 0, a = 0, hp = 0, ap = 0;
-    if (jj < m) tuple(jj, i, h, a, true);
-    const uint32_t ui = __shfl_up(i, 1, 64);
-    const uint64_t uh = __shfl_up(h, 1, 64), ua = __shfl_up(a, 1, 64);
-    if (jj < m && jj > 0) {
-      if (lane == 0) {
-        tuple(jj - 1, ip, hp, ap, false);
-      } else {
-        ip = ui;
-        hp = uh;
-        ap = ua;
-      }
-      // a pair of items neither of which this pass recomputes kept its keys:
-      // its order stands (ordc: their trace chunks, stored with the order)
-      if (!k.dcur || k.dcur[ordc[jj]] || k.dcur[ordc[jj - 1]])
-        inv = inv || hp > h || (hp == h && (ap > a || (ap == a && tie_key(k, ip) > tie_key(k, i))));
+  for (uint64_t jj = gid(); jj < m; jj += nthreads()) {
+    bool inv = false;
+    // a pair of items neither of which this pass recomputes kept its keys:
+    // its order stands (ordc: their trace chunks, stored with the order)
+    if (jj > 0 && (!k.dcur || k.dcur[ordc[jj]] || k.dcur[ordc[jj - 1]])) {
+      const uint32_t i = ids[ord[jj]], ip = ids[ord[jj - 1]];
+      uint64_t h, a, hp, ap;
+      tuple(i, h, a);
+      tuple(ip, hp, ap);
+      inv = hp > h || (hp == h && (ap > a || (ap == a && tie_key(k, ip) > tie_key(k, i))));
     }
+    const unsigned long long bm = __ballot(inv);
+    if (bm && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)bm) - 1u &&
+        __hip_atomic_load(mm + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull)
+      atomicOr(mm + 3, 1ull);
   }
-  const unsigned long long bm = __ballot(inv);
-  if (bm && lane == (uint32_t)__ffsll((long long)bm) - 1u &&
-      __hip_atomic_load(mm + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull)
-    atomicOr(mm + 3, 1ull);
-  qarr_range(lo, hi, mm);
 }
 
 // a sort round's order kept for the next pass: the list indices and the
@@ -929,7 +898,7 @@ __device__ __forceinline__ int64_t qmax(int64_t a, int64_t b) { return a > b ? a
 //             order; segment = the position (a zero-hold item alone); the
 //             arrival computed here as k_qarr would (no k_qarr launched)
 //   kQKept    a cyclic schedule's kept order that still sorts the round
-//             (list indices; k_qarr_ord checked it)
+//             (list indices; k_ordchk checked it)
 //   kQSorted  the round's sorted keys row | replica | arrival - amin with
 //             their list indices
 constexpr int kQArrays = 0, kQList = 1, kQKept = 2, kQSorted = 3;
@@ -984,13 +953,7 @@ __device__ __forceinline__ uint64_t qitem(const K &k, const QSrc &q, uint64_t j,
       if (SRC == kQKept || !live(k, i)) {
         a = k.IA[i];  // (kQList: an item a quiet pass does not recompute keeps its own)
       } else {
-        const uint32_t par = k.ipar[i];
-        if (par == kNone) {
-          a = k.A[k.itr[i]];
-        } else {
-          const uint32_t ks = k.ip[v].kstep;
-          a = (ks == 0 ? k.IS[par] : k.bk[(uint64_t)par * k.bw + ks]) + P.off;
-        }
+        a = item_arrival(k, i, v, P.off);
         k.IA[i] = a;
       }
     }
@@ -1832,22 +1795,21 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         // (a no-sort round reads no arrival range back; k_qscan computes its arrivals)
         uint64_t *slot = mm + 4 * (qn & 1u), *slot_next = mm + 4 * ((qn + 1) & 1u);
         const bool chk = !nosort && have_ord[r];
-        if (chk) {  // arrivals and the kept order's check in one pass
-          ++qn;
-          hipLaunchKernelGGL(k_qarr_ord, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
-                             (const uint32_t *)(ord + qoff[r]), (const uint16_t *)(ordc + qoff[r]), m,
-                             (unsigned long long *)slot, (unsigned long long *)slot_next);
-        } else if (!(nosort && qscan)) {
+        if (!(nosort && qscan)) {
           ++qn;
           hipLaunchKernelGGL(k_qarr, dim3(grid_for(m)), dim3(kT), 0, s, kk, qids + qoff[r], m,
                              (unsigned long long *)slot, (unsigned long long *)slot_next);
+          if (chk)  // (its flag in the same slot: one read-back)
+            hipLaunchKernelGGL(k_ordchk, dim3(grid_for(m)), dim3(kT), 0, s, kk, (const uint32_t *)(qids + qoff[r]),
+                               (const uint32_t *)(ord + qoff[r]), (const uint16_t *)(ordc + qoff[r]), m,
+                               (unsigned long long *)slot);
         }
         // a quiet pass after the first: a round whose arrivals all equal the
         // previous pass's keeps its starts (its queues are skipped)
         // (sort rounds only: they read the range back anyway; a sort-free
         // round would pay a stream synchronisation for the check)
         const bool may_skip = kk.quiet && !kk.first && !nosort && !no_skip;
-        // range, change flag, kept-order flag (k_qarr_ord)
+        // range, change flag, kept-order flag (k_ordchk)
         uint64_t hmm[4] = {0, 0, 1, 1};
         if ((!nosort || may_skip) &&
             (hipMemcpyAsync(hmm, slot, 32, hipMemcpyDeviceToHost, s) != hipSuccess || sync_s() != hipSuccess)) {
