@@ -227,23 +227,23 @@ struct CountSink {
   template <typename TT>
   __device__ __forceinline__ void resp(uint32_t, uint32_t, TT, bool) {}
 };
-// records of the current trace go to rec[base + hop]
+// records of the current trace go to rec[base + hop], each written once,
+// whole, when its invocation closes (tree_walk.h close_rec): position, its
+// duration without contention (a lower bound is all k_relmax needs: u64
+// durations saturate at 2^32 - 1; the entry's is 0), caller hop, trace and
+// in mode B the response status in bit 31 (mode A draws the own errors
+// afterwards, k_own).  Before: the record at the open and the duration and
+// status at the close — two scattered stores per item.
 template <bool MB>
 struct EmitSink : CountSink {
+  static constexpr bool kCloseRec = true;
   uint4 *rec;
   uint64_t base;
   uint32_t t;
-  __device__ __forceinline__ void exec(uint32_t p, uint32_t hop, uint32_t caller, bool own) {
-    rec[base + hop] = uint4{p, 0u, caller == tw::kNoCaller ? kNone : caller, t | (own ? 0x80000000u : 0u)};
-  }
-  // (a lower bound is all k_relmax needs: u64 durations saturate at 2^32 - 1)
-  // mode B: the response status (a failed step, or the own error) into bit
-  // 31 of w; mode A draws the own errors afterwards (k_own)
   template <typename TT>
-  __device__ __forceinline__ void dur(uint32_t hop, TT T, bool st) {
-    const uint64_t i = base + hop;
-    rec[i].y = (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T;
-    if (MB && st) rec[i].w |= 0x80000000u;
+  __device__ __forceinline__ void rec_close(uint32_t p, uint32_t hop, uint32_t caller, TT T, bool st) {
+    rec[base + hop] = uint4{p, (uint64_t)T > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)T,
+                            caller == tw::kNoCaller ? kNone : caller, t | (MB && st ? 0x80000000u : 0u)};
   }
 };
 
@@ -285,9 +285,6 @@ __device__ __forceinline__ void prewalk_body(const K &k, unsigned long long *wor
   while (true) {
     if (active && L.done) {
       if constexpr (!EMIT) k.cnt[t] = L.hops();
-      if constexpr (EMIT && MB) {  // the entry's status (its response ends the walk: no dur call)
-        if (L.root500) s.rec[s.base].w |= 0x80000000u;
-      }
       active = false;
     }
     unsigned long long idle = __ballot(!active);

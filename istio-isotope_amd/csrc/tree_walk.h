@@ -166,6 +166,17 @@ template <class S>
 struct has_exec<S, decltype((void)&S::exec)> {
   static constexpr bool value = true;
 };
+// or (a sink with kCloseRec) ONE rec_close(position, hop, caller hop,
+// duration, status) per executed invocation when it closes — a leaf at its
+// visit, the entry with duration 0 — so a record is written once, whole
+template <class S, class = void>
+struct close_rec {
+  static constexpr bool value = false;
+};
+template <class S>
+struct close_rec<S, decltype((void)S::kCloseRec)> {
+  static constexpr bool value = S::kCloseRec;
+};
 //
 // One step() is a MACRO step: close the current invocation if the walk has
 // passed its subtree, then process position p (a call: skip it, run a leaf
@@ -408,13 +419,16 @@ TW_PRAGMA_UNROLL
       done = true;
       lat = T;
       root500 = st;
+      if constexpr (close_rec<Sink>::value) sink.rec_close(0u, cur_hop(), kNoCaller, (TT)0, st);
       return false;
     }
     sink.resp(nodes.load(f_pos).site(), x.row, T, st);
     if constexpr (has_exec<Sink>::value) sink.dur(cur_hop(), T, st);
     const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
+    const uint32_t cpos = f_pos, chop = cur_hop();
     pop();
+    if constexpr (close_rec<Sink>::value) sink.rec_close(cpos, chop, cur_hop(), T, st);
     fold(c, st, cc);
     return true;
   }
@@ -449,6 +463,8 @@ TW_PRAGMA_UNROLL
       const bool own = own_error(hop, fl, x.thr, k0, k1);
       add_err(own);
       if constexpr (has_exec<Sink>::value) sink.exec(p, hop, entry ? kNoCaller : cur_hop(), own);
+      if constexpr (close_rec<Sink>::value)
+        sink.rec_close(p, hop, entry ? kNoCaller : cur_hop(), entry ? (TT)0 : (TT)x.tc, own);
       if (entry) {
         done = true;
         lat = x.tc;
