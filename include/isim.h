@@ -115,9 +115,12 @@ typedef struct {
 #define ISIM_ST_N_500 4
 #define ISIM_ST_NOT_MIN_LATENCY 5 /* ~min latency (so min and max both merge with MAX) */
 #define ISIM_ST_MAX_LATENCY 6
-#define ISIM_ST_DES_RETRY 7       /* DES batches NOT accumulated: a latency reached 2^31 ns in 32-bit rows
-                                     (rerun them with ISIM_DES_FLAG_WIDE; isim_serve_des does), or a cyclic
-                                     schedule found no fixed point within 256 passes */
+#define ISIM_ST_DES_RETRY 7       /* DES batches NOT accumulated: low 32 bits, a latency reached 2^31 ns in
+                                     32-bit rows (rerun them with ISIM_DES_FLAG_WIDE; isim_serve_des does), or
+                                     a cyclic schedule found no fixed point within 256 passes; high 32 bits,
+                                     batches FAILED by a device fault (a queue pass's decoupled look-back gave
+                                     up waiting for an earlier tile: an error, never retried — isim_serve_des
+                                     and the item engine return ISIM_EHIP) */
 #define ISIM_ST_PROM 8            /* [2][33] latency histogram, Prometheus duration buckets
                                      (prometheus/handler.go:26-31), index [status500][bucket] */
 #define ISIM_N_PROM 33
@@ -269,10 +272,13 @@ ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32
  * of one handler may be in flight on one device at once (launches on ONE
  * stream are ordered and never collide; with more than 256 streams in
  * flight, order them with events or use one handler per stream).  A lane tree
- * walk deeper than 16 calling invocations spills frames to one of 4 areas per
- * (handler, device): each such launch waits for the previous launch that used
- * its area (an event recorded after every spilling launch), so launches on
- * different streams never share frames. */
+ * walk deeper than its register frames (16 calling invocations on narrow
+ * trees, fewer on wide ones) spills frames to one of up to 4 areas per
+ * (handler, device), each allocated when a stream first needs it: each such
+ * launch waits for the previous launch that used its area (an event recorded
+ * after every spilling launch), so launches on different streams never share
+ * frames.  A spilling walk cannot be graph-captured: on a capturing stream it
+ * returns ISIM_EINVAL. */
 ISIM_API int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces,
                       isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
 
@@ -370,6 +376,12 @@ ISIM_API int isim_serve_des(isim_handler *h, int device, const isim_des_params *
                    uint64_t n_traces, isim_trace_rec *h_records, uint64_t *h_stats, uint64_t *h_des_table);
 /* DES table rows -> svc_rows[n_services][ISIM_DES_ROW_WORDS] (zero for unreachable services). */
 ISIM_API int isim_des_fold(const isim_handler *h, const uint64_t *des_table, uint64_t *svc_rows);
+/* Test hook (no reference counterpart): the polls a DES queue pass's decoupled
+ * look-back makes for an earlier tile before it fails the batch (device
+ * fault flag; default 2^26, never reached in practice).  0 makes every
+ * look-back fail at once, so tests can drive the error path.  Process-wide; read at each DES launch. */
+ISIM_API void isim_debug_set_spin_limit(uint32_t polls);
+ISIM_API uint32_t isim_debug_spin_limit(void);
 
 /* ---- multi-device: trace shards + one RCCL all-reduce ----
  * north_star: traces shard evenly across the GPUs of a node; the histograms

@@ -84,7 +84,10 @@ struct DevState {
   uint32_t *d_sum_row = nullptr;        // kind 7: per LDS sum index, its row
   uint32_t *d_slot_tc = nullptr;        // kind 7: per slot, the leaf callee's latency
   uint32_t *d_lds_slot = nullptr;       // kind 7, wide tree: per LDS counter its slot
-  uint32_t *d_spill = nullptr;          // kind 7: frames below the register stack, kSpillAreas areas
+  // kind 7: frames below the register stack, up to kSpillAreas areas (the
+  // first allocated with the program, the others when a further stream first
+  // needs one)
+  uint32_t *d_spill[isim::kSpillAreas] = {};
   uint32_t spill_lanes = 0;
   size_t spill_words = 0;               // u32 words of one area
   hipEvent_t spill_ev[isim::kSpillAreas] = {};     // recorded after each area's latest launch
@@ -92,21 +95,38 @@ struct DevState {
   bool spill_used[isim::kSpillAreas] = {};
   uint32_t spill_next = 0;
   hipMemPool_t des_pool = nullptr;      // the item engine's per-batch arrays (a private pool)
+  bool des_ready = false;               // every DES upload above succeeded (des_prepare)
 };
 
+// the DES plan's device copies (des_prepare), freed together; the pool only
+// after the device has drained the hipFreeAsync calls queued on user streams
+void free_des(DevState &d) {
+  for (void **q : {&d.d_des_pos, (void **)&d.d_des_child, (void **)&d.d_des_level, (void **)&d.d_des_arr,
+                   &d.d_des_ext, &d.d_des_steps, (void **)&d.d_des_mult, (void **)&d.d_des_fast,
+                   (void **)&d.d_des_sort, (void **)&d.d_des_zero, (void **)&d.d_des_pipe, &d.d_des_ipos,
+                   (void **)&d.d_des_sround, &d.d_des_nodes, &d.d_des_text, &d.d_des_tstep}) {
+    if (*q) (void)hipFree(*q);
+    *q = nullptr;
+  }
+  if (d.des_pool) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemPoolDestroy(d.des_pool);
+    d.des_pool = nullptr;
+  }
+  d.des_ready = false;
+}
+
 void free_dev(DevState &d) {
+  free_des(d);
   for (void *q : {(void *)d.d_prog, (void *)d.d_mult, (void *)d.d_closes, (void *)d.d_close_end,
                   (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_stage, (void *)d.d_const_stats,
-                  d.d_des_pos, (void *)d.d_des_child, (void *)d.d_des_level, (void *)d.d_des_mult,
-                  (void *)d.d_des_fast, (void *)d.d_des_zero, (void *)d.d_des_sort, (void *)d.d_des_arr,
-                  (void *)d.d_des_pipe,
-                  d.d_des_ext, d.d_des_steps, d.d_des_ipos, d.d_des_nodes, d.d_des_text, d.d_des_tstep,
-                  (void *)d.d_des_sround, (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
-                  (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_spill, (void *)d.d_lds_slot})
+                  (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
+                  (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_lds_slot})
+    if (q) (void)hipFree(q);
+  for (uint32_t *q : d.d_spill)
     if (q) (void)hipFree(q);
   for (hipEvent_t e : d.spill_ev)
     if (e) (void)hipEventDestroy(e);
-  if (d.des_pool) (void)hipMemPoolDestroy(d.des_pool);
   d = DevState();
 }
 
@@ -382,7 +402,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
                        ((p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) +
                         (p.tree_wide ? isim::kTreeSpillWide : 0u)) *
                        st.spill_lanes;
-      HIPCHK(hipMalloc(&st.d_spill, st.spill_words * isim::kSpillAreas * sizeof(uint32_t)));
+      HIPCHK(hipMalloc(&st.d_spill[0], st.spill_words * sizeof(uint32_t)));
       for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
   }
@@ -651,23 +671,26 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
-  if (st->d_spill) {
+  if (st->d_spill[0]) {
     // a spilling walk: the area its stream used last (else the next one,
-    // round robin), ordered after the area's previous launch by an event; the
-    // wait, launch and record are one step under the handler's lock.  A
-    // capturing stream that used the area last skips the wait (its own order
-    // covers it, and a capture may not wait on work from outside it).
+    // round robin; allocated on first use), ordered after the area's previous
+    // launch by an event; the wait, launch and record are one step under the
+    // handler's lock.  Not graph-capturable: a captured launch
+    // would keep its area in the graph, and nothing could order its replays
+    // against the eager launches that later take the same area.
     const hipStream_t hs = (hipStream_t)hip_stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(hs, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return fail(ISIM_EINVAL, "a lane tree walk that spills frames (more nested calling invocations than its "
+                               "register frames) cannot be captured into a HIP graph");
     std::lock_guard<std::mutex> lk(h->spill_mu);
     uint32_t a = isim::kSpillAreas;
     for (uint32_t i = 0; i < isim::kSpillAreas; ++i)
       if (st->spill_used[i] && st->spill_last[i] == hs) a = i;
     if (a == isim::kSpillAreas) a = st->spill_next++ % isim::kSpillAreas;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(hs, &cs);
-    if (st->spill_used[a] && !(cs == hipStreamCaptureStatusActive && st->spill_last[a] == hs))
-      HIPCHK(hipStreamWaitEvent(hs, st->spill_ev[a], 0));
-    kp.spill = st->d_spill + a * st->spill_words;
+    if (!st->d_spill[a]) HIPCHK(hipMalloc(&st->d_spill[a], st->spill_words * sizeof(uint32_t)));
+    if (st->spill_used[a]) HIPCHK(hipStreamWaitEvent(hs, st->spill_ev[a], 0));
+    kp.spill = st->d_spill[a];
     HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, hs));
     HIPCHK(hipEventRecord(st->spill_ev[a], hs));
     st->spill_last[a] = hs;
@@ -855,7 +878,8 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
   rc = prepare_device(h, device, st);
   if (rc != ISIM_OK) return rc;
   std::lock_guard<std::mutex> lk(h->mu);
-  if (st->d_des_pos) return ISIM_OK;
+  if (st->des_ready) return ISIM_OK;
+  free_des(*st);  // the remains of an earlier attempt that failed part-way
   const isim::DesPlan &d = h->des;
   auto up = [&](void **dst, const void *src, size_t bytes) -> bool {
     if (hipMalloc(dst, bytes ? bytes : 8) != hipSuccess) return false;
@@ -870,11 +894,16 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
       !up((void **)&st->d_des_mult, d.slot_mult.data(), d.slot_mult.size() * 4) ||
       !up((void **)&st->d_des_fast, d.fast_pos.data(), d.fast_pos.size() * 4) ||
       !up((void **)&st->d_des_sort, d.sort_pos.data(), d.sort_pos.size() * 4) ||
-      !up((void **)&st->d_des_zero, d.zero_pos.data(), d.zero_pos.size() * 4))
+      !up((void **)&st->d_des_zero, d.zero_pos.data(), d.zero_pos.size() * 4)) {
+    free_des(*st);
     return fail(ISIM_EHIP, "DES plan upload failed");
+  }
   std::vector<uint32_t> pipe(d.pipe_pos);
   pipe.insert(pipe.end(), d.pipe_dep.begin(), d.pipe_dep.end());
-  if (!up((void **)&st->d_des_pipe, pipe.data(), pipe.size() * 4)) return fail(ISIM_EHIP, "DES plan upload failed");
+  if (!up((void **)&st->d_des_pipe, pipe.data(), pipe.size() * 4)) {
+    free_des(*st);
+    return fail(ISIM_EHIP, "DES plan upload failed");
+  }
   if (d.items) {
     const isim::Program &p = h->prog;
     // the per-batch item arrays come from a pool of this handler's own (kept
@@ -885,16 +914,21 @@ int des_prepare(isim_handler *h, int device, DevState *&st) {
     props.location.id = device;
     uint64_t keep = ~0ull;
     if (hipMemPoolCreate(&st->des_pool, &props) != hipSuccess ||
-        hipMemPoolSetAttribute(st->des_pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess)
+        hipMemPoolSetAttribute(st->des_pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) {
+      free_des(*st);
       return fail(ISIM_EHIP, "DES item pool creation failed");
+    }
     if (!up(&st->d_des_ipos, d.item_pos.data(), d.item_pos.size() * sizeof(isim::DesItemPos)) ||
         !up((void **)&st->d_des_sround, d.step_round.data(), d.step_round.size() * 4) ||
         !(p.tree_wide ? up(&st->d_des_nodes, p.tree_nodes_w.data(), p.tree_nodes_w.size() * sizeof(isim::TreeNodeW))
                       : up(&st->d_des_nodes, p.tree_nodes.data(), p.tree_nodes.size() * sizeof(isim::TreeNode))) ||
         !up(&st->d_des_text, p.tree_ext.data(), p.tree_ext.size() * sizeof(isim::TreeExt)) ||
-        !up(&st->d_des_tstep, p.tree_step.data(), p.tree_step.size() * sizeof(isim::TreeStep)))
+        !up(&st->d_des_tstep, p.tree_step.data(), p.tree_step.size() * sizeof(isim::TreeStep))) {
+      free_des(*st);
       return fail(ISIM_EHIP, "DES plan upload failed");
+    }
   }
+  st->des_ready = true;
   return ISIM_OK;
 }
 
@@ -1087,6 +1121,11 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
         break;
       }
       if (!retry) break;
+      if (retry >= isim::kDesFaultUnit) {
+        rc = fail(ISIM_EHIP, "DES batch failed: a queue pass's look-back gave up waiting for an earlier chunk "
+                             "(device fault flag); the batch was not accumulated");
+        break;
+      }
       if ((p.flags & ISIM_DES_FLAG_WIDE) || h->des.items) {
         rc = fail(ISIM_EINVAL, "DES batch not accumulated with 64-bit rows: the cyclic schedule found no fixed point "
                                "within 256 passes (or arrivals beyond the sort keys)");
@@ -1119,6 +1158,10 @@ int isim_serve_des(isim_handler *h, int device, const isim_des_params *dp, uint6
   (void)hipSetDevice(prev);
   return rc;
 }
+
+void isim_debug_set_spin_limit(uint32_t polls) { isim::des_set_spin_limit(polls); }
+
+uint32_t isim_debug_spin_limit(void) { return isim::des_spin_limit(); }
 
 int isim_des_fold(const isim_handler *h, const uint64_t *des_table, uint64_t *svc_rows) {
   if (!h || !des_table || !svc_rows) return fail(ISIM_EINVAL, "null argument");

@@ -195,6 +195,16 @@ uint64_t des_workspace_bytes(const DesPlan &plan, uint64_t n, uint64_t stats_wor
 // Points L's workspace parts into `workspace` (L.plan, n_traces, stats_words, table_rows set).
 void des_carve(DesLaunch &L, void *workspace);
 int des_launch(const DesLaunch &L, void *stream);
+// Polls a decoupled look-back (des.hip chain pass, pipelined pass; des_items.hip
+// k_qscan) makes for a predecessor before it gives up and FAILS the batch (a
+// device fault flag: the batch is not accumulated and the call reports it).
+// Default 2^26 (never expected: tickets order the tiles); 0 makes every
+// look-back fail at once (isim_debug_set_spin_limit, tests only).
+constexpr uint32_t kDesSpinLimit = 1u << 26;
+uint32_t des_spin_limit();
+void des_set_spin_limit(uint32_t polls);
+// Bit of ISIM_ST_DES_RETRY's high word: batches dropped for a device fault
+constexpr uint64_t kDesFaultUnit = 1ull << 32;
 // Chained-scan workspace of the down pass: a ticket counter per launch, then
 // one 32-byte state per (position, chunk of 4096 traces); zeroed per batch.
 uint64_t des_chain_bytes(const DesPlan &plan, uint64_t n);

@@ -30,6 +30,7 @@
 // (ISIM_DES_FLAG_WIDE; isim_serve_des does that itself).  Bytes per
 // (position, trace), narrow: queue pass 4 R + 4 W, up pass 4 R (S) + 4 R
 // (arrival row) + 4 R per child + 4 W.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -54,6 +55,7 @@ namespace dev {
 
 constexpr uint32_t kDesPer = 8;                   // traces per thread in the arrivals
 constexpr uint32_t kDesThreads = 1024;
+constexpr uint32_t kDesOvfFault = 4u;  // ovf bit: a look-back gave up (the batch fails)
 constexpr uint32_t kDesChunk = kDesPer * kDesThreads;  // 8192 traces per arrivals chunk
 constexpr uint32_t kPer = 4;                           // consecutive traces per thread in the row passes
 constexpr uint32_t kDownChunk = kPer * kDesThreads;    // traces per down-pass chunk
@@ -194,7 +196,9 @@ struct DesK {
   uint64_t *stats;            // narrow rows: the staging copy (des_commit)
   uint64_t *table;            // [rows][ISIM_DES_ROW_WORDS] (staged likewise)
   isim_trace_rec *records;
-  uint32_t *ovf;              // bit 0: a 32-bit row value reached 2^31; bit 1: no fixed point
+  uint32_t *ovf;              // bit 0: a 32-bit row value reached 2^31; bit 1: no fixed point;
+                              // kDesOvfFault: a look-back gave up (the batch is dropped as a fault)
+  uint32_t spin_limit;        // look-back polls before that fault (des_spin_limit)
   uint32_t *changed;          // fixed-point passes: set when a stored row value changes (null: no tracking)
   uint32_t quiet;             // fixed-point passes before the last: no statistics
   const uint32_t *stbits;     // own error status of (position, trace): bit t%32 of word [v][t/32]
@@ -1537,6 +1541,10 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
       int64_t top = (int64_t)chunk - 1;
       uint32_t spins = 0;
       for (;;) {
+        if (spins >= k.spin_limit) {  // never expected (tickets order the chunks): fail the batch
+          if (lane == 0) atomicOr(k.ovf, kDesOvfFault);
+          break;
+        }
         const int64_t j = top - (int64_t)lane;  // lane 0 = the nearest chunk
         const uint32_t fl = j >= 0 ? ld_flag(&cs[j].flag) : 2u;  // j < 0: the idle start, prefix 0
         const uint64_t m0 = __ballot(fl == 0), m2 = __ballot(fl == 2);
@@ -1544,7 +1552,7 @@ __device__ __forceinline__ void chain_body(const DesK &k, uint32_t v, uint32_t c
         const uint64_t below = f2 >= 64 ? ~0ull : ((1ull << f2) - 1);
         if (m0 & below) {  // a chunk this one needs has not published yet
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 26)) break;  // never expected: tickets order the chunks
+          ++spins;
           continue;
         }
         // chunks nearer than the first inclusive prefix give their own key,
@@ -1638,12 +1646,12 @@ __device__ __forceinline__ void pipe_body(const DesK &k, uint32_t v, uint32_t de
         if (threadIdx.x == 0) {
           uint32_t pv, spins = 0;
           while ((pv = ld_flag(k.prog + dep)) <= chunk) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {
-              atomicOr(k.ovf, 4u);
+            if (spins++ >= k.spin_limit) {  // never expected: fail the batch
+              atomicOr(k.ovf, kDesOvfFault);
               pv = 0xFFFFFFFFu;
               break;
             }
+            __builtin_amdgcn_s_sleep(2);
           }
           s_known = pv;
         }
@@ -2414,8 +2422,12 @@ __global__ void __launch_bounds__(kDesUpThreads) des_zero(DesK k) {
 __global__ void __launch_bounds__(256) des_commit(const uint64_t *__restrict__ stage, uint64_t *stats,
                                                   uint64_t *table, uint64_t stats_words, uint64_t table_words,
                                                   const uint32_t *ovf) {
-  if (*ovf) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long *)(stats + ISIM_ST_DES_RETRY), 1ull);
+  if (const uint32_t o = *ovf) {
+    // dropped: a retry (narrow rows overflowed, no fixed point) or a fault
+    // (a look-back gave up: counted in the word's high half, an error)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      atomicAdd((unsigned long long *)(stats + ISIM_ST_DES_RETRY),
+                (unsigned long long)((o & kDesOvfFault) ? kDesFaultUnit : 1ull));
     return;
   }
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < stats_words + table_words;
@@ -2631,6 +2643,10 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
 // read one flag per pass).
 constexpr uint32_t kMaxPasses = 256;
 
+static std::atomic<uint32_t> g_spin_limit{kDesSpinLimit};
+uint32_t des_spin_limit() { return g_spin_limit.load(std::memory_order_relaxed); }
+void des_set_spin_limit(uint32_t polls) { g_spin_limit.store(polls, std::memory_order_relaxed); }
+
 int des_launch(const DesLaunch &L, void *stream_) {
   using namespace dev;
   hipStream_t stream = (hipStream_t)stream_;
@@ -2649,6 +2665,7 @@ int des_launch(const DesLaunch &L, void *stream_) {
   k.E = L.E;
   k.blk = L.blk;
   k.ovf = L.ovf;
+  k.spin_limit = des_spin_limit();
   k.stbits = L.stbits;
   k.st_wpr = (uint32_t)status_wpr(L.n_traces);
   // statistics go to the staging copy, merged by des_commit unless the batch

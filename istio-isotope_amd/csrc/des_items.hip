@@ -174,6 +174,10 @@ struct K {
   uint32_t *ifst;
   uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
   uint32_t count_changes;          // ISIM_DES_DEBUG: changed[1] counts the values a quiet pass changed
+  // a look-back that gave up after spin_limit polls (des_spin_limit) sets
+  // *fault: the batch is not accumulated and des_items_launch fails
+  uint32_t *fault;
+  uint32_t spin_limit;
 };
 
 // a quiet pass flags a change with ONE atomic per wave, and none once the
@@ -647,8 +651,13 @@ __device__ __forceinline__ uint64_t tie_key(const K &k, uint32_t i) {
   return ((uint64_t)k.itr[i] << 32) | k.ihop[i];
 }
 // runs of equal keys in a sorted round, re-ordered by (trace, hop): the run's
-// first thread insertion-sorts it (runs are rare and short).  LIST: the
-// values are list indices into ids (k_qkey1), else item ids (k_qkey2)
+// first thread sorts it — insertion sort for short runs (the common case:
+// runs are rare and short), heapsort past kTieInsert so that one lane's work
+// stays O(r log r) when many items meet one service at one instant (a wide
+// fan-out to one replica, near-zero gaps).  Tie keys are unique
+// (one item per (trace, hop)), so the order is the same either way.  LIST:
+// the values are list indices into ids (k_qkey1), else item ids (k_qkey2)
+constexpr uint64_t kTieInsert = 32;
 template <bool LIST>
 __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_t *val, uint64_t m,
                                                const uint32_t *ids) {
@@ -658,15 +667,48 @@ __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_
     if (key[j + 1] != kj || (j > 0 && key[j - 1] == kj)) continue;  // the first of a run of ties only
     uint64_t e = j + 2;
     while (e < m && key[e] == kj) ++e;
-    for (uint64_t x = j + 1; x < e; ++x) {
-      const uint32_t v = val[x];
-      const uint64_t t = tk(v);
-      uint64_t y = x;
-      while (y > j && tk(val[y - 1]) > t) {
-        val[y] = val[y - 1];
-        --y;
+    if (e - j <= kTieInsert) {
+      for (uint64_t x = j + 1; x < e; ++x) {
+        const uint32_t v = val[x];
+        const uint64_t t = tk(v);
+        uint64_t y = x;
+        while (y > j && tk(val[y - 1]) > t) {
+          val[y] = val[y - 1];
+          --y;
+        }
+        val[y] = v;
       }
-      val[y] = v;
+      continue;
+    }
+    // heapsort of val[j, e) by tie key (a max-heap, then the max moved to the end)
+    uint32_t *a = val + j;
+    const uint64_t r = e - j;
+    auto sift = [&](uint64_t root, uint64_t len) {
+      const uint32_t v = a[root];
+      const uint64_t t = tk(v);
+      for (;;) {
+        uint64_t c = 2 * root + 1;
+        if (c >= len) break;
+        uint64_t tc = tk(a[c]);
+        if (c + 1 < len) {
+          const uint64_t t1 = tk(a[c + 1]);
+          if (t1 > tc) {
+            ++c;
+            tc = t1;
+          }
+        }
+        if (tc <= t) break;
+        a[root] = a[c];
+        root = c;
+      }
+      a[root] = v;
+    };
+    for (uint64_t x = r / 2; x-- > 0;) sift(x, r);
+    for (uint64_t len = r - 1; len > 0; --len) {
+      const uint32_t top = a[0];
+      a[0] = a[len];
+      a[len] = top;
+      sift(0, len);
     }
   }
 }
@@ -1050,6 +1092,10 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, QSrc q, QState *q
       int64_t top = (int64_t)tile - 1;
       uint32_t spins = 0;
       for (;;) {
+        if (spins >= k.spin_limit) {  // never expected (tickets order the tiles): fail the batch
+          if (lane == 0) atomicOr(k.fault, 1u);
+          break;
+        }
         const int64_t jt = top - (int64_t)lane;  // lane 0: the nearest tile
         uint32_t fl = kQInc;                    // before tile 0: an empty prefix
         if (jt >= 0) {
@@ -1061,7 +1107,7 @@ __global__ void __launch_bounds__(kT) k_qscan(K k, uint64_t m, QSrc q, QState *q
         const uint64_t upto = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1);
         if (m0 & upto) {  // a tile this one needs has not published yet
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > (1u << 26)) break;  // never expected: tickets order the tiles
+          ++spins;
           continue;
         }
         int64_t x = kQMin;
@@ -1266,6 +1312,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
 
 // ---- 5. records and the latency statistics
 __global__ void __launch_bounds__(kT) k_final(K k) {
+  if (*k.fault) return;  // a failed batch writes no record and accumulates nothing
   __shared__ uint32_t hp[2 * ISIM_N_PROM], hl[2 * ISIM_N_LOG2];
   __shared__ unsigned long long red[6][kT / 64];
   for (uint32_t i = threadIdx.x; i < 2 * ISIM_N_PROM; i += kT) hp[i] = 0;
@@ -1334,7 +1381,8 @@ __global__ void __launch_bounds__(kT) k_final(K k) {
 }
 
 __global__ void k_flag_retry(unsigned long long *stats, const uint32_t *ovf) {
-  if (ovf[0] || ovf[1]) atomicAdd(stats + ISIM_ST_DES_RETRY, 1ull);
+  if (ovf[2]) atomicAdd(stats + ISIM_ST_DES_RETRY, (unsigned long long)kDesFaultUnit);  // a fault: an error
+  else if (ovf[0] || ovf[1]) atomicAdd(stats + ISIM_ST_DES_RETRY, 1ull);
 }
 
 }  // namespace dit
@@ -1560,7 +1608,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       M * 8, M * 8, M * 4, M * 4,                              // round: key a/b, val a/b
       M * 4, M * 4, M * 4, M * 4, M * 16, M * 16, M * 4,      // rk a/b, rv a/b, mp in/out, sid
       4, 4, 16,                                                // (k_qscan ticket, spare); ovf: key overflow, no fixed
-                                                               // point, (unused), step-op count
+                                                               // point, look-back fault, step-op count
       96,                                                      // two arrival-range slots; change flag, count
       k.bw ? M * k.bw * 4 : 4, k.bw ? M * k.bw * 8 : 8,        // step ops sorted
       (uint64_t)(R + 1) * 4, (uint64_t)rows_n * 8,              // step-op offsets; hold per row
@@ -1605,6 +1653,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *qticket = (uint32_t *)carve(parts[29]);  // k_qscan's tile tickets (its states: mp_out)
   (void)carve(parts[30]);
   uint32_t *ovf = (uint32_t *)carve(parts[31]);
+  k.fault = ovf + 2;
+  k.spin_limit = des_spin_limit();
   uint64_t *mm = (uint64_t *)carve(parts[32]);
   uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] how many (debug)
   uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
@@ -1976,7 +2026,20 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     // 5. records and statistics
     hipLaunchKernelGGL(k_final, dim3(grid_for(n, 1024)), dim3(kT), 0, s, k);
     hipLaunchKernelGGL(k_flag_retry, dim3(1), dim3(1), 0, s, k.stats, ovf);
-    if (hipGetLastError() != hipSuccess) rc = fail("kernel launch");
+    if (hipGetLastError() != hipSuccess) {
+      rc = fail("kernel launch");
+      break;
+    }
+    // a look-back that gave up (k_qscan) fails the batch loudly: nothing was
+    // accumulated (k_final) and the call returns the error
+    uint32_t fault = 0;
+    if (hipMemcpyAsync(&fault, ovf + 2, 4, hipMemcpyDeviceToHost, s) != hipSuccess || sync_s() != hipSuccess) {
+      rc = fail("fault read-back");
+      break;
+    }
+    if (fault)
+      rc = fail("a queue scan's look-back gave up waiting for an earlier tile (k_qscan): the batch was not "
+                "accumulated");
   } while (0);
   return rc;
 }

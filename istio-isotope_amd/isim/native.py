@@ -138,6 +138,8 @@ SIGNATURES = {
                                         _VP, C.c_uint64, _VP]),
     "isim_serve_des": (C.c_int, [_VP, C.c_int, C.POINTER(DesParams), C.c_uint64, C.c_uint64, _VP, _VP, _VP]),
     "isim_des_fold": (C.c_int, [_VP, _VP, _VP]),
+    "isim_debug_set_spin_limit": (None, [C.c_uint32]),
+    "isim_debug_spin_limit": (C.c_uint32, []),
     "isim_multi_get_id": (C.c_int, [C.POINTER(MultiId)]),
     "isim_multi_precheck": (C.c_int, [C.c_int]),
     "isim_multi_init_rank": (C.c_int, [C.POINTER(MultiId), C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]),

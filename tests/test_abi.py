@@ -180,3 +180,19 @@ def test_des_last_batch_zero_before_any_batch():
     d = isim.DesHandler(h, 1_000_000)
     assert d.info.items == 1
     assert d.last_batch() == {"passes": 0, "syncs": 0, "items": 0}
+
+
+def test_debug_spin_limit_hook():
+    """The look-back timeout hook: process-wide, read at
+    each DES launch; the default is 2^26 polls.  The GPU side of the error
+    path is tests/test_des_items_gpu.py::test_lookback_timeout_fails_loudly."""
+    lib = native.load()
+    assert lib.isim_debug_spin_limit() == 1 << 26
+    try:
+        lib.isim_debug_set_spin_limit(0)
+        assert lib.isim_debug_spin_limit() == 0
+        lib.isim_debug_set_spin_limit(12345)
+        assert lib.isim_debug_spin_limit() == 12345
+    finally:
+        lib.isim_debug_set_spin_limit(1 << 26)
+    assert lib.isim_debug_spin_limit() == 1 << 26

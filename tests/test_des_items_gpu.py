@@ -83,6 +83,12 @@ CASES = {
     "canonical_p50": lambda: _sleepy(_prob_canonical()),
     "tree_reps_p70": lambda: _with_prob(_sleepy_tree(3, 4, reps_leaves=3), 70),
     "seq_tree_p50": lambda: _with_prob(_sleepy(tree_topology(3, 3, sequential=True)), 50),
+    # ~54 calls of one trace reach `z` at the same instant: runs of equal queue
+    # keys longer than k_tiefix's insertion-sort bound (its heapsort)
+    "fanout_ties": lambda: {"services": [
+        {"name": "a", "isEntrypoint": True,
+         "script": [{"sleep": "100us"}, [{"call": {"service": "z", "probability": 90}}] * 60]},
+        {"name": "z", "script": [{"sleep": "10us"}]}]},
 }
 
 
@@ -361,3 +367,70 @@ def test_items_qscan_equals_scan_by_key(gpu, monkeypatch, case):
     assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))
     rows = d.fold(got[2])
     assert int(rows[:, native.DES_SUM_WAIT].sum()) > 0
+
+
+def test_items_c4w_graph(gpu):
+    """the DES item engine on c4w's own graph (the
+    100,000-service realistic graph at probability 30: a wide tree whose
+    pre-walk runs the 16-byte-node lane walk), 20,000 traces at the config-5
+    load against des_oracle.c — records, stats and the DES table
+    (create_realistic_topology.py:28-76, executable.go:84-179,
+    svc/service.go:30-31)."""
+    import bench
+    j, _ = bench.build_graph("c4w")
+    c = DesCase(j, 6_000_000)
+    assert c.d.info.items == 1 and c.h.launch_info(0)["tree_wide"] == 1
+    _, _, rows = c.compare((1 << 32) - 10_000, 20_000)
+    assert int(rows[:, native.DES_COUNT].sum()) > 20_000
+
+
+@pytest.fixture
+def spin_limit_zero():
+    lib = native.load()
+    lib.isim_debug_set_spin_limit(0)
+    try:
+        yield
+    finally:
+        lib.isim_debug_set_spin_limit(1 << 26)
+
+
+def test_lookback_timeout_fails_loudly(gpu, spin_limit_zero):
+    """VERDICT r5 item 3 / ADVICE r5: a decoupled look-back that gives up
+    (forced here: isim_debug_set_spin_limit(0) makes every look-back fail at
+    once) fails the batch — ISIM_EHIP with the reason, nothing accumulated,
+    no record written — instead of returning ISIM_OK with wrong queue starts.
+    The item engine's k_qscan (des_items.hip) through both the device entry
+    and isim_serve_des, then the static engine's chained queue pass (des.hip)
+    whose async entry flags the fault in ISIM_ST_DES_RETRY's high half."""
+    import torch
+    c = DesCase(CASES["mesh_des"](), 20_000)
+    n = 300_000
+    with pytest.raises(native.IsimError) as ei:
+        c.d.serve(0, n, device=0)
+    assert ei.value.code == native.EHIP and "look-back" in str(ei.value)
+    ws = torch.zeros(c.d.workspace_bytes(n) + 8, dtype=torch.uint8, device="cuda")
+    stats = torch.zeros(len(c.h.new_stats()), dtype=torch.int64, device="cuda")
+    table = torch.zeros(max(1, c.d.table_words), dtype=torch.int64, device="cuda")
+    rec = torch.full((n * 2,), -1, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(native.IsimError):
+        c.d.serve_device(0, n, rec.data_ptr(), stats.data_ptr(), table.data_ptr(), ws.data_ptr(), ws.numel(), s)
+    torch.cuda.synchronize()
+    got = stats.cpu().numpy().view(np.uint64)
+    assert int(got[native.ST_DES_RETRY]) == 1 << 32 and int(got[native.ST_N_TRACES]) == 0
+    assert int(got.sum()) == 1 << 32 and int(table.abs().sum()) == 0
+    assert bool((rec == -1).all())
+    # the static (level-synchronous) engine: the chained pass's look-back
+    doc = realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.05))
+    hs = isim.Handler(isim.ServiceGraph.from_json(obj_to_json(doc)), None, isim.SimParams())
+    ds = isim.DesHandler(hs, 700_000)
+    assert ds.info.items == 0
+    with pytest.raises(native.IsimError) as ei:
+        ds.serve(0, 1 << 18, device=0)
+    assert ei.value.code == native.EHIP and "look-back" in str(ei.value)
+
+
+def test_lookback_limit_restored_runs_clean(gpu):
+    """After the hook is reset the same batches run and match the oracle."""
+    assert native.load().isim_debug_spin_limit() == 1 << 26
+    DesCase(CASES["mesh_des"](), 20_000).compare(0, 2000)

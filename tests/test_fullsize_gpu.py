@@ -307,3 +307,27 @@ def test_config3s_bench_batch(gpu):
     _launch_edge_windows(c, rec, begin, n, L, width=128)
     _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=11)
     c.compare(begin + n - 2048, 4096)
+
+
+def test_config4w_bench_batch(gpu):
+    """c4w exactly as bench.py times it —
+    bench.build_graph("c4w") (create_realistic_topology.py:28-76's multitier
+    graph at 100,000 services, probability 30 on every call, errorRate U[0,1%])
+    on the WIDE lane tree walk (kind 7, 16-byte nodes, 100,000 positions and
+    call sites), BENCH_BATCH["c4w"] = 2^22 traces per launch, two launches into
+    one stats buffer with trace ids crossing 2^32; oracle windows at every
+    launch edge and internal split, sampled windows, and the full stats
+    (per service, per site, svc_dur) of a window (executable.go:84-179)."""
+    j, _ = bench.build_graph("c4w")
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7 and li["tree_wide"] == 1
+    n, L = bench.BENCH_BATCH["c4w"], 2
+    assert n == 1 << 22
+    begin = (1 << 32) - n - n // 3  # the second launch crosses 2^32
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    assert rec["hops"].min() >= 1 and f["n_500"] > 0
+    _launch_edge_windows(c, rec, begin, n, L, width=128)
+    _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=13)
+    c.compare(begin + n - 2048, 4096)

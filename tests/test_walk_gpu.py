@@ -367,6 +367,49 @@ def test_tree_spill_two_streams(gpu):
         assert np.array_equal(fk["site_calls"], k * f1["site_calls"])
 
 
+def test_tree_graph_capture(gpu):
+    """isim_serve_device is graph-capturable after the first
+    call on a device (isim.h), except for a spilling lane tree walk, whose
+    spill area a graph would pin while eager launches on other streams take
+    the same area: that capture returns ISIM_EINVAL.  A non-spilling dynamic
+    walk captured on one stream and replayed alongside eager launches of the
+    same handler on a second stream gives each its own, correct results."""
+    import torch
+    dev = torch.device("cuda", 0)
+    deep = Case(_prob_chain(40), None, isim.SimParams())
+    deep.gpu(0, 1000)  # the first call prepares the device
+    st = torch.zeros(deep.handler.stats_words, dtype=torch.int64, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        with pytest.raises(isim.IsimError) as ei:
+            deep.handler.serve_device(0, 1000, 0, st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert ei.value.code == isim.native.EINVAL and "captured" in str(ei.value)
+
+    c = Case(_prob_chain(8), None, isim.SimParams())
+    assert c.handler.launch_info(0)["kernel_kind"] == 7
+    n, b1, b2 = 50_000, 1 << 30, 77
+    ref1, ref2 = c.gpu(b1, n), c.gpu(b2, n)
+    rec1 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    st1 = torch.zeros(c.handler.stats_words, dtype=torch.int64, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        c.handler.serve_device(b1, n, rec1.data_ptr(), st1.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    other = torch.cuda.Stream(dev)
+    rec2 = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    st2 = torch.zeros(c.handler.stats_words, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    k = 4
+    for _ in range(k):
+        g.replay()
+        c.handler.serve_device(b2, n, rec2.data_ptr(), st2.data_ptr(), other.cuda_stream)
+    torch.cuda.synchronize()
+    for rec, stt, ref in ((rec1, st1, ref1), (rec2, st2, ref2)):
+        assert np.array_equal(rec.cpu().numpy().view(isim.REC_DTYPE), ref[0])
+        fk, f1 = c.handler.fold(stt.cpu().numpy().view(np.uint64)), c.handler.fold(ref[1])
+        assert fk["n_traces"] == k * n and fk["sum_latency"] == k * f1["sum_latency"]
+        assert np.array_equal(fk["site_calls"], k * f1["site_calls"])
+
+
 @pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
 def test_tree_u64_time(gpu, mode):
     """The lane tree walk with u64 time (Program::tree_t64): a chain of 1.5 s
