@@ -99,6 +99,9 @@ typedef struct {
                                    (parity tests of the general path on static graphs; no DES) */
 #define ISIM_FLAG_WAVE_WALK 32u /* dynamic walks on the wave-walk interpreter (kinds 2/3: a wave walks the union
                                    of its 64 traces' call paths) instead of the lane tree walk (kind 7) */
+#define ISIM_FLAG_CLOSE_LIST 64u /* mode B on the draw stream: the close-list kernel (kind 6) instead of sparse
+                                    ancestor marking (kind 8, the default when its per-invocation mark table
+                                    fits the LDS) */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -177,9 +180,11 @@ typedef struct {
   int32_t max_blocks;        /* resident workgroups on the device (grid cap) */
   int32_t kernel_kind;       /* 0/1 static interpreter u32/u64 time, 2/3 dynamic u32/u64, 4 draw stream,
                                 5 draw stream with the mode-B bit stack (call depth <= 32),
-                                6 draw stream with the mode-B close list (the default in mode B),
+                                6 draw stream with the mode-B close list (ISIM_FLAG_CLOSE_LIST, or a stream
+                                too long for kind 8's LDS mark table),
                                 7 lane tree walk (dynamic walks whose unrolled tree of potential
-                                invocations has at most 2^24 positions; else 2/3) */
+                                invocations has at most 2^24 positions; else 2/3),
+                                8 draw stream with mode-B sparse ancestor marking (the default in mode B) */
   int32_t fill;              /* 1: a draw-free static walk: one trace walked, batches are a record fill
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
   int32_t tree_wide;         /* kind 7 on a wide tree (more than 65,535 positions, call sites or rows, or

@@ -53,6 +53,9 @@ struct DevState {
   isim::StreamClose *d_closes = nullptr;  // mode-B draw stream (kind 6): close list
   uint32_t *d_close_slot = nullptr;       // per close: call-site slot
   uint32_t *d_close_end = nullptr;        // and its per-chunk ends
+  uint32_t *d_mark_end = nullptr;         // mode-B draw stream (kind 8): per record its subtree's last record
+  uint32_t *d_mark_slot = nullptr;        // and its call-site slot
+  uint32_t mark_words = 0;                // kind 8: position marks per workgroup (records + the sentinel)
   uint32_t *d_dur = nullptr;   // dynamic walks: per-slot duration-table word (row | leaf bucket << 24)
   unsigned long long *d_work = nullptr;  // kWorkSlots sets of batch queues, zero between launches
   uint32_t *d_stage = nullptr;  // draw stream: kWorkSlots rows of n_slots u32 500 counts, zero between launches
@@ -119,7 +122,7 @@ void free_des(DevState &d) {
 void free_dev(DevState &d) {
   free_des(d);
   for (void *q : {(void *)d.d_prog, (void *)d.d_mult, (void *)d.d_closes, (void *)d.d_close_end,
-                  (void *)d.d_close_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_stage, (void *)d.d_const_stats,
+                  (void *)d.d_close_slot, (void *)d.d_mark_end, (void *)d.d_mark_slot, (void *)d.d_dur, (void *)d.d_work, (void *)d.d_stage, (void *)d.d_const_stats,
                   (void *)d.d_tree_ext, (void *)d.d_tree_dyn, (void *)d.d_tree_step,
                   (void *)d.d_sum_row, (void *)d.d_slot_tc, (void *)d.d_lds_slot})
     if (q) (void)hipFree(q);
@@ -166,7 +169,7 @@ struct isim_handler {
 namespace {
 
 // Kernel kinds 4-6 walk the draw stream (static walks).
-bool is_stream(uint32_t kind) { return kind >= 4 && kind <= 6; }
+bool is_stream(uint32_t kind) { return (kind >= 4 && kind <= 6) || kind == 8; }
 
 // Rows of the device per-service duration table (dynamic walks only).
 uint64_t svc_dur_rows(const isim_handler *h) {
@@ -245,6 +248,21 @@ int build_device(isim_handler *h, int device, DevState &st) {
   // (ISIM_FLAG_BIT_STACK), else the close list (any depth)
   if (st.kind == 4 && h->params.error_mode == ISIM_MODE_B)
     st.kind = (h->params.flags & ISIM_FLAG_BIT_STACK) ? (p.max_depth <= 32 ? 5u : 4u) : 6u;
+  // mode B by sparse ancestor marking (kind 8) when its per-position mark
+  // table fits the LDS next to the histograms (ISIM_FLAG_CLOSE_LIST: kind 6)
+  if (st.kind == 6 && !(h->params.flags & ISIM_FLAG_CLOSE_LIST)) {
+    const uint32_t words = p.stream_nodes + 1u;
+    const uint32_t need = isim::kLdsAccBytes + isim::kHistWords * 4u + 4u * words;
+    if (need <= lds_max) {
+      st.kind = 8;
+      st.mark_words = words;
+      counters = true;
+      waves = 16;
+      st.threads = waves * 64u;
+      st.lds_bytes = need;
+      st.lds_counters = 1;
+    }
+  }
   st.kernel = isim::walk_kernel((int)st.kind, h->params.error_mode == ISIM_MODE_B, counters);
   // dynamic walks: the lane tree walk (kind 7) when the unrolled tree was
   // built and its LDS layout placed (program.cpp place_tree); else the wave walk
@@ -322,7 +340,8 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (per_cu < 1) return fail(ISIM_EHIP, "walk kernel cannot be resident (occupancy 0)");
   st.per_cu = (uint32_t)per_cu;
   st.max_blocks = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
-  const void *src = is_stream(st.kind) ? (const void *)p.stream.data()
+  const void *src = st.kind == 8          ? (const void *)p.stream_mark.data()
+                    : is_stream(st.kind) ? (const void *)p.stream.data()
                     : tree                ? (p.tree_wide ? (const void *)p.tree_nodes_w.data()
                                                          : (const void *)p.tree_nodes.data())
                                           : (const void *)p.code.data();
@@ -384,6 +403,20 @@ int build_device(isim_handler *h, int device, DevState &st) {
                   2 * sizeof(uint32_t));
     if (rc != ISIM_OK) return rc;
   }
+  if (st.kind == 8) {
+    // the fold's inputs (per real record) and the launches' mark rows
+    std::vector<uint32_t> slot(p.stream_nodes);
+    for (uint32_t r = 0; r < p.stream_nodes; ++r) slot[r] = p.stream[r].meta & 0xFFFFFFu;
+    HIPCHK(hipMalloc(&st.d_mark_end, p.stream_nodes * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(st.d_mark_end, p.stream_end.data(), p.stream_nodes * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&st.d_mark_slot, p.stream_nodes * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(st.d_mark_slot, slot.data(), p.stream_nodes * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const size_t bytes = (size_t)isim::kWorkSlots * st.mark_words * sizeof(uint32_t);
+    HIPCHK(hipMalloc(&st.d_stage, bytes));
+    HIPCHK(hipMemset(st.d_stage, 0, bytes));
+    HIPCHK(hipFuncSetAttribute(isim::mark_fold_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(st.mark_words * 4u)));
+  }
   HIPCHK(hipMalloc(&st.d_work, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   HIPCHK(hipMemset(st.d_work, 0, (size_t)isim::kWorkWords * isim::kWorkSlots * sizeof(unsigned long long)));
   // per-workgroup LDS site counters are u32: launch_walk splits a batch so
@@ -409,7 +442,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
   if (is_stream(st.kind)) {
     st.max_mult = 1;
     for (uint32_t m : p.stream_mult) st.max_mult = std::max<uint64_t>(st.max_mult, m);
-    if (st.lds_counters && p.n_slots > 0 && p.n_slots <= isim::kStageMaxSlots) {
+    if (st.kind != 8 && st.lds_counters && p.n_slots > 0 && p.n_slots <= isim::kStageMaxSlots) {
       const size_t bytes = (size_t)isim::kWorkSlots * p.n_slots * sizeof(uint32_t);
       HIPCHK(hipMalloc(&st.d_stage, bytes));
       HIPCHK(hipMemset(st.d_stage, 0, bytes));
@@ -667,7 +700,8 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const uint32_t slot = __atomic_fetch_add(&st->work_next, 1u, __ATOMIC_RELAXED) % isim::kWorkSlots;
   kp.work = st->d_work + isim::kWorkWords * slot;
   // u32 staging of the 500 counts: the launch split (launch_walk) keeps n x max_mult below 2^32
-  kp.stage = st->d_stage ? st->d_stage + (size_t)slot * h->prog.n_slots : nullptr;
+  kp.stage = st->d_stage ? st->d_stage + (size_t)slot * (st->kind == 8 ? st->mark_words : h->prog.n_slots) : nullptr;
+  kp.mark_words = st->mark_words;
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
@@ -698,10 +732,17 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   } else {
     HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, (hipStream_t)hip_stream));
   }
+  if (st->kind == 8) {  // the launch's position marks into the per-site 500 counters
+    uint32_t *row = kp.stage;
+    uint32_t n = h->prog.stream_nodes, words = st->mark_words, n_slots = (uint32_t)h->prog.n_slots;
+    const uint32_t *end = st->d_mark_end, *mslot = st->d_mark_slot;
+    void *args3[] = {&row, &n, &words, &end, &mslot, &d_stats, &n_slots};
+    HIPCHK(hipLaunchKernel(isim::mark_fold_kernel(), dim3(1), dim3(1024), args3, words * 4u, (hipStream_t)hip_stream));
+  }
   if (is_stream(st->kind) && h->prog.n_slots > 0) {
     uint32_t n_slots = (uint32_t)h->prog.n_slots;
     const uint32_t *mult = st->d_mult;
-    uint32_t *stage = kp.stage;
+    uint32_t *stage = st->kind == 8 ? nullptr : kp.stage;
     void *args2[] = {&mult, &n_slots, &n_traces, &d_stats, &stage};
     HIPCHK(hipLaunchKernel(isim::stream_calls_kernel(), dim3((n_slots + 255) / 256), dim3(256), args2, 0,
                            (hipStream_t)hip_stream));

@@ -64,6 +64,27 @@ struct StreamClose {
 };
 static_assert(sizeof(StreamClose) == 8, "StreamClose must be 8 bytes");
 constexpr uint32_t kClosePad = 16;  // zero StreamClose records after the list (block prefetch)
+
+// Mode B on the draw stream by sparse ancestor marking (kernel kind 8, the
+// default): an invocation responds 500 iff an invocation of its subtree drew
+// an error, i.e. the 500s of a trace are the union of the root paths of its
+// erring invocations.  With e_1 < e_2 < ... the erring records (preorder),
+// that union is counted per position by +1 at every e_i and -1 at
+// LCA(e_{i-1}, e_i): the subtree sum of those marks at v is 1 iff v responded
+// 500 (summed over traces: v's 500 count; linear, so all traces share one
+// per-position table).  For preorder records u < w, LCA(u, w) is the parent of
+// the shallowest record in (u, w], so a lane only keeps, per trace, the
+// minimum of the records' keys since its last error; at an error that minimum
+// names the LCA and its depth, and the trace's new 500s are
+// depth(e_i) - depth(LCA).  Stream record (same 8-byte shape as Node):
+// thr, and key = always (31) | depth (24-30) | parent record (0-23); the
+// entry's parent is the sentinel record n (a counter nobody reads); padding
+// records have key kMarkPadKey (above every real key).  A per-launch fold
+// (isim_mark_fold) turns the position marks into subtree sums and adds them
+// to the per-site 500 counters.
+constexpr uint32_t kMarkPadKey = 0x7FFFFFFFu;
+constexpr uint32_t kMarkKeyMask = 0x7FFFFFFFu;  // key without the always bit
+constexpr uint32_t kMarkPosMask = 0xFFFFFFu;
 constexpr uint32_t kChunkGroups = 8;                  // Philox groups (4 records) per chunk
 constexpr uint32_t kChunkRecords = 4 * kChunkGroups;  // 32: one bit per record per lane
 
@@ -206,6 +227,7 @@ struct KParams {
   const StreamClose *closes;     // kind 6: close list (+kClosePad zero records of tail padding)
   const uint32_t *close_slot;    // kind 6: per close, the call-site slot of the closing invocation
   const uint32_t *close_end;     // kind 6: per chunk, closes up to and including it
+  uint32_t mark_words;           // kind 8: position marks (records + the sentinel) in the LDS table
   const TreeExt *tree_ext;       // kind 7: per position (the nodes are the `prog` argument)
   const TreeStep *tree_step;     // kind 7: per position (read under TF_XPRE / TF_XCMAX)
   const TreeDynRow *tree_dyn;    // kind 7: rows with an LDS bucket table
@@ -263,6 +285,7 @@ inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds
               : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide);
 }
 void *stream_calls_kernel();
+void *mark_fold_kernel();  // kind 8: the per-launch fold of the position marks (walk.hip isim_mark_fold)
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)
 uint32_t stream_traces_per_wave();
 

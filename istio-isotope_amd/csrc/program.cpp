@@ -746,12 +746,18 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
       uint32_t pre;  // stream position of the invocation
       uint32_t slot;
     };
+    // kind 8 (sparse ancestor marking): per record its depth and parent
+    std::vector<uint32_t> depth_of, parent_of;
     struct Pop {
       uint32_t pre, end, slot;  // a calling invocation: its subtree spans records [pre, end]
     };
     std::vector<Frame> stack;
     std::vector<Pop> pops;
+    out.stream_end.clear();
     rec(entry, kSlotRoot);
+    depth_of.push_back(0);
+    parent_of.push_back(~0u);  // the sentinel, set below
+    out.stream_end.push_back(0);
     stack.push_back({entry, 0, 0u, kSlotRoot});
     while (!stack.empty()) {
       Frame &top = stack.back();
@@ -759,20 +765,33 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
         const int32_t sid = svc_sites[top.svc][top.next++];
         const uint32_t slot = (uint32_t)out.site_slot[sid];
         const uint32_t pre = (uint32_t)out.stream.size();
+        depth_of.push_back((uint32_t)stack.size());
+        parent_of.push_back(top.pre);
+        out.stream_end.push_back(0);
         rec(sites[sid].callee, slot);
         stack.push_back({sites[sid].callee, 0, pre, slot});
       } else {
         const uint32_t end = (uint32_t)out.stream.size() - 1;
         if (top.pre != end && top.slot != kSlotRoot) pops.push_back({top.pre, end, top.slot});
+        out.stream_end[top.pre] = end;
         stack.pop_back();
         out.stream.back().meta += 1u << 24;  // the subtree ending here closes after this record
       }
     }
     out.stream_nodes = (uint32_t)out.stream.size();
+    // the mark stream (kind 8): thr | always | depth | parent; the entry's
+    // parent is the sentinel record n (depth <= max_depth - 1 <= 63: 7 bits)
+    out.stream_mark.clear();
+    for (uint32_t r = 0; r < out.stream_nodes; ++r) {
+      const Node &nd = out.stream[r];
+      const uint32_t par = r == 0 ? out.stream_nodes : parent_of[r];
+      out.stream_mark.push_back(Node{nd.thr, (nd.meta & 0x80000000u) | (depth_of[r] << 24) | (par & kMarkPosMask)});
+    }
     out.stream_mult.assign((size_t)out.n_slots, 0u);
     for (const Node &nd : out.stream)
       if ((nd.meta & 0xFFFFFFu) != kSlotRoot) out.stream_mult[nd.meta & 0xFFFFFFu] += 1;
     while (out.stream.size() % 4) out.stream.push_back(Node{0u, kSlotPad});
+    while (out.stream_mark.size() % 4) out.stream_mark.push_back(Node{0u, kMarkPadKey});
     // close list of the mode-B stream kernel (kernel_abi.h, StreamClose)
     const uint32_t n_rec = (uint32_t)out.stream.size();
     const uint32_t n_chunks = (n_rec + kChunkRecords - 1) / kChunkRecords;

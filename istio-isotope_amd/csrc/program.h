@@ -39,6 +39,8 @@ struct Program {
   std::vector<StreamClose> stream_closes;       // mode B (kind 6): closes of calling invocations
   std::vector<uint32_t> stream_close_slot;      // per close: call-site slot
   std::vector<uint32_t> stream_close_end;       // per chunk of kChunkRecords records
+  std::vector<Node> stream_mark;                // mode B (kind 8): thr | key (kernel_abi.h), padded like stream
+  std::vector<uint32_t> stream_end;             // kind 8: per record, the last record of its subtree
   // per-service invocation durations (RecordResponseSent, prometheus/handler.go:101-106)
   std::vector<uint64_t> svc_time;   // per service: T_max; the exact duration when static_walk
   std::vector<int32_t> svc_row;     // per service: row in the duration table (-1: unreachable)

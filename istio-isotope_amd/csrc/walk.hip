@@ -1006,6 +1006,150 @@ __device__ __forceinline__ void walk_stream_cl(const Ctx &c, CNode4 *__restrict_
   }
 }
 
+// Mode B on the draw stream by sparse ancestor marking (kernel kind 8, the
+// default; kernel_abi.h kMarkPadKey).  The walk is mode A's — one Philox block
+// per group of 4 records, one compare per record and trace — plus, per record
+// and trace, one v_min of the record's key into the lane's running minimum
+// since its trace's last error.  Only where some lane errs (the branch mode A
+// takes for its counters anyway) the erring lanes mark: +1 at the record (one
+// ds_add for the wave), -1 at the LCA that minimum names (a ds_sub per
+// erring lane), and the trace's new 500s depth(e) - depth(LCA) into its error
+// count.  The entry responds 500 iff its trace erred at all.  Costs against
+// the close list (kind 6): no per-chunk close tests (4,389 per trace on
+// config 3), no error-bit shifts, no call-depth limit.
+template <int TPL, bool FULL>
+__device__ __forceinline__ void walk_stream_mark(const Ctx &c, CNode4 *__restrict__ stream, uint32_t n_groups,
+                                                 uint32_t n_nodes, uint64_t t_static, uint64_t trace_begin,
+                                                 uint64_t n_traces, uint64_t base) {
+  const uint32_t lane = lane_id();
+  const bool lane0 = lane == 0;
+  uint64_t idx[TPL], all[TPL];
+  uint32_t t_lo[TPL], t_hi[TPL], t_hi_u[TPL];
+  bool valid[TPL];
+  bool hi_uniform = true;
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    idx[u] = base + 64u * u + lane;
+    valid[u] = idx[u] < n_traces;
+    const uint64_t t = trace_begin + idx[u];
+    t_lo[u] = (uint32_t)t;
+    t_hi[u] = (uint32_t)(t >> 32);
+    t_hi_u[u] = rfl(t_hi[u]);
+    hi_uniform = hi_uniform && ballot(t_hi[u] != t_hi_u[u]) == 0 && t_hi_u[u] == t_hi_u[0];
+    all[u] = ballot(valid[u]);
+  }
+  uint32_t errh[TPL], mk[TPL];
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    errh[u] = 0;
+    mk[u] = 0xFFFFFFFFu;
+  }
+  uint32_t *marks = c.cnt;
+  auto group = [&](const Node4 &q, uint32_t g) {
+    uint32_t x[TPL][4];
+#pragma unroll
+    for (int u = 0; u < TPL; ++u) x[u][0] = x[u][1] = x[u][2] = x[u][3] = 0;
+    if ((q.n[0].thr | q.n[1].thr | q.n[2].thr | q.n[3].thr) != 0) {
+      if (hi_uniform) {
+        philox_lockstep<TPL>(t_lo, t_hi_u[0], g, c.k0, c.k1, x);
+      } else {
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) philox_group(t_lo[u], t_hi[u], t_hi_u[u], hi_uniform, g, c.k0, c.k1, x[u]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t kw = q.n[j].meta;
+      const uint32_t key = kw & kMarkKeyMask;
+      const uint64_t always = (kw & 0x80000000u) ? ~0ull : 0ull;  // errorRate 1: no draw, always 500
+      uint64_t own[TPL], any = 0;
+#pragma unroll
+      for (int u = 0; u < TPL; ++u) {
+        own[u] = ballot(x[u][j] < q.n[j].thr) | always;
+        if constexpr (!FULL) own[u] &= all[u];
+        mk[u] = mk[u] < key ? mk[u] : key;
+        any |= own[u];
+      }
+      if (any) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) n += popc(own[u]);
+        if (lane0) atomicAdd(marks + 4u * g + (uint32_t)j, n);
+        const uint32_t d1 = (key >> 24) + 1u;
+#pragma unroll
+        for (int u = 0; u < TPL; ++u) {
+          if (lane_in(own[u])) {
+            atomicSub(marks + (mk[u] & kMarkPosMask), 1u);
+            errh[u] += d1 - (mk[u] >> 24);
+            mk[u] = 0xFFFFFFFFu;
+          }
+        }
+      }
+    }
+  };
+  // group g+1 is loaded (the device buffer carries two zero groups of tail
+  // padding) before group g is processed (walk_stream)
+  Node4 cur = load_group(stream);
+  for (uint32_t g = 0; g < n_groups; ++g) {
+    const Node4 nxt = load_group(stream + g + 1);
+    group(cur, g);
+    cur = nxt;
+  }
+#pragma unroll
+  for (int u = 0; u < TPL; ++u) {
+    const uint64_t root_st = ballot(errh[u] != 0u) & all[u];
+    finish_batch(c, idx[u], valid[u], all[u], t_static, n_nodes, root_st, errh[u]);
+  }
+}
+
+// Kind 8's per-launch fold (one workgroup): the launch's position marks
+// (u32, wrapping: the -1s at an LCA reached often go "negative") become
+// subtree sums S(v) = P[end(v)] - P[v - 1] over their prefix sums P — the
+// launch's count of 500 responses of the invocation at record v, below 2^32
+// (launch_walk's split) — added to the per-site 500 counters; the row is
+// zeroed for the next launch that takes this work slot.
+__global__ void __launch_bounds__(1024) isim_mark_fold(uint32_t *__restrict__ stage, uint32_t n, uint32_t words,
+                                                       const uint32_t *__restrict__ end,
+                                                       const uint32_t *__restrict__ slot,
+                                                       uint64_t *__restrict__ gstats, uint32_t n_slots) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  uint32_t *P = reinterpret_cast<uint32_t *>(lds);
+  __shared__ uint32_t wtot[16];
+  const uint32_t tid = threadIdx.x, nt = blockDim.x;
+  for (uint32_t i = tid; i < words; i += nt) {
+    P[i] = i < n ? stage[i] : 0u;
+    stage[i] = 0u;
+  }
+  __syncthreads();
+  // each thread a contiguous segment: local sums, a block scan of the
+  // segment totals, then the segment rewritten as inclusive prefix sums
+  const uint32_t seg = (n + nt - 1) / nt;
+  const uint32_t b = tid * seg, e = b + seg < n ? b + seg : n;
+  uint32_t tot = 0;
+  for (uint32_t i = b; i < e; ++i) tot += P[i];
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  uint32_t inc = tot;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  uint32_t pre = inc - tot;
+  for (uint32_t w = 0; w < wave; ++w) pre += wtot[w];
+  for (uint32_t i = b; i < e; ++i) {
+    pre += P[i];
+    P[i] = pre;
+  }
+  __syncthreads();
+  unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SITES + n_slots);
+  for (uint32_t v = 1 + tid; v < n; v += nt) {
+    const uint32_t s = P[end[v]] - P[v - 1];
+    if (s) atomicAdd(st + slot[v], (unsigned long long)s);
+  }
+}
+
 // Executed-call counters of a static walk: every trace makes mult[slot] calls
 // through each reachable call site, so a launch over n_traces adds
 // mult[slot] * n_traces (exact; added once per launch).
@@ -1084,7 +1228,7 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
     lstk = reinterpret_cast<TT *>(stk + wave * per_wave);
     hstk = reinterpret_cast<uint32_t *>(stk + wave * per_wave + kp.max_frames * 64u * 2u * (uint32_t)sizeof(TT));
   }
-  const uint32_t zero_words = (kLdsAccBytes / 4) + kHistWords + (LDSC ? 2u * kp.n_slots : 0u);
+  const uint32_t zero_words = (kLdsAccBytes / 4) + kHistWords + (LDSC ? (KIND == 8 ? kp.mark_words : 2u * kp.n_slots) : 0u);
   uint32_t *z = reinterpret_cast<uint32_t *>(lds);
   for (uint32_t i = threadIdx.x; i < zero_words; i += blockDim.x) z[i] = 0;
   __syncthreads();
@@ -1111,7 +1255,12 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
       const uint64_t base = b * 64 * kStreamTPL;
       CNode4 *st = (CNode4 *)(const __attribute__((address_space(1))) Ins *)prog;
       const uint32_t ng = kp.n_nodes ? (kp.n_nodes + 3) / 4 : 0;
-      if constexpr (KIND == 6) {
+      if constexpr (KIND == 8) {
+        if (base + 64 * kStreamTPL <= kp.n_traces)
+          walk_stream_mark<kStreamTPL, true>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces, base);
+        else
+          walk_stream_mark<kStreamTPL, false>(c, st, ng, kp.n_nodes, kp.t_static, kp.trace_begin, kp.n_traces, base);
+      } else if constexpr (KIND == 6) {
         CClose *cl = (CClose *)(const __attribute__((address_space(1))) StreamClose *)kp.closes;
         CU32 *ce = (CU32 *)(const __attribute__((address_space(1))) uint32_t *)kp.close_end;
         if (base + 64 * kStreamTPL <= kp.n_traces)
@@ -1140,7 +1289,10 @@ __global__ void __launch_bounds__(kWgThreads, KIND >= 4 ? ISIM_STREAM_WAVES : 1)
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
-  if constexpr (LDSC) {
+  if constexpr (KIND == 8) {  // the position marks, folded into the site counters by isim_mark_fold
+    for (uint32_t i = threadIdx.x; i < kp.mark_words; i += blockDim.x)
+      if (c.cnt[i]) atomicAdd(kp.stage + i, c.cnt[i]);
+  } else if constexpr (LDSC) {
     if (kp.stage) {  // draw stream: only the 500 counts are counted here (calls: isim_stream_calls)
       for (uint32_t i = threadIdx.x; i < kp.n_slots; i += blockDim.x)
         if (c.cnt[kp.n_slots + i]) atomicAdd(kp.stage + i, c.cnt[kp.n_slots + i]);
@@ -1179,11 +1331,16 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters) {
     case 5:  // the bit stack only exists in mode B
       if (!modeb) return pick<4>(false, lds_counters);
       return lds_counters ? (void *)&dev::isim_walk<5, true, true> : (void *)&dev::isim_walk<5, true, false>;
+    case 8:  // sparse ancestor marking: mode B, position marks in LDS only
+      if (!modeb) return pick<4>(false, lds_counters);
+      return lds_counters ? (void *)&dev::isim_walk<8, true, true> : nullptr;
     default:  // 6: the close list only exists in mode B
       if (!modeb) return pick<4>(false, lds_counters);
       return lds_counters ? (void *)&dev::isim_walk<6, true, true> : (void *)&dev::isim_walk<6, true, false>;
   }
 }
+
+void *mark_fold_kernel() { return (void *)&dev::isim_mark_fold; }
 
 void *stream_calls_kernel() { return (void *)&dev::isim_stream_calls; }
 void *fill_const_kernel() { return (void *)&dev::isim_fill_const; }

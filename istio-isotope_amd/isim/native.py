@@ -30,6 +30,7 @@ FLAG_WALK_ALL = 4  # draw-free static walks: walk every trace (default: one walk
 FLAG_BIT_STACK = 8  # mode B on the draw stream: the bit-stack kernel (kind 5/4) instead of the close list (6)
 FLAG_DYNAMIC = 16  # every walk on the general (dynamic) kernels, kind 7 (or 2/3)
 FLAG_WAVE_WALK = 32  # dynamic walks on the wave-walk interpreter (kinds 2/3) instead of the lane tree walk (7)
+FLAG_CLOSE_LIST = 64  # mode B on the draw stream: the close list (kind 6) instead of sparse ancestor marking (8)
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4

@@ -20,10 +20,11 @@ from parity import Case, assert_records_equal, with_defaults
 pytestmark = pytest.mark.gpu
 
 
-def _device_run(case: Case, begin: int, n: int, launches: int = 1):
+def _device_run(case: Case, begin: int, n: int, launches: int = 1, raw: bool = False):
     """`launches` consecutive isim_serve_device calls of n traces each (trace
     ids begin + i*n), records into one device buffer, ONE stats buffer
-    accumulated across them (bench.time_walk's pattern)."""
+    accumulated across them (bench.time_walk's pattern); raw: the stats
+    words themselves instead of their fold."""
     import torch
     h = case.handler
     dev = torch.device("cuda", 0)
@@ -39,7 +40,8 @@ def _device_run(case: Case, begin: int, n: int, launches: int = 1):
     rec["latency_ns"] = r[:, 0]
     rec["hops"] = (r[:, 1] & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     rec["status_err"] = (r[:, 1] >> np.uint64(32)).astype(np.uint32)
-    return rec, h.fold(stats.cpu().numpy().view(np.uint64))
+    st = stats.cpu().numpy().view(np.uint64)
+    return rec, (st if raw else h.fold(st))
 
 
 def _check_window(case: Case, rec, begin, s0, width):
@@ -188,10 +190,10 @@ def test_config3_bench_batch(gpu):
 
 def test_config3_bench_batch_mode_b(gpu):
     """config 3's graph in mode B with the informative errorRate
-    (bench.mode_b_legs "mode_b_informative"), the close-list kernel, 2^24
-    traces per launch, two launches into one stats buffer."""
+    (bench.mode_b_legs "mode_b_informative"), sparse ancestor marking (kind
+    8), 2^24 traces per launch, two launches into one stats buffer."""
     c = Case(config3_informative(), None, isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_WALK_ALL))
-    assert c.handler.launch_info(0)["kernel_kind"] == 6
+    assert c.handler.launch_info(0)["kernel_kind"] == 8
     n, L = bench.BENCH_BATCH["c3"], 2
     begin = 5 * n
     rec, f = _device_run(c, begin, n, L)
@@ -331,3 +333,27 @@ def test_config4w_bench_batch(gpu):
     _launch_edge_windows(c, rec, begin, n, L, width=128)
     _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=13)
     c.compare(begin + n - 2048, 4096)
+
+
+@pytest.mark.parametrize("informative", [True, False])
+def test_mode_b_marking_equals_close_list(gpu, informative):
+    """mode B by sparse ancestor marking (kind 8: +1 at
+    every erring invocation, -1 at the LCA of consecutive ones, subtree sums
+    per launch) against the independent close-list kernel (kind 6: every
+    calling invocation's subtree tested) on config 3's graph (~50 erring
+    invocations per trace at U[0,1%], ~0.5 at U[0,1e-4]), 2^22 traces of one
+    launch from a trace id crossing 2^32: records and every statistic equal
+    (executable.go:131-143, handler.go:66-75 with the 500 propagated)."""
+    j = config3_informative() if informative else obj_to_json(config3_topology())
+    n, begin = 1 << 22, (1 << 32) - (1 << 21)
+    out = []
+    for flags in (0, isim.native.FLAG_CLOSE_LIST):
+        c = Case(j, None, isim.SimParams(error_mode=isim.MODE_B, flags=isim.native.FLAG_WALK_ALL | flags))
+        assert c.handler.launch_info(0)["kernel_kind"] == (6 if flags else 8)
+        out.append(_device_run(c, begin, n, raw=True))
+    (r8, s8), (r6, s6) = out
+    assert np.array_equal(r8, r6)
+    # every stats word: header, histograms, per-site calls and per-site callee 500s
+    bad = np.nonzero(s8 != s6)[0]
+    assert bad.size == 0, f"stats words differ at {bad[:8].tolist()}"
+    assert int(s8[isim.native.ST_N_500]) > 0

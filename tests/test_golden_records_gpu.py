@@ -1,7 +1,7 @@
 """The committed per-trace record fixtures (tests/golden/records/, made once
 by the C oracle) reproduced by every HIP kernel kind
 through the C ABI, bit for bit: records and stats of the walks (draw stream,
-mode-B close list and bit stack, static interpreter, lane tree walk, wave
+mode-B ancestor marking, close list and bit stack, static interpreter, lane tree walk, wave
 walk) and records, stats and DES tables of the per-replica DES (32-bit rows
 with the automatic wide retry, and 64-bit rows).  Unlike the parity tests
 these compare with stored outputs, so no oracle runs here."""
@@ -20,6 +20,7 @@ KERNELS = {
     "default": 0,
     "stream_walk": N.FLAG_WALK_ALL,
     "bitstack": N.FLAG_WALK_ALL | N.FLAG_BIT_STACK,
+    "closelist": N.FLAG_WALK_ALL | N.FLAG_CLOSE_LIST,
     "interp": N.FLAG_NO_STREAM,
     "dynamic": N.FLAG_DYNAMIC,
     "dynamic_wave": N.FLAG_DYNAMIC | N.FLAG_WAVE_WALK,
@@ -47,8 +48,8 @@ def _expected_stats(case, fx, des=False):
 @pytest.mark.parametrize("kernel", list(KERNELS))
 @pytest.mark.parametrize("case", gr.WALK_CASES, ids=gr.case_id)
 def test_walk_matches_fixture(gpu, case, kernel):
-    if kernel == "bitstack" and case["params"]["error_mode"] == 0:
-        pytest.skip("the bit stack is a mode-B kernel")
+    if kernel in ("bitstack", "closelist") and case["params"]["error_mode"] == 0:
+        pytest.skip("the bit stack and the close list are mode-B kernels")
     fx = gr.load(case)
     _, h = _handler(case, KERNELS[kernel])
     recs, stats = h.serve(case["begin"], case["n"])

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 N = isim.native
 KERNELS = {
     "stream": 0,                                   # draw-free graphs: one walk + record fill
-    "stream_walk": N.FLAG_WALK_ALL,                # kinds 4 (mode A) / 6 (mode B close list)
+    "stream_walk": N.FLAG_WALK_ALL,                # kinds 4 (mode A) / 8 (mode B ancestor marking)
+    "closelist": N.FLAG_WALK_ALL | N.FLAG_CLOSE_LIST,  # mode B: kind 6 (the close list)
     "bitstack": N.FLAG_WALK_ALL | N.FLAG_BIT_STACK,  # mode B: kind 5
     "interp": N.FLAG_NO_STREAM,                    # static interpreter, kinds 0/1
     "dynamic": N.FLAG_DYNAMIC,                     # general path: the lane tree walk, kind 7
@@ -35,8 +36,8 @@ KERNELS = {
 def test_kat_hip(gpu, case, kernel):
     hop, req, resp, mode = kat.params(case)
     flags = KERNELS[kernel]
-    if kernel == "bitstack" and mode == 0:
-        pytest.skip("the bit stack is a mode-B kernel")
+    if kernel in ("bitstack", "closelist") and mode == 0:
+        pytest.skip("the bit stack and the close list are mode-B kernels")
     j = kat.graph_json(case["graph"])
     g = isim.ServiceGraph.from_json(j)
     h = isim.Handler(g, case["entry"], isim.SimParams(seed=1, hop_base_ns=hop, req_ps_per_byte=req,
@@ -49,6 +50,10 @@ def test_kat_hip(gpu, case, kernel):
         assert kind == 7 or (h.info.time_bits == 64 and kind == 3)
     elif kernel == "interp":
         assert kind in (0, 1) or not h.info.static_walk
+    elif kernel == "stream_walk" and mode == 1 and h.info.static_walk:
+        assert kind == 8
+    elif kernel == "closelist" and h.info.static_walk:
+        assert kind == 6
     n = 3000
     begin = (1 << 32) - 1500  # the batch straddles trace id 2^32
     recs, stats = h.serve(begin, n)

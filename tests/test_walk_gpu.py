@@ -27,10 +27,11 @@ def _fixture_json(path, error_rate=None):
 
 
 KERNELS = {"stream": 0, "interp": isim.native.FLAG_NO_STREAM, "bitstack": isim.native.FLAG_BIT_STACK,
+           "closelist": isim.native.FLAG_CLOSE_LIST,
            # the general path on every graph: the lane tree walk (kind 7) and the wave walk (kinds 2/3)
            "tree": isim.native.FLAG_DYNAMIC,
            "wave": isim.native.FLAG_DYNAMIC | isim.native.FLAG_WAVE_WALK}
-STREAM_KINDS = (4, 5, 6)
+STREAM_KINDS = (4, 5, 6, 8)
 
 
 def dynamic_kind(handler, flags):
@@ -57,7 +58,9 @@ def test_reference_topologies(gpu, path, mode, kernel):
         elif mode == isim.MODE_A:
             assert kind == 4
         elif kernel == "stream":
-            assert kind == 6  # mode B: the close list
+            assert kind == 8  # mode B: sparse ancestor marking
+        elif kernel == "closelist":
+            assert kind == 6
         else:
             assert kind == (5 if c.handler.info.max_depth <= 32 else 4)
     c.compare(0, 3000)
@@ -204,14 +207,17 @@ def test_mode_b_stack_depths(gpu, depth, kind):
     c.compare(5, 3000)
 
 
+@pytest.mark.parametrize("kind", [6, 8])
 @pytest.mark.parametrize("depth", [1, 2, 31, 33, 64])
 @pytest.mark.parametrize("fan", [0, 2, 40])
-def test_mode_b_close_list_depths(gpu, depth, fan):
-    # the close-list kernel (kind 6) has no depth limit; chains whose subtrees
-    # end inside, at and across the 32-record chunk boundaries
-    c = Case(_chain(depth, fan), None, isim.SimParams(error_mode=isim.MODE_B))
+def test_mode_b_close_list_depths(gpu, depth, fan, kind):
+    # the close-list kernel (kind 6) and sparse ancestor marking (kind 8) have
+    # no depth limit; chains whose subtrees end inside, at and across the
+    # 32-record chunk boundaries (kind 6), LCAs at every depth (kind 8)
+    flags = isim.native.FLAG_CLOSE_LIST if kind == 6 else 0
+    c = Case(_chain(depth, fan), None, isim.SimParams(error_mode=isim.MODE_B, flags=flags))
     assert c.handler.info.max_depth == depth
-    assert c.handler.launch_info(0)["kernel_kind"] == 6
+    assert c.handler.launch_info(0)["kernel_kind"] == kind
     c.compare(5, 3000)
     c.compare((1 << 32) - 700, 1500)
 
