@@ -102,6 +102,16 @@ typedef struct {
 #define ISIM_FLAG_CLOSE_LIST 64u /* mode B on the draw stream: the close-list kernel (kind 6) instead of sparse
                                     ancestor marking (kind 8, the default when its per-invocation mark table
                                     fits the LDS) */
+/* Independent-check paths (the same results by a different algorithm; tests
+ * compare them with the defaults at sizes the CPU oracle does not reach): */
+#define ISIM_FLAG_TREE_WIDE 128u      /* dynamic walks: the wide lane-tree format (16-byte nodes, 32-bit frames)
+                                         for any tree, not only past the 8-byte nodes' 16-bit fields */
+#define ISIM_FLAG_DES_SCAN_BY_KEY 256u /* DES item engine: every queue by rocPRIM's scan by key over max-plus maps
+                                         instead of the one-pass look-back scan (k_qscan) */
+#define ISIM_FLAG_DES_SORT_ALL 512u   /* DES item engine, cyclic schedules: sort every queue round of every pass
+                                         (no reuse of the previous pass's sorted order) */
+#define ISIM_FLAG_DES_TWO_SORTS 1024u /* DES item engine: every sorted queue round by two stable sorts (replica |
+                                         arrival, then service) instead of one combined key */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {

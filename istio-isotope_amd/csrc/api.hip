@@ -275,15 +275,14 @@ int build_device(isim_handler *h, int device, DevState &st) {
                                   p.tree_frames > isim::tree_reg_frames(p.tree_frames, p.tree_t64, p.tree_wide),
                                   p.tree_layout.nodes_lds != 0,
                                   (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
-                                  p.tree_layout.wg_per_cu == 2 && !std::getenv("ISIM_TREE_OCC1"), p.tree_t64,
+                                  p.tree_layout.wg_per_cu == 2, p.tree_t64,
                                   p.tree_wide);
     if (!st.kernel) return fail(ISIM_EHIP, "no lane-tree-walk kernel for this tree");
     st.lds_bytes = p.tree_layout.bytes;
     st.lds_counters = 1;
     // the workgroup size with the most resident waves per CU (registers and
     // the LDS layout both bound it: two 768-thread workgroups = 24 waves when
-    // the kernel fits 80 VGPRs and the layout half the LDS); ISIM_TREE_THREADS
-    // forces one (A/B experiments)
+    // the kernel fits 80 VGPRs and the layout half the LDS)
     HIPCHK(hipFuncSetAttribute((const void *)st.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)st.lds_bytes));
     uint32_t best_t = isim::kWgThreads, best_res = 0;
@@ -295,8 +294,6 @@ int build_device(isim_handler *h, int device, DevState &st) {
         best_t = t;
       }
     }
-    if (const char *e = std::getenv("ISIM_TREE_THREADS"); e && std::atoi(e) >= 64)
-      best_t = std::min<uint32_t>(isim::kWgThreads, (uint32_t)std::atoi(e) & ~63u);
     st.threads = best_t;
   }
   if (!p.static_walk && !tree) {
@@ -1056,6 +1053,7 @@ int isim_serve_des_device(isim_handler *h, const isim_des_params *dp, uint64_t t
     L.mean_ns = dp->mean_interarrival_ns;
     L.seed = h->params.seed;
     L.n_slots = (uint32_t)h->prog.n_slots;
+    L.flags = h->params.flags;
     L.pool = st->des_pool;
     isim::DesItemsReport rep{};
     L.report = &rep;

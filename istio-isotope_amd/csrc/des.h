@@ -240,6 +240,7 @@ struct DesItemsLaunch {
   isim_trace_rec *d_records;
   uint64_t n_traces, trace_begin, mean_ns, seed;
   uint32_t n_slots;
+  uint32_t flags;  // isim_params.flags (ISIM_FLAG_DES_*: the independent-check paths)
   void *pool;  // hipMemPool_t
   DesItemsReport *report;  // filled when the batch ends (null: none)
 };

@@ -2550,8 +2550,7 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       kp.chain_ticket = tickets + 4 * r + 2;
       bool n32 = false;
       if constexpr (sizeof(T) == 4) {
-        static const bool off = std::getenv("ISIM_DES_NO_PIPE32") != nullptr;  // A/B switch, read once
-        n32 = pl.pipe_n32 && !off;
+        n32 = pl.pipe_n32;
         if (n32) hipLaunchKernelGGL((des_down_pipe<T, true>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
       }
       if (!n32) hipLaunchKernelGGL((des_down_pipe<T, false>), dim3(sg.cnt), dim3(kDownThreads), 0, stream, kp);
@@ -2628,8 +2627,7 @@ static int des_rounds(const DesLaunch &L, dev::DesK k, uint32_t *tickets, hipStr
       k.splits = splits_for(width);
       bool n32 = false;
       if constexpr (sizeof(T) == 4) {
-        static const bool off = std::getenv("ISIM_DES_NO_UP32") != nullptr;  // A/B switch, read once
-        n32 = pl.up_n32 && !off;
+        n32 = pl.up_n32;
         if (n32) hipLaunchKernelGGL((des_up<T, true>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
       }
       if (!n32) hipLaunchKernelGGL((des_up<T, false>), dim3(k.splits, width), dim3(kDesUpThreads), 0, stream, k);
@@ -2725,7 +2723,6 @@ int des_launch(const DesLaunch &L, void *stream_) {
         return 1;
       if (!changed) break;
     }
-    if (std::getenv("ISIM_DES_DEBUG")) std::fprintf(stderr, "isim des: cyclic schedule, %u passes\n", p + 1);
     if (p == kMaxPasses) {
       static const uint32_t no_fixed_point = 2;
       if (hipMemcpyAsync(L.ovf, &no_fixed_point, 4, hipMemcpyHostToDevice, stream) != hipSuccess ||

@@ -172,8 +172,6 @@ struct K {
   // item the call step it failed at (kNone: it did not fail)
   uint32_t modeb;
   uint32_t *ifst;
-  uint32_t no_acc;                 // A/B timing only (ISIM_DES_ITEMS_NO_ACC): skip the callee-max atomics (wrong results)
-  uint32_t count_changes;          // ISIM_DES_DEBUG: changed[1] counts the values a quiet pass changed
   // a look-back that gave up after spin_limit polls (des_spin_limit) sets
   // *fault: the batch is not accumulated and des_items_launch fails
   uint32_t *fault;
@@ -189,8 +187,6 @@ __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t 
     if (diff && k.dnext) k.dnext[k.itr[item] >> k.cshift] = 1;
     const unsigned long long m = __ballot(diff);
     if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1u) {
-      // ISIM_DES_DEBUG: count the changed values (one atomic per wave)
-      if (k.count_changes) atomicAdd(k.changed + 1, (uint32_t)__popcll(m));
       if (__hip_atomic_load(k.changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(k.changed, 1u);
     }
   }
@@ -1274,7 +1270,7 @@ __global__ void __launch_bounds__(kT) k_fin(K k, const uint32_t *ids, uint64_t m
       }
       store_tracked(k, k.IF + i, F, i);
       const uint32_t par = k.ipar[i];
-      if (par != kNone && !k.no_acc)
+      if (par != kNone)
         atomicMax((unsigned long long *)(k.acc + (uint64_t)par * k.aw + p.kstep), (unsigned long long)F);
       if (k.quiet) continue;
       const uint32_t own = k.iown[i];
@@ -1455,10 +1451,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.k0 = (uint32_t)L.seed;
   k.k1 = (uint32_t)(L.seed >> 32);
   k.n_slots = L.n_slots;
-  k.no_acc = std::getenv("ISIM_DES_ITEMS_NO_ACC") != nullptr;
   k.modeb = pl.modeb ? 1u : 0u;
-  const bool debug = std::getenv("ISIM_DES_DEBUG") != nullptr;
-  k.count_changes = debug ? 1u : 0u;
   uint32_t max_reps = 1, max_row = 0;
   for (const DesPos &q : pl.pos) {
     max_reps = std::max(max_reps, q.reps);
@@ -1516,10 +1509,10 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   }
   k.spill = spill_buf;
   // the nodes in LDS (1024-thread workgroups, one per CU at these register
-  // counts) when they fit in 96 KB; ISIM_DES_ITEMS_GLOBAL_NODES: always global
+  // counts) when they fit in 96 KB
   k.n_nodes = L.n_nodes;
   const uint32_t lds_nodes = L.n_nodes * 8u;
-  const bool ldsn = !L.tree_wide && lds_nodes <= 96u * 1024u && !std::getenv("ISIM_DES_ITEMS_GLOBAL_NODES");
+  const bool ldsn = !L.tree_wide && lds_nodes <= 96u * 1024u ;
   auto launch = [&](auto kern, unsigned long long *w) {
     if (ldsn) {
       (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_nodes);
@@ -1656,7 +1649,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   k.fault = ovf + 2;
   k.spin_limit = des_spin_limit();
   uint64_t *mm = (uint64_t *)carve(parts[32]);
-  uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] how many (debug)
+  uint32_t *chg = (uint32_t *)(mm + 8);  // [0] a quiet pass changed a value, [1] (spare)
   uint32_t *op_k2 = (uint32_t *)carve(parts[33]);
   unsigned long long *op_v2 = (unsigned long long *)carve(parts[34]);
   uint32_t *d_soff = (uint32_t *)carve(parts[35]);
@@ -1680,10 +1673,11 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint32_t *ifst = (uint32_t *)carve(parts[52]);
   k.ifst = pl.modeb ? ifst : nullptr;
   // the rounds' queues by k_qscan (its keys a - j h need j h < 2^62), else
-  // rocPRIM's scan by key over the maps and k_qout (A/B: ISIM_DES_ITEMS_SCAN_BY_KEY)
+  // rocPRIM's scan by key over the maps and k_qout (ISIM_FLAG_DES_SCAN_BY_KEY:
+  // always, an independent check of k_qscan)
   uint64_t max_hold = 0;
   for (uint64_t hv : row_hold) max_hold = std::max(max_hold, hv);
-  const bool qscan = std::getenv("ISIM_DES_ITEMS_SCAN_BY_KEY") == nullptr &&
+  const bool qscan = !(L.flags & ISIM_FLAG_DES_SCAN_BY_KEY) &&
                      (max_hold == 0 || M <= (1ull << 62) / max_hold);
   QState *qstate = (QState *)mp_out;  // mp_out's bytes: >= 32 B per 512 items
   uint32_t qepoch = 0, qtbase = 0;
@@ -1791,17 +1785,9 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       }
     }
     const uint32_t row_bits = bits_for(max_row);
-    // A/B switch: always the two-sort queue path
-    const bool two_sorts = std::getenv("ISIM_DES_ITEMS_TWO_SORTS") != nullptr;
-    // A/B switch: never skip an unchanged round
-    const bool no_skip = std::getenv("ISIM_DES_ITEMS_NO_SKIP") != nullptr;
-    // A/B switch: quiet passes with the statistics pass's 16 items per lane
-    const bool fat_quiet = std::getenv("ISIM_DES_ITEMS_FAT_QUIET") != nullptr;
-    uint32_t stats_span = kQSpan;  // A/B: ISIM_DES_ITEMS_STATS_SPAN (1..64)
-    if (const char *e = std::getenv("ISIM_DES_ITEMS_STATS_SPAN")) {
-      const long v = std::strtol(e, nullptr, 10);
-      if (v >= 1 && v <= 64) stats_span = (uint32_t)v;
-    }
+    // ISIM_FLAG_DES_TWO_SORTS: always the two-sort queue path (an independent check)
+    const bool two_sorts = (L.flags & ISIM_FLAG_DES_TWO_SORTS) != 0;
+    constexpr uint32_t stats_span = kQSpan;
     // 4. rounds; a cyclic schedule: quiet passes from zero (a lower bound of
     // every time: the iteration only raises values) until no stored value
     // changes, then the pass that records the statistics (des.hip des_launch)
@@ -1810,16 +1796,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     // never carried over); a cut step begin reads the last computed ones
     // (k_acc_init moves them to acc_prev).  After the first pass a quiet pass
     // recomputes only the items of the trace chunks the previous pass
-    // changed (k.dcur; ISIM_DES_ITEMS_NO_INCR: every item)
+    // changed (k.dcur)
     uint32_t qn = 0;       // k_qarr launches: the arrival-range slot alternates
-    uint64_t skipped = 0;  // queue rounds a quiet pass skipped (ISIM_DES_DEBUG)
-    uint64_t reused = 0;   // queue sorts a kept order replaced (ISIM_DES_DEBUG)
-    // A/B switch: never reuse a kept order
-    const bool keep_ord = pl.cyclic && std::getenv("ISIM_DES_ITEMS_NO_ORDER_REUSE") == nullptr;
+    // ISIM_FLAG_DES_SORT_ALL: never reuse a kept order (an independent check)
+    const bool keep_ord = pl.cyclic && !(L.flags & ISIM_FLAG_DES_SORT_ALL);
     std::vector<uint8_t> have_ord(R, 0);
     std::vector<uint64_t> rlo(R, ~0ull), rhi(R, 0);  // per sort round: its arrival range over the passes
-    // A/B switch: every quiet pass recomputes every item
-    const bool no_incr = std::getenv("ISIM_DES_ITEMS_NO_INCR") != nullptr;
     // k_qscan's states (their epochs: 1, 2, ... per launch) and ticket
     if (qscan && (hipMemsetAsync(qstate, 0, al256((M + 511) / 512 * sizeof(QState)), s) != hipSuccess ||
                   hipMemsetAsync(qticket, 0, 4, s) != hipSuccess)) {
@@ -1831,7 +1813,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
     // items per lane of k_qout / k_fin: runs of one row / position summed
     // before the statistics atomics; a quiet pass records none, and one item
     // per lane gives its finish groups (~0.8 M items on c4d) 16x the waves
-    const uint32_t span = kk.quiet && !fat_quiet ? 1u : stats_span;
+    const uint32_t span = kk.quiet ? 1u : stats_span;
     for (uint32_t r = 0; r < R && !rc; ++r) {
       if (soff[r + 1] > soff[r])
         hipLaunchKernelGGL(k_steps, dim3(grid_for(soff[r + 1] - soff[r])), dim3(kT), 0, s, kk, op_v2 + soff[r],
@@ -1855,7 +1837,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         // previous pass's keeps its starts (its queues are skipped)
         // (sort rounds only: they read the range back anyway; a sort-free
         // round would pay a stream synchronisation for the check)
-        const bool may_skip = kk.quiet && !kk.first && !nosort && !no_skip;
+        const bool may_skip = kk.quiet && !kk.first && !nosort;
         // range, change flag, kept-order flag (k_ordchk)
         uint64_t hmm[4] = {0, 0, 1, 1};
         if ((!nosort || may_skip) &&
@@ -1865,7 +1847,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         }
         const bool bad = hmm[3] != 0;
         if (may_skip && !hmm[2]) {
-          ++skipped;
           goto finishes;
         }
         if (!nosort) {
@@ -1882,7 +1863,6 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         QSrc qsrc{qids + qoff[r], ord + qoff[r], key_b, val_b, hmm[0], rep_bits, ab, rk_a, rk_b, sid, mp_in};
         int qsk = kQArrays;
         if (chk && !bad) {  // the kept order holds: no sort
-          ++reused;
           qsk = kQKept;
           if (!qscan)
             hipLaunchKernelGGL(k_pairs1o, dim3(grid_for(m)), dim3(kT), 0, s, kk, m, (const uint32_t *)(ord + qoff[r]),
@@ -1987,7 +1967,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         kq.first = p == 0 ? 1u : 0u;
         // the first pass recomputes everything; later ones the chunks the
         // previous pass changed
-        kq.dcur = p == 0 || no_incr ? nullptr : chg_a;
+        kq.dcur = p == 0 ? nullptr : chg_a;
         kq.dnext = chg_b;
         pass(kq);
         if (rc) break;
@@ -1998,22 +1978,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
           break;
         }
         rep.passes = p + 2;  // the quiet passes so far and the recording pass
-        if (debug) {
-          // and the trace chunks the next pass recomputes
-          std::vector<uint8_t> ch(n_chunks);
-          uint64_t live_n = 0;
-          if (hipMemcpy(ch.data(), chg_a, n_chunks, hipMemcpyDeviceToHost) == hipSuccess)
-            for (uint8_t c : ch) live_n += c != 0;
-          std::fprintf(stderr, "isim des items: pass %u changed %u values, %llu of %llu trace chunks live\n", p + 1,
-                       changed[1], (unsigned long long)live_n, (unsigned long long)n_chunks);
-        }
         if (!changed[0]) break;
       }
-      if (debug)
-        std::fprintf(stderr,
-                   "isim des items: cyclic schedule, %u passes, %llu unchanged queue rounds skipped, %llu sorts "
-                   "replaced by the kept order\n",
-                   p + 1, (unsigned long long)skipped, (unsigned long long)reused);
       if (!rc && p == kMaxPasses) {
         static const uint32_t one = 1;
         if (hipMemcpyAsync(ovf + 1, &one, 4, hipMemcpyHostToDevice, s) != hipSuccess) rc = fail("flag");

@@ -526,9 +526,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
     out.pipe_n32 = out.pipe_n32 && ps.hold < kDesN32HoldMax && ps.off < (1ull << 30) &&
                    (!(ps.flags & kDesFlagFused) || ps.floor < (1ull << 30));
   }
-  // finishes without the start row (kDesFlagNoStart; ISIM_DES_NO_NOSTART
-  // set: off, for A/B measurements)
-  if (!out.items && !out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_NOSTART")) {
+  // finishes without the start row (kDesFlagNoStart)
+  if (!out.items && !out.general && !out.cyclic) {
     for (uint32_t v = 0; v < np; ++v) {
       if ((out.pos[v].flags & kDesFlagFused) || kids[v].empty()) continue;
       const ScriptShape &sh = shape[pos_svc[v]];
@@ -540,9 +539,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
   }
   // durations recorded by the caller (des.hip des_up): one call step per
   // script (every arrival is start(caller) + off), no fixed-point passes, the
-  // caller's first kDesDurKids non-fused callees (ISIM_DES_NO_PARENT_DUR set:
-  // every position records its own, for A/B measurements)
-  if (!out.items && !out.general && !out.cyclic && !std::getenv("ISIM_DES_NO_PARENT_DUR")) {
+  // caller's first kDesDurKids non-fused callees
+  if (!out.items && !out.general && !out.cyclic) {
     for (uint32_t v = 0; v < np; ++v) {
       if (kids[v].size() > kDesUpChildLds) continue;
       uint32_t j = 0;

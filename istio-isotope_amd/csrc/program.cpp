@@ -93,8 +93,8 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   const uint32_t P = (uint32_t)out.tree_nodes_w.size(), S = (uint32_t)out.n_slots;
   const uint32_t R = (uint32_t)out.row_svc.size();
   const uint32_t head = kLdsAccBytes + kHistWords * 4u + kTreeLutBytes;  // + the duration-bucket LUT
-  // per-slot counters: guarded 16-bit pairs (4 B per slot; ISIM_TREE_CNT32 set: two u32, A/B measurements)
-  const uint32_t cb = std::getenv("ISIM_TREE_CNT32") ? 8u : 4u;
+  // per-slot counters: guarded 16-bit pairs (4 B per slot)
+  const uint32_t cb = 4u;
   // rows by heat (the entry's row, 0, is the end-to-end histogram: no LDS row)
   std::vector<uint32_t> order;
   for (uint32_t r = 1; r < R; ++r)
@@ -107,17 +107,14 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
   const Cand cands[4] = {{true, kTreeLdsHalf}, {true, kTreeLdsFull}, {false, kTreeLdsHalf}, {false, kTreeLdsFull}};
   int pick = -1;
   // wide rows unless they do not all fit in any candidate and compact ones
-  // hold more (ISIM_TREE_COMPACT / ISIM_TREE_WIDE force one: A/B measurements)
+  // hold more
   bool compact = false;
-  // ISIM_TREE_NODES_GLOBAL set: only the layouts with the nodes in global memory (A/B measurements)
-  // ISIM_TREE_NODES_LDS set: only the layouts with the nodes in LDS (A/B measurements)
-  const int first = std::getenv("ISIM_TREE_NODES_GLOBAL") ? 2 : 0;
-  const int last = std::getenv("ISIM_TREE_NODES_LDS") ? 2 : 4;
+  const int first = 0, last = 4;
   // walks deeper than 8 calling invocations run kernels built for 4 waves per
   // SIMD (tree.hip): one 1024-thread workgroup per CU whatever the layout, so
   // the half-CU layouts would only leave LDS unused
   const bool one_wg = out.tree_frames > 8;
-  const bool force_c = std::getenv("ISIM_TREE_COMPACT") != nullptr, force_w = std::getenv("ISIM_TREE_WIDE") != nullptr;
+  const bool force_c = false, force_w = false;
   // passes: every row fits (wide, then compact), else the fixed part fits (compact: more rows)
   for (int pass = 0; pass < 3 && pick < 0; ++pass) {
     compact = force_c || (!force_w && pass >= 1);
@@ -185,11 +182,12 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
 // the reason in out.tree_why when the walk does not fit it.  A tree past the
 // 8-byte nodes' 16-bit fields (positions, call sites, rows) or whose per-slot
 // counters do not fit in LDS is built WIDE (kernel_abi.h TreeNodeW;
-// ISIM_TREE_FORCE_WIDE set: always, for tests and A/B measurements).
+// ISIM_FLAG_TREE_WIDE: always, an independent check of the narrow format).
 constexpr uint32_t kTreeMaxWidePositions = 1u << 24;
 static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Site> &sites,
                        const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
-                       const std::vector<uint64_t> &tmin, const std::vector<char> &leaf, bool modeb) {
+                       const std::vector<uint64_t> &tmin, const std::vector<char> &leaf, bool modeb,
+                       bool force_wide) {
   out.tree_nodes.clear();
   out.tree_nodes_w.clear();
   out.tree_ext.clear();
@@ -207,7 +205,8 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   // figures (hop cost, callee time, step facts, leaf latency) stay 32-bit
   out.tree_t64 = out.max_latency >= (1ull << 32);
   constexpr uint64_t k32 = 1ull << 32;
-  bool wide = std::getenv("ISIM_TREE_FORCE_WIDE") != nullptr || out.n_slots > (int32_t)kTreeMaxPositions;
+  // ISIM_FLAG_TREE_WIDE: the wide format for any tree (an independent check of the narrow one)
+  bool wide = force_wide || out.n_slots > (int32_t)kTreeMaxPositions;
   if ((uint32_t)out.n_slots >= kSlotRoot) return give_up("more than 2^24 call sites");
   const int32_t n = (int32_t)g.services.size();
   std::vector<ScriptTimes> shape(n);
@@ -815,7 +814,8 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     err = "program too large";
     return ISIM_EINVAL;
   }
-  if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf, p.error_mode == ISIM_MODE_B);
+  if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf, p.error_mode == ISIM_MODE_B,
+                                        (p.flags & ISIM_FLAG_TREE_WIDE) != 0);
   return ISIM_OK;
 }
 

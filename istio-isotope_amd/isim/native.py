@@ -31,6 +31,11 @@ FLAG_BIT_STACK = 8  # mode B on the draw stream: the bit-stack kernel (kind 5/4)
 FLAG_DYNAMIC = 16  # every walk on the general (dynamic) kernels, kind 7 (or 2/3)
 FLAG_WAVE_WALK = 32  # dynamic walks on the wave-walk interpreter (kinds 2/3) instead of the lane tree walk (7)
 FLAG_CLOSE_LIST = 64  # mode B on the draw stream: the close list (kind 6) instead of sparse ancestor marking (8)
+# independent-check paths (isim.h): the same results by a different algorithm
+FLAG_TREE_WIDE = 128  # the wide lane-tree format for any dynamic walk
+FLAG_DES_SCAN_BY_KEY = 256  # DES items: queues by rocPRIM's scan by key (not k_qscan)
+FLAG_DES_SORT_ALL = 512  # DES items, cyclic schedules: sort every round of every pass
+FLAG_DES_TWO_SORTS = 1024  # DES items: two stable sorts per sorted queue round
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4

@@ -144,7 +144,7 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> terr(n);
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
   const tw::CpuNodesW nodes_w{prog.tree_nodes_w.data()};
-  if (prog.tree_wide) {  // a wide tree (ISIM_TREE_FORCE_WIDE): 16-byte nodes, 32-bit frames
+  if (prog.tree_wide) {  // a wide tree (ISIM_FLAG_TREE_WIDE or past the 8-byte nodes): 16-byte nodes, 32-bit frames
     if (modeb) walk_all<true, true>(prog, nodes_w, seed, begin, n, items, dur_of, toff, terr);
     else walk_all<false, true>(prog, nodes_w, seed, begin, n, items, dur_of, toff, terr);
   } else {

@@ -106,6 +106,7 @@ int main(int argc, char **argv) {
   p.req_ps_per_byte = std::strtoull(argv[5], nullptr, 0);
   p.resp_ps_per_byte = std::strtoull(argv[6], nullptr, 0);
   p.flags = ISIM_FLAG_DYNAMIC;  // static graphs too: the tree walk is the general path
+  if (std::getenv("ISIM_TW_WIDE")) p.flags |= ISIM_FLAG_TREE_WIDE;  // every tree in the wide format
   const uint64_t begin = std::strtoull(argv[7], nullptr, 0), n = std::strtoull(argv[8], nullptr, 0);
   Program prog;
   if (compile_program(g, entry, p, prog, err) != ISIM_OK) {

@@ -209,11 +209,10 @@ def test_items_device_entry_accumulates(gpu):
 
 
 @pytest.mark.parametrize("name", ["real300p60", "tree_reps_p70", "canonical_p50"])
-def test_items_two_sort_queue_path(gpu, name, monkeypatch):
+def test_items_two_sort_queue_path(gpu, name):
     # the fallback queue path (replica | arrival, then the row: two stable
     # sorts), taken when row | replica | arrival does not fit one 64-bit key
-    monkeypatch.setenv("ISIM_DES_ITEMS_TWO_SORTS", "1")
-    DesCase(CASES[name](), 500_000).compare(31, 2500)
+    DesCase(CASES[name](), 500_000, flags=native.FLAG_DES_TWO_SORTS).compare(31, 2500)
 
 
 def test_items_c5p_bench_batch_sparse_load(gpu):
@@ -247,12 +246,12 @@ def test_items_c5p_bench_batch_sparse_load(gpu):
 
 
 @pytest.mark.parametrize("mean", [50_000, 400_000])
-def test_items_kept_queue_order(gpu, mean, monkeypatch):
+def test_items_kept_queue_order(gpu, mean):
     """A cyclic schedule's quiet passes reuse a sort round's previous sorted
     order when it still sorts the new arrivals (k_ordchk / k_pairs1o); under
     heavy and light contention, at a size where some kept orders hold and
     some fail, everything equals the run that sorts every round
-    (ISIM_DES_ITEMS_NO_ORDER_REUSE) and, at a smaller size, the oracle."""
+    (ISIM_FLAG_DES_SORT_ALL) and, at a smaller size, the oracle."""
     c = DesCase(CASES["mesh_des"](), mean)
     assert c.d.info.items == 1 and c.d.info.cyclic == 1
     recs, _, _ = c.compare(7, 1500)
@@ -261,18 +260,17 @@ def test_items_kept_queue_order(gpu, mean, monkeypatch):
     assert rep["passes"] >= 2 and rep["syncs"] >= rep["passes"] and rep["items"] == int(recs["hops"].sum())
     n = 40_000
     got = c.d.serve(1 << 20, n, device=0)
-    monkeypatch.setenv("ISIM_DES_ITEMS_NO_ORDER_REUSE", "1")
-    ref = c.d.serve(1 << 20, n, device=0)
+    ref = DesCase(CASES["mesh_des"](), mean, flags=native.FLAG_DES_SORT_ALL).d.serve(1 << 20, n, device=0)
     assert np.array_equal(got[0], ref[0])
     assert np.array_equal(np.asarray(got[1]), np.asarray(ref[1]))
     assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))
 
 
-def _bench_case(cfg):
+def _bench_case(cfg, flags=0):
     import bench
     j, _ = bench.build_graph(cfg)
     mean = 150_000 if cfg == "c4d" else 6_000_000  # bench.py's default gaps
-    return DesCase(j, mean), bench.BENCH_BATCH[cfg]
+    return DesCase(j, mean, flags=flags), bench.BENCH_BATCH[cfg]
 
 
 def test_items_c5p_bench_graph_and_load(gpu):
@@ -335,33 +333,34 @@ def test_items_c3s_u64_walk(gpu):
 
 
 @pytest.mark.parametrize("name", ["real300p60", "canonical_p50", "mesh_des"])
-def test_items_wide_tree(gpu, monkeypatch, name):
-    """The item engine over a wide tree (ISIM_TREE_FORCE_WIDE: 16-byte nodes,
+def test_items_wide_tree(gpu, name):
+    """The item engine over a wide tree (ISIM_FLAG_TREE_WIDE: 16-byte nodes,
     32-bit frames in the pre-walk; positions past 16 bits in the records and
     the renumbering sort), modes A and B, against the oracle."""
-    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
-    DesCase(CASES[name](), 300_000).compare(1000, 3000)
-    DesCase(MODE_B_CASES["seq_tree_abort"](), 300_000, error_mode=isim.MODE_B).compare(9, 2000)
+    W = native.FLAG_TREE_WIDE
+    DesCase(CASES[name](), 300_000, flags=W).compare(1000, 3000)
+    DesCase(MODE_B_CASES["seq_tree_abort"](), 300_000, error_mode=isim.MODE_B, flags=W).compare(9, 2000)
 
 
 @pytest.mark.parametrize("case", ["c5p", "c4d", "mesh_heavy"])
-def test_items_qscan_equals_scan_by_key(gpu, monkeypatch, case):
+def test_items_qscan_equals_scan_by_key(gpu, case):
     """The one-pass queue kernel (k_qscan: a segmented prefix max of
     a_i - i*h with a decoupled look-back across thousands of tiles) against
     the independent path it replaced (rocPRIM's scan by key over max-plus
-    maps, then k_qout; ISIM_DES_ITEMS_SCAN_BY_KEY) at sizes where the rounds
+    maps, then k_qout; ISIM_FLAG_DES_SCAN_BY_KEY) at sizes where the rounds
     span thousands of tiles and queue segments span many of them: records,
     statistics and the DES table identical.  c5p at its bench batch and gap,
     c4d at 2^21 of its bench gap (cyclic, kept orders), and the mesh under
     heavy contention (waits far above the holds: long carries)."""
-    if case == "mesh_heavy":
-        d, n = DesCase(CASES["mesh_des"](), 20_000).d, 300_000
-    else:
-        c, n = _bench_case(case)
-        d, n = c.d, (n if case == "c5p" else 1 << 21)
+    def handler(flags):
+        if case == "mesh_heavy":
+            return DesCase(CASES["mesh_des"](), 20_000, flags=flags).d, 300_000
+        c, n = _bench_case(case, flags)
+        return c.d, (n if case == "c5p" else 1 << 21)
+
+    d, n = handler(0)
     got = d.serve(1 << 22, n, device=0)
-    monkeypatch.setenv("ISIM_DES_ITEMS_SCAN_BY_KEY", "1")
-    ref = d.serve(1 << 22, n, device=0)
+    ref = handler(native.FLAG_DES_SCAN_BY_KEY)[0].serve(1 << 22, n, device=0)
     assert np.array_equal(got[0], ref[0])
     assert np.array_equal(np.asarray(got[1]), np.asarray(ref[1]))
     assert np.array_equal(np.asarray(got[2]), np.asarray(ref[2]))

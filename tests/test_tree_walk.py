@@ -234,9 +234,10 @@ def test_u64_time(checker, tmp_path, mode):
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_forced_wide(checker, tmp_path, monkeypatch, mode):
-    """Every tree shape in the wide format (ISIM_TREE_FORCE_WIDE): meshes,
-    concurrent and sequential realistic graphs, the spilling depths, u64 time."""
-    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
+    """Every tree shape in the wide format (ISIM_FLAG_TREE_WIDE, set by the
+    checker under ISIM_TW_WIDE): meshes, concurrent and sequential realistic
+    graphs, the spilling depths, u64 time."""
+    monkeypatch.setenv("ISIM_TW_WIDE", "1")
     assert compare(checker, tmp_path, with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
                    mode, n=1000, wide=True)
     deep = realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2), probability=70)

@@ -443,18 +443,17 @@ def test_tree_u64_time(gpu, mode):
 # the hottest call sites counted in LDS, the rest by global atomics (tree.hip
 # WideSink; isim_launch_info.tree_wide)
 @pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
-def test_tree_wide_forced(gpu, monkeypatch, mode):
-    """Every tree shape in the wide format (ISIM_TREE_FORCE_WIDE): a mesh,
+def test_tree_wide_forced(gpu, mode):
+    """Every tree shape in the wide format (ISIM_FLAG_TREE_WIDE): a mesh,
     a deep concurrent realistic graph, a 40-deep chain (spilled frames), u64
     time — bit-exact against the oracle on windows across 2^32."""
-    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
     docs = [with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
             obj_to_json(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2),
                                            probability=70)),
             _prob_chain(40),
             obj_to_json(realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.1), probability=75))]
     for j in docs:
-        c = Case(j, None, isim.SimParams(error_mode=mode))
+        c = Case(j, None, isim.SimParams(error_mode=mode, flags=isim.native.FLAG_TREE_WIDE))
         li = c.handler.launch_info(0)
         assert li["kernel_kind"] == 7 and li["tree_wide"] == 1
         c.compare(1000, 3000)
@@ -472,7 +471,7 @@ def test_tree_wide_by_size(gpu):
     c.compare(77, 2000)
 
 
-def test_tree_wide_equals_narrow(gpu, monkeypatch):
+def test_tree_wide_equals_narrow(gpu):
     """2^24 traces of one graph on the 8-byte kernel and forced wide: equal
     records and statistics word for word — at that size a workgroup counts
     more than 2^15 calls at the hot sites, so the wide sink's guarded LDS
@@ -482,8 +481,7 @@ def test_tree_wide_equals_narrow(gpu, monkeypatch):
     narrow = Case(j, None, isim.SimParams())
     assert narrow.handler.launch_info(0)["tree_wide"] == 0
     r1, s1 = narrow.gpu(12345, n)
-    monkeypatch.setenv("ISIM_TREE_FORCE_WIDE", "1")
-    wide = Case(j, None, isim.SimParams())
+    wide = Case(j, None, isim.SimParams(flags=isim.native.FLAG_TREE_WIDE))
     assert wide.handler.launch_info(0)["tree_wide"] == 1
     r2, s2 = wide.gpu(12345, n)
     assert np.array_equal(r1, r2)
