@@ -187,9 +187,10 @@ struct close_rec<S, decltype((void)S::kCloseRec)> {
 // drawn once, when it opens, and kept in its frame (f_res), so returning from
 // a callee never recomputes the caller's block and the scans need no draw.
 // CONC: the walk has concurrent steps (without them no frame keeps a step max).
-// SPILL: calling invocations deeper than FRAMES below the current one are kept
-// in memory at sp[(level * kTreeSpillWords + word) * sp_stride] (the kernel:
-// global memory, one column per lane; the CPU check: a vector).
+// SPILL: the FRAMES register frames are a ring over the top of the stack; the
+// calling invocations below it are kept in memory at sp[(level *
+// kTreeSpillWords + word) * sp_stride] (the kernel: global memory, one column
+// per lane; the CPU check: a vector).
 // DRAW: some callee draws its error against a threshold (without, no error
 // block is cached: 5 registers fewer).
 // TT: the time type — uint32_t when the walk's latency bound is below 2^32
@@ -271,6 +272,8 @@ struct Lane {
     he = 0;
     he_err = 0;
     d = 0;
+    lo = 0;
+    hs = 0;
     ek_blk = 0xFFFFFFFFu;  // the error block belongs to the previous trace of the lane
     p = 0;
     end = 1;
@@ -287,37 +290,97 @@ struct Lane {
     }
   }
 
+  // SPILL (round 6): the register frames are a ring holding the TOP of the
+  // stack — frames [lo, d) in slots (hs - (d - lo)) .. hs - 1 mod FRAMES —
+  // and only frames below lo live in memory, at level = frame index.  A push
+  // onto a full ring evicts its oldest frame (frame lo, in the slot the new
+  // frame takes); a pop from an empty ring reads its frame from memory.  A walk
+  // that moves up and down within FRAMES levels (the deep subtrees, where most
+  // calling invocations are) touches no memory; the old layout (frames below
+  // FRAMES in registers, every deeper push and pop in memory) paid a frame's
+  // write and read for each of them.
+  uint32_t lo = 0, hs = 0;
+  ISIM_TW void ring_put(uint32_t slot, uint32_t pe, uint32_t hf, uint32_t res, TT acc, TT cmax, uint32_t en,
+                        uint32_t hp) {
+TW_PRAGMA_UNROLL
+    for (int i = 0; i < FRAMES; ++i) {
+      const bool m = slot == (uint32_t)i;
+      s_pe[i] = m ? pe : s_pe[i];
+      s_hf[i] = m ? hf : s_hf[i];
+      s_res[i] = m ? res : s_res[i];
+      s_acc[i] = m ? acc : s_acc[i];
+      if (CONC) s_cmax[i] = m ? cmax : s_cmax[i];
+      if (W) {
+        s_end[i] = m ? en : s_end[i];
+        s_hop[i] = m ? hp : s_hop[i];
+      }
+    }
+  }
+  ISIM_TW void ring_get(uint32_t slot, uint32_t &pe, uint32_t &hf, uint32_t &r, TT &a, TT &c, uint32_t &en,
+                        uint32_t &hp) const {
+TW_PRAGMA_UNROLL
+    for (int i = 0; i < FRAMES; ++i) {
+      const bool m = slot == (uint32_t)i;
+      pe = m ? s_pe[i] : pe;
+      hf = m ? s_hf[i] : hf;
+      r = m ? s_res[i] : r;
+      a = m ? s_acc[i] : a;
+      if (CONC) c = m ? s_cmax[i] : c;
+      if (W) {
+        en = m ? s_end[i] : en;
+        hp = m ? s_hop[i] : hp;
+      }
+    }
+  }
+  ISIM_TW void mem_put(uint32_t level, uint32_t pe, uint32_t hf, uint32_t res, TT acc, TT cmax, uint32_t en,
+                       uint32_t hp) {
+    uint32_t *q = sp + level * kSW * sp_stride;
+    q[0] = pe;
+    q[sp_stride] = hf;
+    q[2 * sp_stride] = res;
+    q[3 * sp_stride] = (uint32_t)acc;
+    q[4 * sp_stride] = (uint32_t)cmax;
+    if constexpr (sizeof(TT) == 8) {
+      q[5 * sp_stride] = (uint32_t)((uint64_t)acc >> 32);
+      q[6 * sp_stride] = (uint32_t)((uint64_t)cmax >> 32);
+    }
+    if constexpr (W) {
+      q[kSW0 * sp_stride] = en;
+      q[(kSW0 + 1) * sp_stride] = hp;
+    }
+  }
+  ISIM_TW void mem_get(uint32_t level, uint32_t &pe, uint32_t &hf, uint32_t &r, TT &a, TT &c, uint32_t &en,
+                       uint32_t &hp) const {
+    const uint32_t *q = sp + level * kSW * sp_stride;
+    pe = q[0];
+    hf = q[sp_stride];
+    r = q[2 * sp_stride];
+    a = q[3 * sp_stride];
+    c = q[4 * sp_stride];
+    if constexpr (sizeof(TT) == 8) {
+      a |= (TT)((uint64_t)q[5 * sp_stride] << 32);
+      c |= (TT)((uint64_t)q[6 * sp_stride] << 32);
+    }
+    if constexpr (W) {
+      en = q[kSW0 * sp_stride];
+      hp = q[(kSW0 + 1) * sp_stride];
+    }
+  }
+
   ISIM_TW void push() {
     const uint32_t pe = W ? f_pos : f_pos | (end << 16), hf = f_hf;
-    if (SPILL && d >= (uint32_t)FRAMES) {
-      uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
-      q[0] = pe;
-      q[sp_stride] = hf;
-      q[2 * sp_stride] = f_res;
-      q[3 * sp_stride] = (uint32_t)f_acc;
-      q[4 * sp_stride] = (uint32_t)f_cmax;
-      if constexpr (sizeof(TT) == 8) {
-        q[5 * sp_stride] = (uint32_t)((uint64_t)f_acc >> 32);
-        q[6 * sp_stride] = (uint32_t)((uint64_t)f_cmax >> 32);
+    if constexpr (SPILL) {
+      if (d - lo == (uint32_t)FRAMES) {  // a full ring: its oldest frame (in slot hs) to memory
+        uint32_t ope = 0, ohf = 0, ores = 0, oen = 0, ohp = 0;
+        TT oacc = 0, ocm = 0;
+        ring_get(hs, ope, ohf, ores, oacc, ocm, oen, ohp);
+        mem_put(lo, ope, ohf, ores, oacc, ocm, oen, ohp);
+        ++lo;
       }
-      if constexpr (W) {
-        q[kSW0 * sp_stride] = end;
-        q[(kSW0 + 1) * sp_stride] = f_hop;
-      }
+      ring_put(hs, pe, hf, f_res, f_acc, f_cmax, end, f_hop);
+      hs = hs + 1u == (uint32_t)FRAMES ? 0u : hs + 1u;
     } else {
-TW_PRAGMA_UNROLL
-      for (int i = 0; i < FRAMES; ++i) {
-        const bool m = d == (uint32_t)i;
-        s_pe[i] = m ? pe : s_pe[i];
-        s_hf[i] = m ? hf : s_hf[i];
-        s_res[i] = m ? f_res : s_res[i];
-        s_acc[i] = m ? f_acc : s_acc[i];
-        if (CONC) s_cmax[i] = m ? f_cmax : s_cmax[i];
-        if (W) {
-          s_end[i] = m ? end : s_end[i];
-          s_hop[i] = m ? f_hop : s_hop[i];
-        }
-      }
+      ring_put(d, pe, hf, f_res, f_acc, f_cmax, end, f_hop);
     }
     ++d;
   }
@@ -326,35 +389,16 @@ TW_PRAGMA_UNROLL
     --d;
     uint32_t pe = 0, hf = 0, r = 0, en = 0, hp = 0;
     TT a = 0, c = 0;
-    if (SPILL && d >= (uint32_t)FRAMES) {
-      const uint32_t *q = sp + (d - (uint32_t)FRAMES) * kSW * sp_stride;
-      pe = q[0];
-      hf = q[sp_stride];
-      r = q[2 * sp_stride];
-      a = q[3 * sp_stride];
-      c = q[4 * sp_stride];
-      if constexpr (sizeof(TT) == 8) {
-        a |= (TT)((uint64_t)q[5 * sp_stride] << 32);
-        c |= (TT)((uint64_t)q[6 * sp_stride] << 32);
-      }
-      if constexpr (W) {
-        en = q[kSW0 * sp_stride];
-        hp = q[(kSW0 + 1) * sp_stride];
+    if constexpr (SPILL) {
+      if (d >= lo) {
+        hs = hs == 0u ? (uint32_t)FRAMES - 1u : hs - 1u;
+        ring_get(hs, pe, hf, r, a, c, en, hp);
+      } else {  // an empty ring: the frame from memory
+        mem_get(d, pe, hf, r, a, c, en, hp);
+        lo = d;
       }
     } else {
-TW_PRAGMA_UNROLL
-      for (int i = 0; i < FRAMES; ++i) {
-        const bool m = d == (uint32_t)i;
-        pe = m ? s_pe[i] : pe;
-        hf = m ? s_hf[i] : hf;
-        r = m ? s_res[i] : r;
-        a = m ? s_acc[i] : a;
-        if (CONC) c = m ? s_cmax[i] : c;
-        if (W) {
-          en = m ? s_end[i] : en;
-          hp = m ? s_hop[i] : hp;
-        }
-      }
+      ring_get(d, pe, hf, r, a, c, en, hp);
     }
     if constexpr (W) {
       f_pos = pe;
