@@ -55,6 +55,9 @@ BENCH_BATCH = {
     # a 100k-service realistic graph at probability 30: a WIDE tree (100,000
     # positions and call sites, past the 8-byte nodes; round 5)
     "c4w": 1 << 22,
+    # a DAG of shared callees past the unrolled tree (8^9 potential
+    # invocations): the lane walk over the site graph (round 6)
+    "cdag": 1 << 22,
     # the DES workspace is ~162 KB per trace on the 10k graph (rows sized
     # for u64: 170 GB at 2^20 of the 288 GB HBM); longer batches amortise
     # the pipelined queue pass's fill and drain (2^16 20.8,
@@ -82,9 +85,10 @@ def parse():
     # 2^24 traces (256 MB of records) per launch: the per-launch flush and
     # tail amortise (config 3: 2^22 335, 2^23 339, 2^24 340 M traces/s)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="traces per rank per step")
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c3p", "c3s", "c4", "c4w", "c5", "c5p", "c4d"])
+    ap.add_argument("--config", default="c3",
+                    choices=["c1", "c2", "c3", "c3p", "c3s", "c4", "c4w", "cdag", "c5", "c5p", "c4d"])
     ap.add_argument("--prob", type=int, default=0,
-                    help="c3p / c3s / c4w: the probability on every call (1..99; 0: 50, c4w 30)")
+                    help="c3p / c3s / c4w / cdag: the probability on every call (1..99; 0: 50, c4w 30, cdag 10)")
     ap.add_argument("--no-wave-leg", action="store_true",
                     help="c3p / c3s: skip the wave-interpreter leg (kinds 2/3, ISIM_FLAG_WAVE_WALK) on the same graph")
     ap.add_argument("--fill", action="store_true", help="draw-free static walks (config 2): walk one trace and "
@@ -105,7 +109,7 @@ def parse():
     args = ap.parse_args()
     args.des_auto_batch = False  # c5 with the default batch: shrink it to the device's free HBM
     if not args.prob:
-        args.prob = 30 if args.config == "c4w" else 50
+        args.prob = {"c4w": 30, "cdag": 10}.get(args.config, 50)
     if not args.mean_interarrival_ns:
         args.mean_interarrival_ns = 150_000 if args.config == "c4d" else 6_000_000
     return args
@@ -154,6 +158,14 @@ def build_graph(config: str, prob: int = 50):
                             f"seed 42), concurrent fan-out, sleep U{{1..5}}ms, errorRate U[0,1%], probability {prob} "
                             "on every call: a wide tree (100,000 positions and call sites), lane tree walk",
                 "services": 100000, "probability": prob}
+    elif config == "cdag":
+        from isim.generators import layered_dag_topology
+        j = obj_to_json(layered_dag_topology(probability=prob))
+        desc = {"workload": "a layered DAG of shared callees (9 layers x 8 services, every service calls every "
+                            "service of the next layer in one concurrent step at probability 10, sleep 1 ms, "
+                            "errorRate 5 %): 8^9 = 134M potential invocations per trace, past the unrolled tree — "
+                            "the lane walk over the site graph (one node per call site)",
+                "services": 72, "probability": prob}
     elif config == "c5":
         j = obj_to_json(config3_topology())
         desc = {"workload": "config 3's 10k-service graph + per-replica worker-pool contention: open-loop Poisson "
@@ -720,7 +732,7 @@ def main():
     }
     if args.config == "c3" and args.mode == "A" and not args.no_mode_b:
         line.update(mode_b_legs(args, json_text, rank, world, dev, multi))
-    if args.config in ("c3p", "c3s", "c4w") and not args.no_wave_leg:
+    if args.config in ("c3p", "c3s", "c4w", "cdag") and not args.no_wave_leg:
         line["wave_walk"] = wave_walk_leg(args, json_text, params, rank, world, dev, multi)
         line["speedup_vs_wave_walk"] = value / line["wave_walk"]["value"]
     if rank == 0 and world == 1 and not args.no_cpu:

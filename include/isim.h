@@ -112,6 +112,8 @@ typedef struct {
                                          (no reuse of the previous pass's sorted order) */
 #define ISIM_FLAG_DES_TWO_SORTS 1024u /* DES item engine: every sorted queue round by two stable sorts (replica |
                                          arrival, then service) instead of one combined key */
+#define ISIM_FLAG_TREE_DAG 2048u      /* dynamic walks: the lane walk over the site graph (one node per call site)
+                                         for any graph, not only where the unrolled tree would pass 2^24 positions */
 
 /* One 16-byte record per simulated request trace. */
 typedef struct {
@@ -133,7 +135,9 @@ typedef struct {
                                      a cyclic schedule found no fixed point within 256 passes; high 32 bits,
                                      batches FAILED by a device fault (a queue pass's decoupled look-back gave
                                      up waiting for an earlier tile: an error, never retried — isim_serve_des
-                                     and the item engine return ISIM_EHIP) */
+                                     and the item engine return ISIM_EHIP; such a batch writes no record and
+                                     counts no trace, and the item engine's per-site / DES-table words it may
+                                     have added are undefined: discard the buffers) */
 #define ISIM_ST_PROM 8            /* [2][33] latency histogram, Prometheus duration buckets
                                      (prometheus/handler.go:26-31), index [status500][bucket] */
 #define ISIM_N_PROM 33
@@ -199,7 +203,9 @@ typedef struct {
                                 (isim_fill_const) + n x its statistics (off with ISIM_FLAG_WALK_ALL) */
   int32_t tree_wide;         /* kind 7 on a wide tree (more than 65,535 positions, call sites or rows, or
                                 per-site counters past the LDS): 16-byte nodes, the hottest sites counted
-                                in LDS, the rest by global atomics; else 0 */
+                                in LDS, the rest by global atomics; 2: kind 7 on the site
+                                graph (one node per call site: a DAG whose unrolled tree would pass 2^24
+                                positions, or ISIM_FLAG_TREE_DAG), wide as 1; else 0 */
   uint64_t max_launch_traces; /* isim_serve_device splits a batch into launches of at most this many traces
                                  (per-workgroup u32 LDS counters must not wrap) */
 } isim_launch_info;

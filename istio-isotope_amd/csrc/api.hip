@@ -276,7 +276,7 @@ int build_device(isim_handler *h, int device, DevState &st) {
                                   p.tree_layout.nodes_lds != 0,
                                   (p.tree_flags & isim::kTreeAnyConc) != 0, (p.tree_flags & isim::kTreeAnyDraw) != 0,
                                   p.tree_layout.wg_per_cu == 2, p.tree_t64,
-                                  p.tree_wide);
+                                  p.tree_wide, p.tree_dag);
     if (!st.kernel) return fail(ISIM_EHIP, "no lane-tree-walk kernel for this tree");
     st.lds_bytes = p.tree_layout.bytes;
     st.lds_counters = 1;
@@ -616,7 +616,7 @@ int isim_handler_launch_info(isim_handler *h, int device, isim_launch_info *out)
   out->max_blocks = (int32_t)st->max_blocks;
   out->kernel_kind = (int32_t)st->kind;
   out->fill = st->draw_free && !(h->params.flags & ISIM_FLAG_WALK_ALL) ? 1 : 0;
-  out->tree_wide = st->kind == 7 && h->prog.tree_wide ? 1 : 0;
+  out->tree_wide = st->kind == 7 && h->prog.tree_wide ? (h->prog.tree_dag ? 2 : 1) : 0;
   out->max_launch_traces = max_launch_traces(st);
   return ISIM_OK;
 }

@@ -120,7 +120,7 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
       stack.push_back(i);
       for (uint32_t k = (nd.meta >> 24) & 0x7Fu; k > 0; --k) stack.pop_back();
     }
-  } else if (!p.static_walk && p.has_tree()) {
+  } else if (!p.static_walk && p.has_tree() && !p.tree_dag) {
     out.items = true;
     std::vector<std::pair<uint32_t, uint32_t>> stack;  // (position, end of its subtree)
     for (uint32_t i = 0; i < p.tree_positions(); ++i) {
@@ -132,6 +132,8 @@ int build_des_plan(const ServiceGraph &g, const Program &p, bool modeb, DesPlan 
     }
   } else {
     err = p.static_walk ? "DES needs a static walk of at most 2^24 invocations"
+          : p.tree_dag  ? std::string("DES of a dynamic walk needs the lane tree walk's unrolled tree (this walk runs "
+                                      "on the site graph: more than 2^24 potential invocations)")
                         : "DES of a dynamic walk needs the lane tree walk's unrolled tree (" + p.tree_why + ")";
     return ISIM_EINVAL;
   }

@@ -270,19 +270,24 @@ void *walk_kernel(int kind, bool modeb, bool lds_counters);
 // kind 7 variant (tree.hip, compiled once per mode and concurrency):
 // register-stack depth (4, 6, 8, 12, 16; `spill`: 8 registers + the rest in
 // global memory), nodes in LDS or global, the error-block cache.
-void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
-void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
-void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
-void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide);
+void *tree_kernel_m0c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide,
+                       bool dag);
+void *tree_kernel_m0c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide,
+                       bool dag);
+void *tree_kernel_m1c0(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide,
+                       bool dag);
+void *tree_kernel_m1c1(uint32_t frames, bool spill, bool nodes_lds, bool draw, bool occ2, bool t64, bool wide,
+                       bool dag);
 // occ2: the LDS layout fits two workgroups per CU (kernels built for 80 VGPRs);
-// t64: u64 time (Program::tree_t64); wide: a wide tree (Program::tree_wide)
+// t64: u64 time (Program::tree_t64); wide: a wide tree (Program::tree_wide);
+// dag: the site graph (Program::tree_dag, wide)
 inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds, bool conc, bool draw, bool occ2,
-                         bool t64, bool wide = false) {
+                         bool t64, bool wide = false, bool dag = false) {
   if (modeb)
-    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2, t64, wide)
-                : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2, t64, wide);
-  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64, wide)
-              : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide);
+    return conc ? tree_kernel_m1c1(frames, spill, nodes_lds, draw, occ2, t64, wide, dag)
+                : tree_kernel_m1c0(frames, spill, nodes_lds, draw, occ2, t64, wide, dag);
+  return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64, wide, dag)
+              : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide, dag);
 }
 void *stream_calls_kernel();
 void *mark_fold_kernel();  // kind 8: the per-launch fold of the position marks (walk.hip isim_mark_fold)

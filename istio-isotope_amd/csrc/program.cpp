@@ -184,10 +184,12 @@ static bool place_tree(Program &out, const std::vector<double> &row_heat, const 
 // counters do not fit in LDS is built WIDE (kernel_abi.h TreeNodeW;
 // ISIM_FLAG_TREE_WIDE: always, an independent check of the narrow format).
 constexpr uint32_t kTreeMaxWidePositions = 1u << 24;
+constexpr uint32_t kDagLdsPaths = 4096;  // site graph: LDS rows only for services reached <= this often per trace
 static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Site> &sites,
                        const std::vector<std::vector<int32_t>> &svc_sites, const std::vector<uint64_t> &thr,
                        const std::vector<uint64_t> &tmin, const std::vector<char> &leaf, bool modeb,
-                       bool force_wide) {
+                       bool force_wide, bool force_dag) {
+  out.tree_dag = false;
   out.tree_nodes.clear();
   out.tree_nodes_w.clear();
   out.tree_ext.clear();
@@ -199,6 +201,7 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     out.tree_ext.clear();
     out.tree_step.clear();
     out.tree_wide = false;
+    out.tree_dag = false;
     out.tree_why = why;
   };
   // u64 time when the latency bound reaches 2^32 ns; each position's own
@@ -267,6 +270,36 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   };
   std::vector<Frame> stack;
   const int32_t e = out.entry;
+  // the node of call site j of service s (flags, ext, step facts): shared by
+  // the unrolled tree (one per potential invocation) and the site graph (one
+  // per reachable call site); false when a figure does not fit 32 bits
+  auto site_node = [&](int32_t s, size_t j, TreeNodeW &nd, TreeExt &x, TreeStep &tsp) -> bool {
+    const Site &st = sites[svc_sites[s][j]];
+    const CallShape &cs = shape_of(s).calls[j];
+    const int32_t c = st.callee;
+    nd = TreeNodeW{};
+    nd.k = st.k;
+    nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
+    const bool xpre = modeb && cs.step_first && cs.pre != 0;
+    const bool xcmax = cs.step_first && cs.conc && cs.cmax0 != 0;
+    nd.flags = (uint8_t)((cs.step_first ? TF_STEP : 0) | (cs.conc ? TF_CONC : 0) | (leaf[c] ? TF_LEAF : 0) |
+                         err_flags(c) | (probk0[c] ? TF_PROBK0 : 0) | (xpre ? TF_XPRE : 0) | (xcmax ? TF_XCMAX : 0));
+    if (nd.prob) out.tree_flags |= kTreeAnyProb;
+    if (nd.flags & TF_CONC) out.tree_flags |= kTreeAnyConc;
+    if (nd.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
+    nd.slot = (uint32_t)out.site_slot[svc_sites[s][j]];
+    if (st.hop >= k32 || own_time(c) >= k32 || cs.pre >= k32 || cs.cmax0 >= k32) return false;
+    x = TreeExt{};
+    x.H = (uint32_t)st.hop;
+    x.tc = (uint32_t)own_time(c);
+    x.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
+    tsp = TreeStep{(uint32_t)cs.pre, (uint32_t)cs.cmax0};
+    return true;
+  };
+  // per service (reachable, DAG order): expected invocations per trace, and
+  // potential invocations per trace (the site graph's launch-split guard)
+  std::vector<double> svc_heat, svc_paths;
+  bool dag = force_dag;
   TreeNodeW root{};
   root.flags = (uint8_t)((leaf[e] ? TF_LEAF : 0) | err_flags(e) | (probk0[e] ? TF_PROBK0 : 0));
   if (root.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
@@ -279,45 +312,33 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   out.tree_step.push_back(TreeStep{});
   pos_callee.push_back(e);
   uint32_t max_open = leaf[e] ? 0u : 1u;
-  if (!leaf[e]) stack.push_back({e, 0, 0, 1.0});
-  while (!stack.empty()) {
+  if (!dag && !leaf[e]) stack.push_back({e, 0, 0, 1.0});
+  while (!dag && !stack.empty()) {
     Frame &top = stack.back();
     if (top.next < svc_sites[top.svc].size()) {
       const size_t j = top.next++;
-      const Site &st = sites[svc_sites[top.svc][j]];
-      const CallShape &cs = shape_of(top.svc).calls[j];
-      const int32_t c = st.callee;
+      const int32_t c = sites[svc_sites[top.svc][j]].callee;
       if (out.tree_nodes_w.size() >= kTreeMaxPositions) wide = true;
-      if (out.tree_nodes_w.size() >= kTreeMaxWidePositions) return give_up("more than 2^24 potential invocations");
-      TreeNodeW nd{};
-      nd.k = st.k;
-      nd.prob = (st.prob >= 1 && st.prob <= 99) ? (uint8_t)st.prob : (uint8_t)0;
-      const bool xpre = modeb && cs.step_first && cs.pre != 0;
-      const bool xcmax = cs.step_first && cs.conc && cs.cmax0 != 0;
-      nd.flags = (uint8_t)((cs.step_first ? TF_STEP : 0) | (cs.conc ? TF_CONC : 0) | (leaf[c] ? TF_LEAF : 0) |
-                           err_flags(c) | (probk0[c] ? TF_PROBK0 : 0) | (xpre ? TF_XPRE : 0) |
-                           (xcmax ? TF_XCMAX : 0));
-      if (nd.prob) out.tree_flags |= kTreeAnyProb;
-      if (nd.flags & TF_CONC) out.tree_flags |= kTreeAnyConc;
-      if (nd.flags & TF_ERR_DRAW) out.tree_flags |= kTreeAnyDraw;
-      const int32_t slot = out.site_slot[svc_sites[top.svc][j]];
-      nd.slot = (uint32_t)slot;
+      if (out.tree_nodes_w.size() >= kTreeMaxWidePositions) {
+        // shared callees multiply the potential invocations past the tree: the site graph
+        dag = true;
+        break;
+      }
+      TreeNodeW nd;
+      TreeExt x;
+      TreeStep tsp;
+      if (!site_node(top.svc, j, nd, x, tsp)) return give_up("a hop cost, script time or step sleep >= 2^32 ns");
+      const uint32_t slot = nd.slot;
       through[slot] += 1;
       const uint32_t row = (uint32_t)out.svc_row[c];
       if (row_bw[row]) row_through[row] += 1;
       const double heat = top.heat * (nd.prob ? nd.prob / 100.0 : 1.0);
       row_heat[row] += heat;
       slot_heat[slot] += heat;
-      if (st.hop >= k32 || own_time(c) >= k32 || cs.pre >= k32 || cs.cmax0 >= k32)
-        return give_up("a hop cost, script time or step sleep >= 2^32 ns");
-      TreeExt x{};
-      x.H = (uint32_t)st.hop;
-      x.tc = (uint32_t)own_time(c);
-      x.thr = thr[c] >= (1ull << 32) ? 0u : (uint32_t)thr[c];
       const uint32_t pos = (uint32_t)out.tree_nodes_w.size();
       out.tree_nodes_w.push_back(nd);
       out.tree_ext.push_back(x);
-      out.tree_step.push_back(TreeStep{(uint32_t)cs.pre, (uint32_t)cs.cmax0});
+      out.tree_step.push_back(tsp);
       pos_callee.push_back(c);
       if (!leaf[c]) {
         stack.push_back({c, 0, pos, heat});
@@ -328,9 +349,90 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       stack.pop_back();
     }
   }
-  if (out.tree_nodes_w.size() == 1) out.tree_nodes_w[0].size = 1;
-  for (size_t i = 0; i < out.tree_nodes_w.size(); ++i)
-    if (out.tree_nodes_w[i].size == 0) out.tree_nodes_w[i].size = 1;  // leaf positions
+  if (dag) {
+    // the site graph (tree_walk.h NodeD4): node 0 the entry, then each
+    // reachable calling service's sites, contiguous in script order; the
+    // services in reverse post-order of the call DAG (callers before callees)
+    if (out.hops_upper >= (1ull << 31)) return give_up("more than 2^31 invocations per trace in the site graph");
+    out.tree_nodes_w.resize(1);
+    out.tree_ext.resize(1);
+    out.tree_step.resize(1);
+    pos_callee.resize(1);
+    std::fill(row_heat.begin(), row_heat.end(), 0.0);
+    std::fill(slot_heat.begin(), slot_heat.end(), 0.0);
+    out.tree_flags = (out.tree_nodes_w[0].flags & TF_ERR_DRAW) ? kTreeAnyDraw : 0u;
+    wide = true;
+    std::vector<int32_t> order;  // post-order of the reachable calling services
+    {
+      std::vector<char> seen(n, 0);
+      std::vector<std::pair<int32_t, size_t>> st;
+      if (!leaf[e]) {
+        st.push_back({e, 0});
+        seen[e] = 1;
+      }
+      while (!st.empty()) {
+        auto &[s, j] = st.back();
+        if (j < svc_sites[s].size()) {
+          const int32_t c = sites[svc_sites[s][j++]].callee;
+          if (!leaf[c] && !seen[c]) {
+            seen[c] = 1;
+            st.push_back({c, 0});
+          }
+        } else {
+          order.push_back(s);
+          st.pop_back();
+        }
+      }
+    }
+    std::reverse(order.begin(), order.end());  // callers first (a DAG: cycles were rejected)
+    std::vector<uint32_t> first(n, 0), chain(n, 1);
+    uint32_t next = 1;
+    for (int32_t s : order) {
+      first[s] = next;
+      next += (uint32_t)svc_sites[s].size();
+    }
+    if (next >= kTreeMaxWidePositions) return give_up("more than 2^24 call sites in the site graph");
+    svc_heat.assign(n, 0.0);
+    svc_paths.assign(n, 0.0);
+    svc_heat[e] = svc_paths[e] = 1.0;
+    for (int32_t s : order) {
+      for (size_t j = 0; j < svc_sites[s].size(); ++j) {
+        TreeNodeW nd;
+        TreeExt x;
+        TreeStep tsp;
+        if (!site_node(s, j, nd, x, tsp)) return give_up("a hop cost, script time or step sleep >= 2^32 ns");
+        const int32_t c = sites[svc_sites[s][j]].callee;
+        nd.size = leaf[c] ? 0u : first[c];
+        nd.k = nd.k | ((leaf[c] ? 0u : (uint32_t)svc_sites[c].size()) << 16);
+        const double heat = svc_heat[s] * (nd.prob ? nd.prob / 100.0 : 1.0);
+        svc_heat[c] += heat;
+        svc_paths[c] += svc_paths[s];
+        row_heat[(uint32_t)out.svc_row[c]] += heat;
+        slot_heat[nd.slot] += heat;
+        out.tree_nodes_w.push_back(nd);
+        out.tree_ext.push_back(x);
+        out.tree_step.push_back(tsp);
+        pos_callee.push_back(c);
+      }
+    }
+    // nested calling invocations: the longest chain of calling services from the entry
+    for (auto it = order.rbegin(); it != order.rend(); ++it) {  // callees first
+      const int32_t s = *it;
+      for (int32_t si : svc_sites[s]) {
+        const int32_t c = sites[si].callee;
+        if (!leaf[c]) chain[s] = std::max(chain[s], 1u + chain[c]);
+      }
+    }
+    max_open = leaf[e] ? 0u : chain[e];
+    out.tree_nodes_w[0].size = leaf[e] ? 0u : first[e];
+    out.tree_nodes_w[0].k = (leaf[e] ? 0u : (uint32_t)svc_sites[e].size()) << 16;
+    out.tree_dag = true;
+  }
+  if (!out.tree_dag) {
+    if (out.tree_nodes_w.size() == 1) out.tree_nodes_w[0].size = 1;
+    for (size_t i = 0; i < out.tree_nodes_w.size(); ++i)
+      if (out.tree_nodes_w[i].size == 0) out.tree_nodes_w[i].size = 1;  // leaf positions
+  }
   out.tree_frames = max_open ? max_open - 1 : 0;
   if (out.tree_frames > kTreeMaxFrames) return give_up("more than 65 nested calling invocations");
   if (!wide) {  // the 8-byte device nodes and the LDS layout
@@ -364,6 +466,10 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
     out.tree_row_index.assign(R, 0);
     uint32_t room = kTreeLdsHalf - head;
     for (uint32_t r : rorder) {
+      // (the site graph: a row reached by more than kDagLdsPaths potential
+      // invocations per trace keeps global atomics, so its u32 LDS buckets
+      // do not force tiny launches — Program::tree_mult)
+      if (out.tree_dag && svc_paths[out.row_svc[r]] > (double)kDagLdsPaths) continue;
       const uint32_t w = std::max<uint32_t>(1u, row_bw[r]);
       const uint32_t need = row_lds_bytes(w, false);
       if (need > room || out.sum_row.size() >= 0x7FFFu || out.tree_dyn_words + 1u + 2u * w >= 0xFFF0u) continue;
@@ -422,7 +528,11 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
   out.tree_mult = 1;
   if (wide) {  // a hot row's u32 LDS bucket counts: the positions into it (the launch split's guard)
     std::vector<uint32_t> into(R, 0);
-    for (size_t i = 1; i < out.tree_nodes_w.size(); ++i) into[(uint32_t)out.svc_row[pos_callee[i]]] += 1;
+    if (out.tree_dag) {  // the site graph: the potential invocations per trace
+      for (uint32_t r = 1; r < R; ++r) into[r] = (uint32_t)std::min<double>(svc_paths[out.row_svc[r]], 4e9);
+    } else {
+      for (size_t i = 1; i < out.tree_nodes_w.size(); ++i) into[(uint32_t)out.svc_row[pos_callee[i]]] += 1;
+    }
     for (uint32_t r : out.sum_row) out.tree_mult = std::max(out.tree_mult, into[r]);
   } else {
     for (uint32_t m : through) out.tree_mult = std::max(out.tree_mult, m);
@@ -815,7 +925,7 @@ int compile_program(const ServiceGraph &g, int32_t entry, const isim_params &p, 
     return ISIM_EINVAL;
   }
   if (!out.static_walk) build_tree(g, out, sites, svc_sites, thr, tmin, leaf, p.error_mode == ISIM_MODE_B,
-                                        (p.flags & ISIM_FLAG_TREE_WIDE) != 0);
+                                        (p.flags & ISIM_FLAG_TREE_WIDE) != 0, (p.flags & ISIM_FLAG_TREE_DAG) != 0);
   return ISIM_OK;
 }
 

@@ -54,6 +54,7 @@ struct Program {
   std::vector<TreeNode> tree_nodes;
   std::vector<TreeNodeW> tree_nodes_w;
   bool tree_wide = false;           // a wide tree (kernel_abi.h TreeNodeW): 32-bit fields, global statistics
+  bool tree_dag = false;            // the site graph (tree_walk.h NodeD4): one node per call site, always wide
   std::vector<uint16_t> tree_slot_lds;  // wide: per slot its LDS counter (0xFFFF: global atomics)
   std::vector<uint32_t> tree_lds_slot;  // wide: per LDS counter its slot
   std::vector<TreeExt> tree_ext;

@@ -101,6 +101,14 @@ struct GlobalNodesW {
     return tw::NodeW4{v.x, v.y, v.z, v.w};
   }
 };
+// the site graph's nodes (Program::tree_dag, tree_walk.h NodeD4): the same 16 bytes
+struct GlobalNodesD {
+  const uint4 *__restrict__ p;
+  __device__ __forceinline__ tw::NodeD4 load(uint32_t i) const {
+    const uint4 v = p[i];
+    return tw::NodeD4{v.x, v.y, v.z, v.w};
+  }
+};
 
 // A wide tree's statistics (Program::tree_wide: call sites, rows or
 // positions past 16 bits, or counters that do not fit in LDS): the hottest
@@ -326,9 +334,10 @@ struct TreeSink {
 // 768-thread workgroups per CU) when the LDS layout fits half the CU, else 4
 // (one 1024-thread workgroup per CU: up to 128 VGPRs, no spills).
 // T64: u64 time (a latency bound of 2^32 ns or more; tree_walk.h Lane TT).
-// WIDE: a wide tree (16-byte nodes in global memory, WideSink).
+// WIDE: a wide tree (16-byte nodes in global memory, WideSink); DAG (with
+// WIDE): the site graph's nodes (one per call site, tree_walk.h NodeD4).
 template <bool MODEB, int FRAMES, bool SPILL, bool NLDS, bool CONC, bool DRAW, int WPE, bool T64 = false,
-          bool WIDE = false>
+          bool WIDE = false, bool DAG = false>
 __global__ void __launch_bounds__(kWgThreads, WPE)
     isim_tree(const TreeNode *__restrict__ gnodes, isim_trace_rec *__restrict__ records,
               uint64_t *__restrict__ gstats, const uint32_t *__restrict__ slot_tbkt, KParams kp) {
@@ -380,7 +389,8 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   sink.n_rows = kp.n_rows;
   sink.dbg = reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_DES_RETRY);
 #endif
-  using Nodes = std::conditional_t<WIDE, GlobalNodesW, std::conditional_t<NLDS, LdsNodes, GlobalNodes>>;
+  using Nodes = std::conditional_t<WIDE, std::conditional_t<DAG, GlobalNodesD, GlobalNodesW>,
+                                   std::conditional_t<NLDS, LdsNodes, GlobalNodes>>;
   Nodes nodes;
   if constexpr (WIDE)
     nodes.p = reinterpret_cast<const uint4 *>(gnodes);
@@ -658,11 +668,17 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
 #define TREE_WPE2 6
 #endif
 template <bool NLDS, bool DRAW>
-static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wide) {
+static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wide, bool dag) {
   using namespace dev;
   constexpr bool M = TREE_MODEB != 0, C = TREE_CONC != 0;
   if (wide) {  // a wide tree: nodes in global memory; tree_wide_reg_frames register frames (+ the spill)
     if constexpr (!NLDS) {
+      if (dag) {  // the site graph (always wide)
+        if (t64) return spill ? (void *)&isim_tree<M, 4, true, false, C, DRAW, 4, true, true, true>
+                              : (void *)&isim_tree<M, 4, false, false, C, DRAW, 4, true, true, true>;
+        return spill ? (void *)&isim_tree<M, 6, true, false, C, DRAW, 4, false, true, true>
+                     : (void *)&isim_tree<M, 6, false, false, C, DRAW, 4, false, true, true>;
+      }
       if (t64) return spill ? (void *)&isim_tree<M, 4, true, false, C, DRAW, 4, true, true>
                             : (void *)&isim_tree<M, 4, false, false, C, DRAW, 4, true, true>;
       return spill ? (void *)&isim_tree<M, 6, true, false, C, DRAW, 4, false, true>
@@ -691,12 +707,13 @@ static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wi
 #define TREE_CAT2(a, b, c) a##b##c
 #define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
 void *TREE_CAT(tree_kernel_m, TREE_MODEB, TREE_CAT(c, TREE_CONC, ))(uint32_t frames, bool spill, bool nodes_lds,
-                                                                      bool draw, bool occ2, bool t64, bool wide) {
+                                                                      bool draw, bool occ2, bool t64, bool wide,
+                                                                      bool dag) {
   if (nodes_lds && !wide)
-    return draw ? tree_pick<true, true>(frames, spill, occ2, t64, false)
-                : tree_pick<true, false>(frames, spill, occ2, t64, false);
-  return draw ? tree_pick<false, true>(frames, spill, occ2, t64, wide)
-              : tree_pick<false, false>(frames, spill, occ2, t64, wide);
+    return draw ? tree_pick<true, true>(frames, spill, occ2, t64, false, false)
+                : tree_pick<true, false>(frames, spill, occ2, t64, false, false);
+  return draw ? tree_pick<false, true>(frames, spill, occ2, t64, wide, dag)
+              : tree_pick<false, false>(frames, spill, occ2, t64, wide, dag);
 }
 
 }  // namespace isim

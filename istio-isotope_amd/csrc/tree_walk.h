@@ -84,6 +84,8 @@ TW_PRAGMA_UNROLL  // unrolled: config 4 7.28 -> 7.18 ms (the loop's SALU counter
 // through CpuNodes.
 struct NodeW {
   uint32_t w0, w1;  // size | k << 16, prob | flags << 8 | slot << 16
+  static constexpr bool kDag = false;
+  ISIM_TW uint32_t child() const { return 0; }
   ISIM_TW uint32_t size() const { return w0 & 0xFFFFu; }
   ISIM_TW uint32_t k() const { return w0 >> 16; }
   ISIM_TW uint32_t prob() const { return w1 & 0xFFu; }
@@ -104,6 +106,8 @@ struct CpuNodes {
 constexpr uint32_t kSiteLds = 0x80000000u;
 struct NodeW4 {
   uint32_t sz, kk, pf, sl;  // size, k, prob | flags << 8 | LDS counter << 16, slot
+  static constexpr bool kDag = false;
+  ISIM_TW uint32_t child() const { return 0; }
   ISIM_TW uint32_t size() const { return sz; }
   ISIM_TW uint32_t k() const { return kk; }
   ISIM_TW uint32_t prob() const { return pf & 0xFFu; }
@@ -121,6 +125,47 @@ struct CpuNodesW {
     return n;
   }
 };
+// The site graph (round 6, Program::tree_dag): when the unrolled tree of a
+// DAG would exceed kTreeMaxWidePositions (shared callees multiply the
+// potential invocations), the walk runs over ONE node per reachable call site
+// instead — each service's sites contiguous in script order, node 0 the entry
+// — with the same 16-byte TreeNodeW: size = the callee's first site node,
+// k = call index | the callee's site count << 16.  A skipped call then
+// advances by one node (not over a subtree), an open enters the callee's
+// site range, and a close resumes the caller after the closing invocation's
+// own site: the same preorder, hop ids and draws as the unrolled tree.
+struct NodeD4 {
+  uint32_t ch, kk, pf, sl;  // callee's first site node, k | callee's sites << 16, prob | flags | LDS counter, slot
+  static constexpr bool kDag = true;
+  ISIM_TW uint32_t child() const { return ch; }
+  ISIM_TW uint32_t size() const { return kk >> 16; }  // the callee's sites (the children of the opened node)
+  ISIM_TW uint32_t k() const { return kk & 0xFFFFu; }
+  ISIM_TW uint32_t prob() const { return pf & 0xFFu; }
+  ISIM_TW uint32_t flags() const { return (pf >> 8) & 0xFFu; }
+  ISIM_TW uint32_t slot() const { return sl; }
+  ISIM_TW uint32_t site() const { return (pf >> 16) != 0xFFFFu ? kSiteLds | (pf >> 16) : sl; }
+};
+static_assert(sizeof(TreeNodeW) == sizeof(NodeD4), "a site-graph node is a TreeNodeW");
+struct CpuNodesD {
+  const TreeNodeW *p;
+  ISIM_TW NodeD4 load(uint32_t i) const {
+    NodeD4 n;
+    __builtin_memcpy(&n, p + i, sizeof n);
+    return n;
+  }
+};
+// the positions a skipped call passes: its subtree, or (site graph) its own node
+template <class N>
+ISIM_TW uint32_t skip_span(const N &n) {
+  return N::kDag ? 1u : n.size();
+}
+template <class N>
+struct dag_of {
+  static constexpr bool value = N::kDag;
+};
+template <class N>
+struct dag_of<const N> : dag_of<N> {};
+
 ISIM_TW TreeExt load_ext(const TreeExt *ext, uint32_t p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint4 v = reinterpret_cast<const uint4 *>(ext)[p];
@@ -471,6 +516,7 @@ TW_PRAGMA_UNROLL
     const TT c = (TT)x.H + T;
     const bool cc = (fl & HF(FL_CONC_CHILD)) != 0;
     const uint32_t cpos = f_pos, chop = cur_hop();
+    if constexpr (dag_of<decltype(nodes.load(0))>::value) p = cpos + 1u;  // the caller's next site
     pop();
     if constexpr (close_rec<Sink>::value) sink.rec_close(cpos, chop, cur_hop(), T, st);
     fold(c, st, cc);
@@ -493,7 +539,7 @@ TW_PRAGMA_UNROLL
         set_kb(kb);
       }
       if (skipped(n)) {
-        p += n.size();
+        p += skip_span(n);
         return;
       }
     }
@@ -532,8 +578,13 @@ TW_PRAGMA_UNROLL
     f_res = pk ? residues(hop, 0, k0, k1) : 0u;
     f_hf = (W ? 0u : hop) | HF((own ? FL_OWN : 0u) | ((fl & TF_CONC) ? FL_CONC_CHILD : 0u) | ((pk ? 0u : KB_NONE) << KB_SHIFT));
     if (W) f_hop = hop;
-    end = p + n.size();
-    p += 1;
+    if constexpr (dag_of<decltype(n)>::value) {  // the callee's site range
+      p = n.child();
+      end = p + n.size();
+    } else {
+      end = p + n.size();
+      p += 1;
+    }
   }
 
   // pass call position p if its skip draw (already in f_res) says skip
@@ -547,7 +598,7 @@ TW_PRAGMA_UNROLL
     f_acc = acc;
     f_hf = fl;
     f_cmax = cm;
-    p += n.size();
+    p += skip_span(n);
     return true;
   }
 

@@ -155,6 +155,28 @@ def mesh_des_topology(n_services: int = 100_000, layers: int = 8, fanout: int = 
     return doc
 
 
+def layered_dag_topology(layers: int = 9, width: int = 8, probability: int = 10, error_rate: float = 0.05,
+                         sleep: str = "1ms") -> Dict[str, Any]:
+    """A DAG of shared callees: every service of a layer calls every service
+    of the next in one concurrent step, each call at `probability`, after a
+    sleep.  width^layers potential invocations per trace (8^9 = 134M: past the
+    2^24 positions the unrolled tree of the lane tree walk holds, so kind 7
+    runs over the site graph, Program::tree_dag), ~width * probability / 100
+    expected callees per invocation.  Not a reference generator: a shape
+    isotope's validation accepts (validation.go:28-57) that neither
+    create_tree_topology.py nor create_realistic_topology.py emits."""
+    services = []
+    for layer in range(layers):
+        for w in range(width):
+            svc: Dict[str, Any] = {"name": f"l{layer}_{w}", "errorRate": error_rate, "script": [{"sleep": sleep}]}
+            if layer + 1 < layers:
+                svc["script"].append([{"call": {"service": f"l{layer + 1}_{v}", "probability": probability}}
+                                      for v in range(width)])
+            services.append(svc)
+    services[0]["isEntrypoint"] = True
+    return {"services": services}
+
+
 def config3_topology(n: int = 10_000, seed: int = 42) -> Dict[str, Any]:
     """BASELINE config 3: realistic multitier 10k, concurrent fan-out,
     sleep U{1..5} ms, errorRate U[0, 1%]."""

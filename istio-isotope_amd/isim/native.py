@@ -36,6 +36,7 @@ FLAG_TREE_WIDE = 128  # the wide lane-tree format for any dynamic walk
 FLAG_DES_SCAN_BY_KEY = 256  # DES items: queues by rocPRIM's scan by key (not k_qscan)
 FLAG_DES_SORT_ALL = 512  # DES items, cyclic schedules: sort every round of every pass
 FLAG_DES_TWO_SORTS = 1024  # DES items: two stable sorts per sorted queue round
+FLAG_TREE_DAG = 2048  # the lane walk over the site graph for any dynamic walk
 
 # stats layout (isim.h)
 ST_N_TRACES, ST_SUM_LATENCY, ST_SUM_HOPS, ST_SUM_ERR_HOPS, ST_N_500 = 0, 1, 2, 3, 4

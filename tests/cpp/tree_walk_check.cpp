@@ -107,6 +107,7 @@ int main(int argc, char **argv) {
   p.resp_ps_per_byte = std::strtoull(argv[6], nullptr, 0);
   p.flags = ISIM_FLAG_DYNAMIC;  // static graphs too: the tree walk is the general path
   if (std::getenv("ISIM_TW_WIDE")) p.flags |= ISIM_FLAG_TREE_WIDE;  // every tree in the wide format
+  if (std::getenv("ISIM_TW_DAG")) p.flags |= ISIM_FLAG_TREE_DAG;    // every walk over the site graph
   const uint64_t begin = std::strtoull(argv[7], nullptr, 0), n = std::strtoull(argv[8], nullptr, 0);
   Program prog;
   if (compile_program(g, entry, p, prog, err) != ISIM_OK) {
@@ -117,9 +118,9 @@ int main(int argc, char **argv) {
     std::printf("why %s\n", prog.tree_why.c_str());
     return 3;
   }
-  std::fprintf(stderr, "positions %u frames %u lds %u nodes_lds %u wg_per_cu %u lds_rows %u wide %d\n",
+  std::fprintf(stderr, "positions %u frames %u lds %u nodes_lds %u wg_per_cu %u lds_rows %u wide %d dag %d\n",
                prog.tree_positions(), prog.tree_frames, prog.tree_layout.bytes, prog.tree_layout.nodes_lds,
-               prog.tree_layout.wg_per_cu, prog.tree_layout.n_sum, prog.tree_wide ? 1 : 0);
+               prog.tree_layout.wg_per_cu, prog.tree_layout.n_sum, prog.tree_wide ? 1 : 0, prog.tree_dag ? 1 : 0);
   const uint32_t S = (uint32_t)prog.n_slots, R = (uint32_t)prog.row_svc.size();
   Sink sk;
   sk.prog = &prog;
@@ -171,6 +172,7 @@ int main(int argc, char **argv) {
   wbs.sp = was.sp = wcs.sp = wds.sp = spillw.data();
   const tw::CpuNodes nodes{prog.tree_nodes.data()};
   const tw::CpuNodesW nodes_w{prog.tree_nodes_w.data()};
+  const tw::CpuNodesD nodes_d{prog.tree_nodes_w.data()};  // the site graph (Program::tree_dag)
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t lat = 0;
     uint32_t hops = 0, errh = 0;
@@ -178,7 +180,9 @@ int main(int argc, char **argv) {
     auto run = [&](auto &L) {
       L.start(begin + i);
       while (!L.done) {
-        if (prog.tree_wide)
+        if (prog.tree_dag)
+          L.step(nodes_d, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        else if (prog.tree_wide)
           L.step(nodes_w, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
         else
           L.step(nodes, prog.tree_ext.data(), prog.tree_step.data(), sk, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));

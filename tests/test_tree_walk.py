@@ -253,3 +253,48 @@ def test_wide_by_size(checker, tmp_path):
     (70,000 positions and call sites) — wide without forcing, bit-exact."""
     doc = realistic_topology(70000, concurrent=True, sleep_ms=(1, 3), error_rate=(0.0, 0.01), probability=40)
     assert compare(checker, tmp_path, obj_to_json(doc), 0, n=60, wide=True)
+
+
+# ---- the site graph (round 6, Program::tree_dag, tree_walk.h NodeD4): the
+# lane walk over one node per call site, for DAGs whose unrolled tree would
+# pass 2^24 positions (shared callees multiply the potential invocations;
+# validation.go:28-57 accepts any DAG) — wide frames and statistics
+
+def layered_dag(layers=9, width=8, prob=10, error_rate=0.05, sleep="1ms"):
+    """isim.generators.layered_dag_topology as JSON: width^layers potential
+    invocations per trace (8^9 = 134M, past the 2^24 positions of the
+    unrolled tree)."""
+    from isim.generators import layered_dag_topology
+    return obj_to_json(layered_dag_topology(layers, width, prob, error_rate, sleep))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_forced_dag(checker, tmp_path, monkeypatch, mode):
+    """Every dynamic walk over the site graph (ISIM_FLAG_TREE_DAG, set by the
+    checker under ISIM_TW_DAG): meshes, concurrent and sequential realistic
+    graphs (u64 time), the probability-and-concurrency graph, a shared-callee
+    DAG, the spilling depths — bit-exact against the oracle."""
+    monkeypatch.setenv("ISIM_TW_DAG", "1")
+    docs = [with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
+            obj_to_json(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2),
+                                           probability=70)),
+            obj_to_json(realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.1), probability=75)),
+            layered_dag(5, 4, prob=40)]
+    for j in docs:
+        got = run_check(checker, tmp_path, j, mode, n=10)
+        assert got is not None and " dag 1" in got[1]["stderr"], got and got[1]["stderr"]
+        assert compare(checker, tmp_path, j, mode, n=600)
+    monkeypatch.setenv("ISIM_TW_SPILL", "1")
+    assert compare(checker, tmp_path, docs[1], mode, n=300)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dag_by_size(checker, tmp_path, mode):
+    """A DAG whose unrolled tree has 8^9 = 134M positions (past the 2^24 the
+    tree walk takes): the site graph without forcing (65 nodes: the entry and
+    64 call sites), bit-exact against the oracle — before round 6 such walks fell back to the
+    wave interpreter."""
+    j = layered_dag()
+    got = run_check(checker, tmp_path, j, mode, n=10)
+    assert got is not None and " dag 1" in got[1]["stderr"] and " wide 1" in got[1]["stderr"], got
+    assert compare(checker, tmp_path, j, mode, n=3000, begin=(1 << 32) - 1500)

@@ -486,3 +486,62 @@ def test_tree_wide_equals_narrow(gpu):
     r2, s2 = wide.gpu(12345, n)
     assert np.array_equal(r1, r2)
     assert np.array_equal(s1, s2)
+
+
+# ---- the site graph (round 6, Program::tree_dag): kind 7 over one node per
+# call site for DAGs whose unrolled tree would pass 2^24 positions
+# (validation.go:28-57 accepts any DAG; before round 6 such walks ran on the
+# wave interpreter, kinds 2/3, 17-18x slower)
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_tree_dag_forced(gpu, mode):
+    """Every dynamic walk over the site graph (ISIM_FLAG_TREE_DAG): a mesh, a
+    deep concurrent realistic graph, a 40-deep chain (spilled frames), u64
+    time, a shared-callee DAG — bit-exact against the oracle on windows
+    across 2^32 (executable.go:84-179, handler.go:37-79)."""
+    from test_tree_walk import layered_dag
+    docs = [with_defaults(obj_to_json(mesh_topology(1200, 6, seed=3)), errorRate=0.05),
+            obj_to_json(realistic_topology(400, concurrent=True, sleep_ms=(1, 5), error_rate=(0.0, 0.2),
+                                           probability=70)),
+            _prob_chain(40),
+            obj_to_json(realistic_topology(300, sleep_ms=(20, 40), error_rate=(0.0, 0.1), probability=75)),
+            layered_dag(5, 4, prob=40)]
+    for j in docs:
+        c = Case(j, None, isim.SimParams(error_mode=mode, flags=isim.native.FLAG_TREE_DAG))
+        li = c.handler.launch_info(0)
+        assert li["kernel_kind"] == 7 and li["tree_wide"] == 2
+        c.compare(1000, 3000)
+        c.compare((1 << 32) - 700, 1400)
+
+
+@pytest.mark.parametrize("mode", [isim.MODE_A, isim.MODE_B])
+def test_tree_dag_by_size(gpu, mode):
+    """A DAG of 72 services whose unrolled tree has 8^9 = 134M positions
+    (every service of a layer calls every one of the next at probability 10):
+    the site graph without forcing (u32 time: concurrent fan-out) —
+    bit-exact against the oracle,
+    and at 2^20 traces record for record equal to the wave interpreter (kinds
+    2/3, ISIM_FLAG_WAVE_WALK), the path such walks took before.  The DES
+    rejects it (no unrolled tree to schedule)."""
+    from test_tree_walk import layered_dag
+    j = layered_dag()
+    c = Case(j, None, isim.SimParams(error_mode=mode))
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7 and li["tree_wide"] == 2
+    c.compare(5, 3000)
+    c.compare((1 << 32) - 1500, 3000)
+    n = 1 << 20
+    r1, s1 = c.gpu(1 << 33, n)
+    w = isim.Handler(isim.ServiceGraph.from_json(j), None,
+                     isim.SimParams(error_mode=mode, flags=isim.native.FLAG_WAVE_WALK))
+    assert w.launch_info(0)["kernel_kind"] in (2, 3)
+    r2, s2 = w.serve(1 << 33, n)
+    assert np.array_equal(r1, r2)
+    f1, f2 = c.handler.fold(s1), w.fold(s2)
+    for k in ("n_traces", "sum_latency", "sum_hops", "sum_err_hops", "n_500"):
+        assert f1[k] == f2[k], k
+    for k in ("site_calls", "svc_calls", "svc_errs"):
+        assert np.array_equal(np.asarray(f1[k]), np.asarray(f2[k])), k
+    with pytest.raises(isim.IsimError) as ei:
+        isim.DesHandler(c.handler, 1_000_000)
+    assert ei.value.code == isim.native.EINVAL and "site graph" in str(ei.value)
