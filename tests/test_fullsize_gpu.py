@@ -357,3 +357,25 @@ def test_mode_b_marking_equals_close_list(gpu, informative):
     bad = np.nonzero(s8 != s6)[0]
     assert bad.size == 0, f"stats words differ at {bad[:8].tolist()}"
     assert int(s8[isim.native.ST_N_500]) > 0
+
+
+def test_cdag_bench_batch(gpu):
+    """cdag exactly as bench.py times it (round 6): bench.build_graph("cdag"),
+    a layered DAG of shared callees whose unrolled tree would have 8^9 = 134M
+    positions, on the lane walk over the site graph (kind 7, tree_wide 2),
+    BENCH_BATCH["cdag"] = 2^22 traces per launch, two launches into one stats
+    buffer from trace ids crossing 2^32; oracle windows at every launch edge
+    and internal split, sampled windows, and the full stats of a window
+    (executable.go:84-179, validation.go:28-57)."""
+    j, _ = bench.build_graph("cdag", 10)
+    c = Case(j, None, isim.SimParams(flags=isim.native.FLAG_WALK_ALL))
+    li = c.handler.launch_info(0)
+    assert li["kernel_kind"] == 7 and li["tree_wide"] == 2
+    n, L = bench.BENCH_BATCH["cdag"], 2
+    begin = (1 << 32) - n - 12345
+    rec, f = _device_run(c, begin, n, L)
+    _common_properties(f, rec, n * L)
+    assert rec["hops"].min() >= 1 and f["n_500"] > 0
+    _launch_edge_windows(c, rec, begin, n, L, width=128)
+    _sampled_windows(c, rec, begin, n * L, windows=4, width=128, seed=17)
+    c.compare(begin + n - 2048, 4096)

@@ -291,8 +291,8 @@ def test_forced_dag(checker, tmp_path, monkeypatch, mode):
 @pytest.mark.parametrize("mode", [0, 1])
 def test_dag_by_size(checker, tmp_path, mode):
     """A DAG whose unrolled tree has 8^9 = 134M positions (past the 2^24 the
-    tree walk takes): the site graph without forcing (65 nodes: the entry and
-    64 call sites), bit-exact against the oracle — before round 6 such walks fell back to the
+    tree walk takes): the site graph without forcing (457 nodes: the entry and
+    the 456 call sites of the 57 reachable calling services), bit-exact against the oracle — before round 6 such walks fell back to the
     wave interpreter."""
     j = layered_dag()
     got = run_check(checker, tmp_path, j, mode, n=10)

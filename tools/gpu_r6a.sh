@@ -20,11 +20,13 @@ timeout -k 10 1000 python -u -m pytest -x -v --timeout 400 --timeout-method thre
   "tests/test_fullsize_gpu.py::test_config3s_bench_batch" \
   "tests/test_des_items_gpu.py::test_items_match_event_oracle" \
   "tests/test_fullsize_gpu.py::test_config4w_bench_batch" \
-  "tests/test_des_items_gpu.py::test_items_c4w_graph" > $O/tests.log 2>&1
+  "tests/test_des_items_gpu.py::test_items_c4w_graph" \
+  "tests/test_walk_gpu.py::test_tree_dag_forced" "tests/test_walk_gpu.py::test_tree_dag_by_size" \
+  "tests/test_fullsize_gpu.py::test_cdag_bench_batch" > $O/tests.log 2>&1
 rc=$?
 grep -E "FAILED|ERROR|passed|failed" $O/tests.log | tail -20
 [ $rc -eq 0 ] || exit $rc
-for c in c3 c3p c4w; do
+for c in c3 c3p c4w cdag; do
 timeout -k 10 600 python bench.py --config $c > $O/bench_$c.log 2>&1 || { tail -20 $O/bench_$c.log; exit 6; }
 grep '^{' $O/bench_$c.log | tail -1 | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$c', d['value'], d['roofline']['kernel_ms'], {k:(d[k]['value'],d[k]['kernel_ms'],d[k]['kernel_kind']) for k in ('mode_b','mode_b_informative') if k in d})"
 done
