@@ -67,8 +67,8 @@ def _launch_edge_windows(case: Case, rec, begin, n, launches, width=256):
     for i in range(launches):
         lo = i * n
         edges.update([lo, lo + n - width])
-        for cut in range(lo + m, lo + n, m):  # internal splits of launch i
-            edges.add(cut - width // 2)
+        for cut in range(lo + m, lo + n, m):  # internal splits of launch i (a window inside the records)
+            edges.add(min(cut - width // 2, launches * n - width))
     for s0 in sorted(edges):
         _check_window(case, rec, begin, s0, width)
     return m
