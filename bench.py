@@ -203,11 +203,18 @@ def cpu_baseline(json_text: str, params, n_traces: int, trace_begin: int):
     op = OParams(params.seed, params.hop_base_ns, params.req_ps_per_byte, params.resp_ps_per_byte,
                  params.error_mode)
     og = oc.OracleGraph(sg, op)
-    if n_traces <= 0:
+    auto = n_traces <= 0
+    if auto:
         n_traces = 32768 * threads
     t0 = time.perf_counter()
     _, st = oc.run(sg, op, sg.entry(), trace_begin, n_traces, records=False, n_threads=threads, og=og)
     dt = time.perf_counter() - t0
+    if auto and dt < 2.0:
+        # a sample of ~10 s of CPU work (a fast graph finished the first one in under 2 s)
+        n_traces = int(n_traces * min(256.0, 10.0 / max(dt, 1e-3)))
+        t0 = time.perf_counter()
+        _, st = oc.run(sg, op, sg.entry(), trace_begin, n_traces, records=False, n_threads=threads, og=og)
+        dt = time.perf_counter() - t0
     return {"value": n_traces / dt, "unit": "traces/s", "cores": threads, "kind": "port",
             "sample": f"{n_traces} traces of the same workload (trace ids from {trace_begin}), "
                       f"C oracle oracle/isim_oracle.c with OpenMP, {dt:.3g} s",
