@@ -164,8 +164,17 @@ struct K {
   // and marks the chunks whose values it changes (dnext).  Queue scans stay
   // whole-round (a change moves later traces of the queue: their chunks are
   // marked as their starts change)
+  // Round 6: the same marks per TRACE as well (dcur_t / dnext_t, n bytes):
+  // after the first passes about 1 % of the items change per pass, spread
+  // over enough traces that nearly every 256-trace chunk stays marked; a
+  // chunk mark now only pre-filters, an item is recomputed when its own
+  // trace changed (the invariant holds per trace: every dependence between
+  // traces goes through the whole-round queue scans, which mark the traces
+  // whose starts they change)
   const uint8_t *dcur;
   uint8_t *dnext;
+  const uint8_t *dcur_t;
+  uint8_t *dnext_t;
   uint32_t cshift;
   uint16_t *irep;                  // per item: its replica (drawn once per batch)
   // mode B: the walks draw the errors (a failed step ends its script); per
@@ -184,7 +193,11 @@ struct K {
 __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t v, uint32_t item) {
   if (k.changed) {
     const bool diff = *p != v;
-    if (diff && k.dnext) k.dnext[k.itr[item] >> k.cshift] = 1;
+    if (diff && k.dnext) {
+      const uint32_t t = k.itr[item];
+      k.dnext[t >> k.cshift] = 1;
+      k.dnext_t[t] = 1;
+    }
     const unsigned long long m = __ballot(diff);
     if (m && (threadIdx.x & 63u) == (uint32_t)__ffsll((long long)m) - 1u) {
       if (__hip_atomic_load(k.changed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(k.changed, 1u);
@@ -194,8 +207,13 @@ __device__ __forceinline__ void store_tracked(const K &k, uint64_t *p, uint64_t 
 }
 
 __device__ __forceinline__ uint64_t gid() { return (uint64_t)blockIdx.x * kT + threadIdx.x; }
-// the item is recomputed in this pass (its chunk changed in the previous one)
-__device__ __forceinline__ bool live(const K &k, uint32_t i) { return !k.dcur || k.dcur[k.itr[i] >> k.cshift]; }
+// the item is recomputed in this pass (its trace changed in the previous one;
+// the chunk map first: it is small and cached)
+__device__ __forceinline__ bool live(const K &k, uint32_t i) {
+  if (!k.dcur) return true;
+  const uint32_t t = k.itr[i];
+  return k.dcur[t >> k.cshift] && k.dcur_t[t];
+}
 __device__ __forceinline__ uint64_t nthreads() { return (uint64_t)gridDim.x * kT; }
 __device__ __forceinline__ uint64_t item_off(const K &k, uint64_t t) { return t ? k.tend[t - 1] : 0; }
 
@@ -500,8 +518,9 @@ __global__ void __launch_bounds__(kT) k_scatter_ids(K k, const uint32_t *poff, c
 __global__ void __launch_bounds__(kT) k_steps(K k, const unsigned long long *ops, uint64_t m) {
   for (uint64_t j = gid(); j < m; j += nthreads()) {
     const unsigned long long op = ops[j];
-    if (k.dcur && !k.dcur[op >> 48]) continue;  // not recomputed in this pass
+    if (k.dcur && !k.dcur[op >> 48]) continue;  // not recomputed in this pass (its chunk)
     const uint64_t i = (op >> 16) & 0xFFFFFFFFull;
+    if (k.dcur && !k.dcur_t[k.itr[i]]) continue;  // (its trace)
     const uint32_t s = (uint32_t)(op & 0xFFFFu);
     if (k.ifst && s > k.ifst[i]) continue;  // mode B: the script failed at an earlier step
     const DesItemPos p = k.ip[k.ipos[i]];
@@ -1610,7 +1629,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       tmp_bytes,
       M * 2, (n >> chunk_shift(n)) + 1, (n >> chunk_shift(n)) + 1,  // replicas; the two chunk-change maps
       pl.cyclic ? M * 2 : 2,                                    // kept orders' trace chunks
-      pl.modeb ? M * 4 : 4};                                    // mode B: failed call step per item
+      pl.modeb ? M * 4 : 4,                                     // mode B: failed call step per item
+      n + 1, n + 1};                                            // the two per-trace change maps
   uint64_t total = 0;
   for (uint64_t q : parts) total += al256(q ? q : 1);
   if (!pool_alloc(item_mem, total)) return fail("item allocation");
@@ -1672,6 +1692,7 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
   uint16_t *ordc = (uint16_t *)carve(parts[51]);
   uint32_t *ifst = (uint32_t *)carve(parts[52]);
   k.ifst = pl.modeb ? ifst : nullptr;
+  uint8_t *chg_ta = (uint8_t *)carve(parts[53]), *chg_tb = (uint8_t *)carve(parts[54]);
   // the rounds' queues by k_qscan (its keys a - j h need j h < 2^62), else
   // rocPRIM's scan by key over the maps and k_qout (ISIM_FLAG_DES_SCAN_BY_KEY:
   // always, an independent check of k_qscan)
@@ -1960,7 +1981,8 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
       uint32_t p = 0;
       for (; p < kMaxPasses && !rc; ++p) {
         uint32_t changed[2] = {1, 0};
-        if (hipMemsetAsync(kq.changed, 0, 8, s) != hipSuccess || hipMemsetAsync(chg_b, 0, n_chunks, s) != hipSuccess) {
+        if (hipMemsetAsync(kq.changed, 0, 8, s) != hipSuccess || hipMemsetAsync(chg_b, 0, n_chunks, s) != hipSuccess ||
+            hipMemsetAsync(chg_tb, 0, n, s) != hipSuccess) {
           rc = fail("memset");
           break;
         }
@@ -1969,9 +1991,12 @@ int des_items_launch(const DesItemsLaunch &L, void *stream_, std::string &err) {
         // previous pass changed
         kq.dcur = p == 0 ? nullptr : chg_a;
         kq.dnext = chg_b;
+        kq.dcur_t = chg_ta;
+        kq.dnext_t = chg_tb;
         pass(kq);
         if (rc) break;
         std::swap(chg_a, chg_b);
+        std::swap(chg_ta, chg_tb);
         if (hipMemcpyAsync(changed, kq.changed, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             sync_s() != hipSuccess) {
           rc = fail("fixed-point read-back");
