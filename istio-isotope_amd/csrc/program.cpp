@@ -470,15 +470,17 @@ static void build_tree(const ServiceGraph &g, Program &out, const std::vector<Si
       // invocations per trace keeps global atomics, so its u32 LDS buckets
       // do not force tiny launches — Program::tree_mult)
       if (out.tree_dag && svc_paths[out.row_svc[r]] > (double)kDagLdsPaths) continue;
+      // (round 6: the code-200 buckets only — a 500, errorRate-rare, goes to
+      // HBM with its sum — so a hot row takes 12 + 4 w bytes, not 12 + 8 w)
       const uint32_t w = std::max<uint32_t>(1u, row_bw[r]);
-      const uint32_t need = row_lds_bytes(w, false);
-      if (need > room || out.sum_row.size() >= 0x7FFFu || out.tree_dyn_words + 1u + 2u * w >= 0xFFF0u) continue;
+      const uint32_t need = 12u + 4u * w;
+      if (need > room || out.sum_row.size() >= 0x7FFFu || out.tree_dyn_words + 1u + w >= 0xFFF0u) continue;
       room -= need;
       out.tree_row_index[r] = (uint32_t)out.sum_row.size();
       out.tree_row_place[r] = out.tree_dyn_words;
       out.sum_row.push_back(r);
       out.tree_dyn.push_back(TreeDynRow{r, out.tree_dyn_words, out.tree_row_blo[r], w});
-      out.tree_dyn_words += 1u + 2u * w;
+      out.tree_dyn_words += 1u + w;
     }
     L.n_sum = (uint32_t)out.sum_row.size();
     // the hottest call sites (expected calls per trace) keep guarded 16-bit

@@ -132,7 +132,7 @@ struct WideSink {
   uint32_t *cnt;               // LDS: per hot site calls | 500s << 16 (guarded 16-bit fields)
   const uint32_t *lds_slot;    // per LDS counter: its slot
   unsigned long long *sum200;  // LDS: the hot rows' code-200 duration sums
-  uint32_t *dyn;               // LDS: the hot rows' bucket tables (header b_lo | width << 8, [2][width] u32)
+  uint32_t *dyn;               // LDS: the hot rows' code-200 bucket tables (header b_lo | width << 8, [width] u32)
   const uint32_t *sum_row;     // per hot row: its row
   // a leaf callee's durations, n of them (static bucket and latency)
   __device__ __forceinline__ void leaf_dur(uint32_t slot, bool st, unsigned long long n) {
@@ -174,16 +174,18 @@ struct WideSink {
     if (!svc_tab) return;
     if (roww & 0x80000000u) {  // a hot row: sum index << 16 | its bucket table's LDS offset
       const uint32_t idx = (roww >> 16) & 0x7FFFu, place = roww & 0xFFFFu;
+      if (st) {  // a 500 (errorRate-rare): bucket and sum in HBM (the LDS table holds code 200 only)
+        unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)wide_row(sum_row[idx]) *
+                                                                      ISIM_SVC_DUR_WORDS);
+        atomicAdd(r + ISIM_N_PROM + lut_bucket(lut, T), 1ull);
+        atomicAdd(r + 2 * ISIM_N_PROM + 1, (unsigned long long)T);
+        return;
+      }
       const uint32_t hdr = dyn[place], lo = hdr & 0xFFu, w = hdr >> 8;
       uint32_t b = lut_bucket(lut, T) - lo;
       b = b < w ? b : w - 1;  // tmin <= T <= tmax keeps it in range; never write past the table
-      lds_add(dyn + place + 1u + (st ? w : 0u) + b, 1u);
-      if (st)
-        atomicAdd((unsigned long long *)(svc_tab + (uint64_t)wide_row(sum_row[idx]) * ISIM_SVC_DUR_WORDS) +
-                      2 * ISIM_N_PROM + 1,
-                  (unsigned long long)T);
-      else
-        lds_add(sum200 + idx, (unsigned long long)T);
+      lds_add(dyn + place + 1u + b, 1u);
+      lds_add(sum200 + idx, (unsigned long long)T);
       return;
     }
     unsigned long long *r = (unsigned long long *)(svc_tab + (uint64_t)wide_row(roww) * ISIM_SVC_DUR_WORDS);
@@ -621,6 +623,8 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
         const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
         if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));
         if (v >> 16) atomicAdd(row + b + 1u, (unsigned long long)(v >> 16));
+      } else if (WIDE) {  // [width] u32, code 200 (a wide tree's 500s went to HBM)
+        atomicAdd(row + d.b_lo + (i - d.off - 1u), (unsigned long long)v);
       } else {  // [code][width] u32
         const uint32_t j = i - d.off - 1, code = j >= d.width ? 1u : 0u, b = d.b_lo + j - code * d.width;
         atomicAdd(row + code * ISIM_N_PROM + b, (unsigned long long)v);
