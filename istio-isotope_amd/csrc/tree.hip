@@ -539,6 +539,9 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     }
   }
   __syncthreads();
+#ifdef TREE_NO_FLUSH
+  return;  // (timing experiments only: the flush's share of a launch)
+#endif
   // ---- flush the workgroup's accumulators (coalesced over slots / rows)
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
