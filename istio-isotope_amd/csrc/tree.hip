@@ -539,13 +539,11 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     }
   }
   __syncthreads();
-#ifdef TREE_NO_FLUSH
-  return;  // (timing experiments only: the flush's share of a launch)
-#endif
   // ---- flush the workgroup's accumulators (coalesced over slots / rows)
   unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
   for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
     if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
+#ifndef TREE_NO_FLUSH  // (timing experiments only: the slot and row flush's share of a launch)
   // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
   if constexpr (!WIDE) {
   auto calls_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] & 0xFFFFu) : c.cnt[s]; };
@@ -634,6 +632,7 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
       }
     }
   }
+#endif
   if (c.svc_tab) {
     unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
     // the entry's row: its invocations are the traces (end-to-end histogram and sums)

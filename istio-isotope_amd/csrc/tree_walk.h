@@ -223,12 +223,18 @@ struct close_rec<S, decltype((void)S::kCloseRec)> {
   static constexpr bool value = S::kCloseRec;
 };
 //
-// One step() is a MACRO step: close the current invocation if the walk has
-// passed its subtree, then process position p (a call: skip it, run a leaf
+// One step() is a MACRO step: process position p (a call: skip it, run a leaf
 // callee, or open a calling callee), then pass up to kScan further calls whose
-// skip draw says skip, then close again if the walk has passed the subtree.  A wave runs its 64 lanes' steps in lock step, so
+// skip draw says skip, then close the current invocation if the walk has
+// passed its subtree.  A wave runs its 64 lanes' steps in lock step, so
 // fewer, fuller steps per trace are what count (config 4: 25.9 -> 11.1
-// wave iterations per 64 traces).  The skip residues of an invocation are
+// wave iterations per 64 traces) — but so does what a step costs: until
+// round 6 a step also closed FIRST when the previous one left the walk past
+// its subtree (a chain of subtrees ending together), and that second close
+// site, which some lane of a wave needs in ~96 % of its steps, cost more than
+// the steps it saved (c4 5.57 -> 5.05 ms per 2^26 traces with 8.3 -> 9.2
+// wave steps per 64 traces; c3p 25.2 -> 22.7 ms with 289 -> 305: DESIGN.md
+// §5 round 6, tools/wave_sim.py).  The skip residues of an invocation are
 // drawn once, when it opens, and kept in its frame (f_res), so returning from
 // a callee never recomputes the caller's block and the scans need no draw.
 // CONC: the walk has concurrent steps (without them no frame keeps a step max).
@@ -612,16 +618,15 @@ TW_PRAGMA_UNROLL
       return;
     }
 #endif
-    if (p >= end && !close(nodes, ext, sink)) return;
-    if (p < end) process(nodes, ext, stp, sink, k0, k1);
+    if (p < end) process(nodes, ext, stp, sink, k0, k1);  // (else the walk closes at the end of the step)
     bool go = !done;
 TW_PRAGMA_UNROLL
     for (int i = 0; i < kScan; ++i) {
       go = go && p < end && scan(nodes, stp);
     }
-    // and close the invocation if the walk has passed its subtree: a chain of
-    // subtrees ending together takes half the steps (config 4: 12.5 -> 10.4
-    // wave iterations per 64 traces, 7.18 -> 7.03 ms per 2^26 traces)
+    // and close the invocation if the walk has passed its subtree (the step's
+    // one close site; round 4 added it here, after the scans: config 4 12.5 ->
+    // 10.4 wave iterations per 64 traces, 7.18 -> 7.03 ms per 2^26 traces)
     if (!done && p >= end) close(nodes, ext, sink);
   }
 };
