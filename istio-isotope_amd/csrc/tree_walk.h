@@ -187,6 +187,18 @@ constexpr uint32_t KB_NONE = 0x7FFu;
 #define TW_SCAN 3
 #endif
 constexpr int kScan = TW_SCAN;    // skipped calls a step may pass after its action (tree.hip: uniform trips)
+// the scan budget of a walk: kScan, or its node accessor's kScan (tree.hip:
+// nodes read from HBM pass 2 — each scan is a dependent global load: c3p
+// 22.7 -> 22.2 ms, c3s 21.7 -> 21.2, c4w 18.0 -> 18.0; nodes in LDS pass 3:
+// config 4 runs 5.05 ms with 3, 5.68 with 2)
+template <class N, class = void>
+struct scan_of {
+  static constexpr int value = kScan;
+};
+template <class N>
+struct scan_of<N, decltype((void)N::kScan)> {
+  static constexpr int value = N::kScan;
+};
 
 // The four skip draws of a Philox block reduced to what shouldSkipRequest
 // compares (word % 100, 7 bits each): skip call k iff residue(k & 3) < 100 - p.
@@ -621,7 +633,7 @@ TW_PRAGMA_UNROLL
     if (p < end) process(nodes, ext, stp, sink, k0, k1);  // (else the walk closes at the end of the step)
     bool go = !done;
 TW_PRAGMA_UNROLL
-    for (int i = 0; i < kScan; ++i) {
+    for (int i = 0; i < scan_of<Nodes>::value; ++i) {
       go = go && p < end && scan(nodes, stp);
     }
     // and close the invocation if the walk has passed its subtree (the step's
