@@ -439,7 +439,9 @@ int build_device(isim_handler *h, int device, DevState &st) {
     // a full grid; a launch waits for the area's previous launch and fold
     // (launch_walk_one)
     st.part_words = p.tree_layout.off_nodes / 4u;
-    st.area_words = st.spill_words + (size_t)st.max_blocks * st.part_words;
+    const size_t slices = (st.max_blocks + isim::kTreeFoldSlice - 1) / isim::kTreeFoldSlice;
+    st.area_words = st.spill_words + ((size_t)st.max_blocks * st.part_words + 1u) / 2u * 2u +  // (the image 8-B aligned)
+                    slices * 2u * st.part_words;
     HIPCHK(hipMalloc(&st.d_spill[0], st.area_words * sizeof(uint32_t)));
     for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
@@ -736,11 +738,16 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
     kp.part = st->d_spill[a] + st->spill_words;
     kp.part_words = st->part_words;
     HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, hs));
-    // the fold: every statistic of the launch once (tree.hip isim_tree_fold)
+    // the fold: the partials summed by slices of workgroups, then every
+    // statistic of the launch once (tree.hip isim_tree_fold_sum, isim_tree_fold)
+    uint32_t groups = grid, pw = st->part_words, slices = (grid + isim::kTreeFoldSlice - 1) / isim::kTreeFoldSlice;
+    const uint32_t *part = kp.part;
+    uint32_t *img = kp.part + ((size_t)st->max_blocks * st->part_words + 1u) / 2u * 2u;
+    void *sargs[] = {&part, &pw, &groups, &img};
+    HIPCHK(hipLaunchKernel(isim::tree_fold_sum_kernel(), dim3((pw + 255u) / 256u, slices), dim3(256), sargs, 0, hs));
     const uint32_t items = std::max({isim::kHistWords, 2u * kp.n_slots, kp.lay.n_sum, kp.dyn_words, kp.n_lds_slots});
     const uint32_t fold_blocks = std::min<uint32_t>(2048u, (items + 255u) / 256u);
-    uint32_t groups = grid;
-    void *fargs[] = {&d_stats, &dur, &kp, &groups};
+    void *fargs[] = {&d_stats, &dur, &kp, &img, &slices};
     HIPCHK(hipLaunchKernel(isim::tree_fold_kernel(h->prog.tree_wide), dim3(fold_blocks), dim3(256), fargs, 0, hs));
     HIPCHK(hipEventRecord(st->spill_ev[a], hs));
     st->spill_last[a] = hs;

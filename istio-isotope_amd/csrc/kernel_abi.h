@@ -292,8 +292,12 @@ inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds
   return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64, wide, dag)
               : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide, dag);
 }
-// kind 7: the launch's fold of its workgroups' partials (tree.hip isim_tree_fold;
-// args: stats, slot_tbkt, KParams, workgroups)
+// kind 7: the launch's fold of its workgroups' partials (tree.hip): the sums
+// per slice of kTreeFoldSlice workgroups (isim_tree_fold_sum; args: partials,
+// part_words, workgroups, image; grid (ceil(part_words / 256), slices)), then
+// the flush (isim_tree_fold; args: stats, slot_tbkt, KParams, image, slices)
+constexpr uint32_t kTreeFoldSlice = 64;
+void *tree_fold_sum_kernel();
 void *tree_fold_kernel(bool wide);
 void *stream_calls_kernel();
 void *mark_fold_kernel();  // kind 8: the per-launch fold of the position marks (walk.hip isim_mark_fold)

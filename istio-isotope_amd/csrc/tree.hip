@@ -338,8 +338,8 @@ struct TreeSink {
 // The statistics a kind-7 workgroup accumulates in LDS, flushed to the stats
 // buffer, over a value source V: w(i) the u32 LDS word i, lo(i) / hi(i) its
 // 16-bit fields, q(i) the u64 at words i, i + 1, mx(i) the same for a max
-// (LdsVal: the workgroup's own LDS; PartVal: the sum, or max, over the
-// launch's workgroups' partial copies — the fold).  Items are dealt
+// (LdsVal: the workgroup's own LDS; ImgVal: the sum, or max, over the
+// launch's workgroups' partial copies, by slices — the fold).  Items are dealt
 // i = t0, t0 + ts, ...; `lead` adds the header words.
 struct LdsVal {
   const uint32_t *l;
@@ -351,35 +351,43 @@ struct LdsVal {
   }
   __device__ __forceinline__ unsigned long long mx(uint32_t i) const { return q(i); }
 };
-struct PartVal {
-  const uint32_t *p;  // [groups][pw] words
-  uint32_t pw, groups;
-  __device__ __forceinline__ unsigned long long w(uint32_t i) const {
-    unsigned long long s = 0;
-    for (uint32_t g = 0; g < groups; ++g) s += p[(size_t)g * pw + i];
-    return s;
-  }
+// the fold's image (isim_tree_fold_sum): per slice of kTreeFoldSlice
+// workgroups and LDS word, the sums of its low and high 16-bit fields (u32
+// each: a slice's field sums stay below 2^22); the WgAcc max words hold the
+// slice's max as (low word, 0), (high word, 0)
+constexpr uint32_t kAccMaxLo = 10, kAccMaxHi = 14;  // WgAcc notmin, max: LDS words [10, 14)
+struct ImgVal {
+  const uint2 *img;  // [slices][pw] (lo, hi)
+  uint32_t pw, slices;
   __device__ __forceinline__ unsigned long long lo(uint32_t i) const {
     unsigned long long s = 0;
-    for (uint32_t g = 0; g < groups; ++g) s += p[(size_t)g * pw + i] & 0xFFFFu;
+#pragma unroll 8
+    for (uint32_t k = 0; k < slices; ++k) s += img[(size_t)k * pw + i].x;
     return s;
   }
   __device__ __forceinline__ unsigned long long hi(uint32_t i) const {
     unsigned long long s = 0;
-    for (uint32_t g = 0; g < groups; ++g) s += p[(size_t)g * pw + i] >> 16;
+#pragma unroll 8
+    for (uint32_t k = 0; k < slices; ++k) s += img[(size_t)k * pw + i].y;
     return s;
   }
-  __device__ __forceinline__ unsigned long long q(uint32_t i) const {
-    unsigned long long s = 0;
-    for (uint32_t g = 0; g < groups; ++g)
-      s += (unsigned long long)p[(size_t)g * pw + i] | (unsigned long long)p[(size_t)g * pw + i + 1] << 32;
-    return s;
+  __device__ __forceinline__ unsigned long long w(uint32_t i) const {
+    unsigned long long a = 0, b = 0;
+#pragma unroll 8
+    for (uint32_t k = 0; k < slices; ++k) {
+      const uint2 v = img[(size_t)k * pw + i];
+      a += v.x;
+      b += v.y;
+    }
+    return a + (b << 16);
   }
+  __device__ __forceinline__ unsigned long long q(uint32_t i) const { return w(i) + (w(i + 1) << 32); }
   __device__ __forceinline__ unsigned long long mx(uint32_t i) const {
     unsigned long long m = 0;
-    for (uint32_t g = 0; g < groups; ++g) {
+#pragma unroll 8
+    for (uint32_t k = 0; k < slices; ++k) {
       const unsigned long long v =
-          (unsigned long long)p[(size_t)g * pw + i] | (unsigned long long)p[(size_t)g * pw + i + 1] << 32;
+          (unsigned long long)img[(size_t)k * pw + i].x | (unsigned long long)img[(size_t)k * pw + i + 1].x << 32;
       m = v > m ? v : m;
     }
     return m;
@@ -724,23 +732,61 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
   // flushed here by global atomics (a launch captured into a HIP graph)
   if (kp.part) {
     uint32_t *dst = kp.part + (size_t)blockIdx.x * kp.part_words;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(lds);
-    for (uint32_t i = threadIdx.x; i < kp.part_words; i += blockDim.x) dst[i] = src[i];
+    if ((kp.part_words & 1u) == 0) {  // 8-byte words (ds_read_b64, global_store_dwordx2)
+      const lds_u64 *src = (const lds_u64 *)lds;
+      for (uint32_t i = threadIdx.x; i < kp.part_words / 2u; i += blockDim.x)
+        reinterpret_cast<unsigned long long *>(dst)[i] = src[i];
+    } else {
+      const __attribute__((address_space(3))) uint32_t *src = (const __attribute__((address_space(3))) uint32_t *)lds;
+      for (uint32_t i = threadIdx.x; i < kp.part_words; i += blockDim.x) dst[i] = src[i];
+    }
     return;
   }
   tree_flush<WIDE>(LdsVal{reinterpret_cast<const uint32_t *>(lds)}, threadIdx.x, blockDim.x, threadIdx.x == 0, gstats,
                    slot_tbkt, kp);
 }
 
-// The launch's fold: the workgroups' partial words summed, then the same flush
-// (one atomic per nonzero statistic per LAUNCH instead of per workgroup:
-// c3p's 256 workgroups each flushed ~50k counters — 1.1 GB of WRITE per
-// 2^22 launch against 67 MB of records)
+// The launch's fold, in two kernels: the workgroups' partial words summed per
+// slice of kTreeFoldSlice workgroups (one thread per (word, slice): its loads
+// all in flight), then the same flush over the slices' sums — one atomic per
+// nonzero statistic per LAUNCH instead of per workgroup (c3p's 256
+// workgroups each flushed ~50k counters: 1.1 GB of WRITE per 2^22 launch
+// against 67 MB of records)
+template <int = 0>  // (a template: one definition across the four objects of this file)
+__global__ void __launch_bounds__(256) isim_tree_fold_sum(const uint32_t *__restrict__ part, uint32_t pw,
+                                                          uint32_t groups, uint2 *__restrict__ img) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, k = blockIdx.y;
+  if (i >= pw) return;
+  const uint32_t g0 = k * kTreeFoldSlice, g1 = g0 + kTreeFoldSlice < groups ? g0 + kTreeFoldSlice : groups;
+  uint2 *out = img + (size_t)k * pw;
+  if (i >= kAccMaxLo && i < kAccMaxHi) {  // the WgAcc maxima (u64 word pairs): the slice's max
+    if (i & 1u) return;
+    unsigned long long m = 0;
+    for (uint32_t g = g0; g < g1; ++g) {
+      const unsigned long long v =
+          (unsigned long long)part[(size_t)g * pw + i] | (unsigned long long)part[(size_t)g * pw + i + 1] << 32;
+      m = v > m ? v : m;
+    }
+    out[i] = make_uint2((uint32_t)m, 0u);
+    out[i + 1] = make_uint2((uint32_t)(m >> 32), 0u);
+    return;
+  }
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kTreeFoldSlice; ++j) {
+    if (g0 + j < g1) {
+      const uint32_t v = part[(size_t)(g0 + j) * pw + i];
+      lo += v & 0xFFFFu;
+      hi += v >> 16;
+    }
+  }
+  out[i] = make_uint2(lo, hi);
+}
 template <bool WIDE>
 __global__ void __launch_bounds__(256) isim_tree_fold(uint64_t *__restrict__ gstats,
                                                       const uint32_t *__restrict__ slot_tbkt, KParams kp,
-                                                      uint32_t groups) {
-  tree_flush<WIDE>(PartVal{kp.part, kp.part_words, groups}, blockIdx.x * blockDim.x + threadIdx.x,
+                                                      const uint2 *__restrict__ img, uint32_t slices) {
+  tree_flush<WIDE>(ImgVal{img, kp.part_words, slices}, blockIdx.x * blockDim.x + threadIdx.x,
                    gridDim.x * blockDim.x, blockIdx.x == 0 && threadIdx.x == 0, gstats, slot_tbkt, kp);
 }
 
@@ -802,6 +848,7 @@ static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wi
 void *tree_fold_kernel(bool wide) {
   return wide ? (void *)&dev::isim_tree_fold<true> : (void *)&dev::isim_tree_fold<false>;
 }
+void *tree_fold_sum_kernel() { return (void *)&dev::isim_tree_fold_sum<>; }
 #endif
 
 #define TREE_CAT2(a, b, c) a##b##c
