@@ -293,16 +293,13 @@ ISIM_API int isim_handler_slots(const isim_handler *h, int32_t *slot_site, int32
  * of one handler may be in flight on one device at once (launches on ONE
  * stream are ordered and never collide; with more than 256 streams in
  * flight, order them with events or use one handler per stream).  A lane tree
- * walk (kernel kind 7) uses one of up to 4 areas per (handler, device), each
- * allocated when a stream first needs it: its workgroups' accumulators (a
- * second kernel of the launch folds them into d_stats) and, deeper than its
- * register frames (16 calling invocations on narrow trees, fewer on wide
- * ones), its spilled frames; each such launch waits for the previous launch
- * that used its area (an event recorded after every launch's fold), so
- * launches on different streams never share an area.  On a capturing stream
- * a lane tree walk takes no area (its workgroups add their accumulators to
- * d_stats by atomics: the same statistics), and one that spills frames cannot
- * be captured: it returns ISIM_EINVAL. */
+ * walk deeper than its register frames (16 calling invocations on narrow
+ * trees, fewer on wide ones) spills frames to one of up to 4 areas per
+ * (handler, device), each allocated when a stream first needs it: each such
+ * launch waits for the previous launch that used its area (an event recorded
+ * after every spilling launch), so launches on different streams never share
+ * frames.  A spilling walk cannot be graph-captured: on a capturing stream it
+ * returns ISIM_EINVAL. */
 ISIM_API int isim_serve_device(isim_handler *h, uint64_t trace_begin, uint64_t n_traces,
                       isim_trace_rec *d_records, uint64_t *d_stats, void *hip_stream);
 

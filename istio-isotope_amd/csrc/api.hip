@@ -87,15 +87,12 @@ struct DevState {
   uint32_t *d_sum_row = nullptr;        // kind 7: per LDS sum index, its row
   uint32_t *d_slot_tc = nullptr;        // kind 7: per slot, the leaf callee's latency
   uint32_t *d_lds_slot = nullptr;       // kind 7, wide tree: per LDS counter its slot
-  // kind 7: launch areas, up to kSpillAreas (the first allocated with the
-  // program, the others when a further stream first needs one): the frames
-  // below the register stack (spill_words, a spilling walk), then the
-  // workgroups' accumulator partials the launch's fold adds up
+  // kind 7: frames below the register stack, up to kSpillAreas areas (the
+  // first allocated with the program, the others when a further stream first
+  // needs one)
   uint32_t *d_spill[isim::kSpillAreas] = {};
   uint32_t spill_lanes = 0;
-  size_t spill_words = 0;               // u32 words of an area's spilled frames
-  size_t area_words = 0;                // u32 words of one area (spilled frames + partials)
-  uint32_t part_words = 0;              // u32 words of one workgroup's partial (TreeLayout off_nodes / 4)
+  size_t spill_words = 0;               // u32 words of one area
   hipEvent_t spill_ev[isim::kSpillAreas] = {};     // recorded after each area's latest launch
   hipStream_t spill_last[isim::kSpillAreas] = {};  // the stream of that launch
   bool spill_used[isim::kSpillAreas] = {};
@@ -427,23 +424,17 @@ int build_device(isim_handler *h, int device, DevState &st) {
     st.max_mult = std::max<uint32_t>(1, p.tree_mult);
     const uint32_t regf = isim::tree_reg_frames(p.tree_frames, p.tree_t64, p.tree_wide);
     if (p.tree_frames > regf) {
-      // the spilled frames: frames below the register frames, one column per
-      // lane of a full grid
+      // the spill areas: frames below the register frames, one column per
+      // lane of a full grid; a launch waits for the area's previous launch
+      // (launch_walk_one)
       st.spill_lanes = st.max_blocks * st.threads;
       st.spill_words = (size_t)(p.tree_frames - regf) *
                        ((p.tree_t64 ? isim::kTreeSpillWords64 : isim::kTreeSpillWords) +
                         (p.tree_wide ? isim::kTreeSpillWide : 0u)) *
                        st.spill_lanes;
+      HIPCHK(hipMalloc(&st.d_spill[0], st.spill_words * sizeof(uint32_t)));
+      for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    // the launch areas: the spilled frames, then one partial per workgroup of
-    // a full grid; a launch waits for the area's previous launch and fold
-    // (launch_walk_one)
-    st.part_words = p.tree_layout.off_nodes / 4u;
-    const size_t slices = (st.max_blocks + isim::kTreeFoldSlice - 1) / isim::kTreeFoldSlice;
-    st.area_words = st.spill_words + ((size_t)st.max_blocks * st.part_words + 1u) / 2u * 2u +  // (the image 8-B aligned)
-                    slices * 2u * st.part_words;
-    HIPCHK(hipMalloc(&st.d_spill[0], st.area_words * sizeof(uint32_t)));
-    for (hipEvent_t &e : st.spill_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   if (is_stream(st.kind)) {
     st.max_mult = 1;
@@ -711,44 +702,27 @@ static int launch_walk_one(isim_handler *h, DevState *st, uint64_t trace_begin, 
   const void *prog = st->d_prog;
   const uint32_t *dur = st->d_dur;
   void *args[] = {&prog, &d_records, &d_stats, &dur, &kp};
-  const hipStream_t hs = (hipStream_t)hip_stream;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (st->d_spill[0] && (hipStreamIsCapturing(hs, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)) {
-    // a captured kind-7 launch keeps no area (the area would be
-    // fixed in the graph, and nothing could order its replays against the
-    // eager launches that later take the same area): its workgroups flush by
-    // atomics; a walk that spills frames needs its area and is refused
-    if (st->spill_words)
+  if (st->d_spill[0]) {
+    // a spilling walk: the area its stream used last (else the next one,
+    // round robin; allocated on first use), ordered after the area's previous
+    // launch by an event; the wait, launch and record are one step under the
+    // handler's lock.  Not graph-capturable: a captured launch
+    // would keep its area in the graph, and nothing could order its replays
+    // against the eager launches that later take the same area.
+    const hipStream_t hs = (hipStream_t)hip_stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(hs, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
       return fail(ISIM_EINVAL, "a lane tree walk that spills frames (more nested calling invocations than its "
                                "register frames) cannot be captured into a HIP graph");
-    HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, hs));
-  } else if (st->d_spill[0]) {
-    // a kind-7 walk: the area its stream used last (else the next one, round
-    // robin; allocated on first use), ordered after the area's previous launch
-    // and fold by an event; the wait, launch, fold and record are one step
-    // under the handler's lock
     std::lock_guard<std::mutex> lk(h->spill_mu);
     uint32_t a = isim::kSpillAreas;
     for (uint32_t i = 0; i < isim::kSpillAreas; ++i)
       if (st->spill_used[i] && st->spill_last[i] == hs) a = i;
     if (a == isim::kSpillAreas) a = st->spill_next++ % isim::kSpillAreas;
-    if (!st->d_spill[a]) HIPCHK(hipMalloc(&st->d_spill[a], st->area_words * sizeof(uint32_t)));
+    if (!st->d_spill[a]) HIPCHK(hipMalloc(&st->d_spill[a], st->spill_words * sizeof(uint32_t)));
     if (st->spill_used[a]) HIPCHK(hipStreamWaitEvent(hs, st->spill_ev[a], 0));
-    kp.spill = st->spill_words ? st->d_spill[a] : nullptr;
-    kp.part = st->d_spill[a] + st->spill_words;
-    kp.part_words = st->part_words;
+    kp.spill = st->d_spill[a];
     HIPCHK(hipLaunchKernel(st->kernel, dim3(grid), dim3(st->threads), args, st->lds_bytes, hs));
-    // the fold: the partials summed by slices of workgroups, then every
-    // statistic of the launch once (tree.hip isim_tree_fold_sum, isim_tree_fold)
-    uint32_t groups = grid, pw = st->part_words, slices = (grid + isim::kTreeFoldSlice - 1) / isim::kTreeFoldSlice;
-    const uint32_t *part = kp.part;
-    uint32_t *img = kp.part + ((size_t)st->max_blocks * st->part_words + 1u) / 2u * 2u;
-    void *sargs[] = {&part, &pw, &groups, &img};
-    HIPCHK(hipLaunchKernel(isim::tree_fold_sum_kernel(), dim3((pw + 255u) / 256u, slices), dim3(256), sargs, 0, hs));
-    const uint32_t items = std::max({isim::kHistWords, 2u * kp.n_slots, kp.lay.n_sum, kp.dyn_words, kp.n_lds_slots});
-    const uint32_t fold_blocks = std::min<uint32_t>(2048u, (items + 255u) / 256u);
-    void *fargs[] = {&d_stats, &dur, &kp, &img, &slices};
-    HIPCHK(hipLaunchKernel(isim::tree_fold_kernel(h->prog.tree_wide), dim3(fold_blocks), dim3(256), fargs, 0, hs));
     HIPCHK(hipEventRecord(st->spill_ev[a], hs));
     st->spill_last[a] = hs;
     st->spill_used[a] = true;

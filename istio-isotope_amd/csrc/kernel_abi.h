@@ -243,9 +243,6 @@ struct KParams {
   TreeLayout lay;                // kind 7: LDS layout
   const uint32_t *lds_slot;      // kind 7, wide tree: per LDS counter its slot (lay.off_cnt .. off_sums)
   uint32_t n_lds_slots;          // kind 7, wide tree: LDS counters
-  uint32_t *part;                // kind 7: [grid][part_words] the workgroups' accumulator words for the
-                                 // launch's fold (tree_fold_kernel), or null: each workgroup flushes by atomics
-  uint32_t part_words;           // kind 7: lay.off_nodes / 4
 };
 
 // Batch queues of one launch: one counter per XCD (workgroups are dealt to
@@ -292,13 +289,6 @@ inline void *tree_kernel(bool modeb, uint32_t frames, bool spill, bool nodes_lds
   return conc ? tree_kernel_m0c1(frames, spill, nodes_lds, draw, occ2, t64, wide, dag)
               : tree_kernel_m0c0(frames, spill, nodes_lds, draw, occ2, t64, wide, dag);
 }
-// kind 7: the launch's fold of its workgroups' partials (tree.hip): the sums
-// per slice of kTreeFoldSlice workgroups (isim_tree_fold_sum; args: partials,
-// part_words, workgroups, image; grid (ceil(part_words / 256), slices)), then
-// the flush (isim_tree_fold; args: stats, slot_tbkt, KParams, image, slices)
-constexpr uint32_t kTreeFoldSlice = 64;
-void *tree_fold_sum_kernel();
-void *tree_fold_kernel(bool wide);
 void *stream_calls_kernel();
 void *mark_fold_kernel();  // kind 8: the per-launch fold of the position marks (walk.hip isim_mark_fold)
 void *fill_const_kernel();  // (records, n, record, one-trace stats, stats, stats words)

@@ -335,191 +335,6 @@ struct TreeSink {
   }
 };
 
-// The statistics a kind-7 workgroup accumulates in LDS, flushed to the stats
-// buffer, over a value source V: w(i) the u32 LDS word i, lo(i) / hi(i) its
-// 16-bit fields, q(i) the u64 at words i, i + 1, mx(i) the same for a max
-// (LdsVal: the workgroup's own LDS; ImgVal: the sum, or max, over the
-// launch's workgroups' partial copies, by slices — the fold).  Items are dealt
-// i = t0, t0 + ts, ...; `lead` adds the header words.
-struct LdsVal {
-  const uint32_t *l;
-  __device__ __forceinline__ unsigned long long w(uint32_t i) const { return l[i]; }
-  __device__ __forceinline__ unsigned long long lo(uint32_t i) const { return l[i] & 0xFFFFu; }
-  __device__ __forceinline__ unsigned long long hi(uint32_t i) const { return l[i] >> 16; }
-  __device__ __forceinline__ unsigned long long q(uint32_t i) const {
-    return (unsigned long long)l[i] | (unsigned long long)l[i + 1] << 32;
-  }
-  __device__ __forceinline__ unsigned long long mx(uint32_t i) const { return q(i); }
-};
-// the fold's image (isim_tree_fold_sum): per slice of kTreeFoldSlice
-// workgroups and LDS word, the sums of its low and high 16-bit fields (u32
-// each: a slice's field sums stay below 2^22); the WgAcc max words hold the
-// slice's max as (low word, 0), (high word, 0)
-constexpr uint32_t kAccMaxLo = 10, kAccMaxHi = 14;  // WgAcc notmin, max: LDS words [10, 14)
-struct ImgVal {
-  const uint2 *img;  // [slices][pw] (lo, hi)
-  uint32_t pw, slices;
-  __device__ __forceinline__ unsigned long long lo(uint32_t i) const {
-    unsigned long long s = 0;
-#pragma unroll 8
-    for (uint32_t k = 0; k < slices; ++k) s += img[(size_t)k * pw + i].x;
-    return s;
-  }
-  __device__ __forceinline__ unsigned long long hi(uint32_t i) const {
-    unsigned long long s = 0;
-#pragma unroll 8
-    for (uint32_t k = 0; k < slices; ++k) s += img[(size_t)k * pw + i].y;
-    return s;
-  }
-  __device__ __forceinline__ unsigned long long w(uint32_t i) const {
-    unsigned long long a = 0, b = 0;
-#pragma unroll 8
-    for (uint32_t k = 0; k < slices; ++k) {
-      const uint2 v = img[(size_t)k * pw + i];
-      a += v.x;
-      b += v.y;
-    }
-    return a + (b << 16);
-  }
-  __device__ __forceinline__ unsigned long long q(uint32_t i) const { return w(i) + (w(i + 1) << 32); }
-  __device__ __forceinline__ unsigned long long mx(uint32_t i) const {
-    unsigned long long m = 0;
-#pragma unroll 8
-    for (uint32_t k = 0; k < slices; ++k) {
-      const unsigned long long v =
-          (unsigned long long)img[(size_t)k * pw + i].x | (unsigned long long)img[(size_t)k * pw + i + 1].x << 32;
-      m = v > m ? v : m;
-    }
-    return m;
-  }
-};
-template <bool WIDE, class V>
-__device__ __forceinline__ void tree_flush(const V &v, uint32_t t0, uint32_t ts, bool lead, uint64_t *gstats,
-                                           const uint32_t *slot_tbkt, const KParams &kp) {
-  const TreeLayout &lay = kp.lay;
-  const uint32_t S = kp.n_slots;
-  unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
-  unsigned long long *tab = kp.svc_dur ? reinterpret_cast<unsigned long long *>(gstats + ISIM_ST_SVC_DUR(S)) : nullptr;
-  // LDS word offsets: WgAcc (u64 fields), the histograms, the counters, the sums, the bucket tables
-  constexpr uint32_t AW = 0, HW = kLdsAccBytes / 4u;
-  constexpr uint32_t A_LAT = AW + 0, A_HOPS = AW + 2, A_ERR = AW + 4, A_N500 = AW + 6, A_NTR = AW + 8,
-                     A_NOTMIN = AW + 10, A_MAX = AW + 12, A_LAT500 = AW + 14;
-  static_assert(sizeof(WgAcc) == 64, "WgAcc: eight u64 fields in this order");
-  const uint32_t CW = lay.off_cnt / 4u, SW = lay.off_sums / 4u, DW = lay.off_dyn / 4u;
-  for (uint32_t i = t0; i < kHistWords; i += ts) {
-    const unsigned long long x = v.w(HW + i);
-    if (x) atomicAdd(st + ISIM_ST_PROM + i, x);
-  }
-  if constexpr (!WIDE) {  // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
-    auto calls_of = [&](uint32_t s) { return lay.cnt16 ? v.lo(CW + s) : v.w(CW + s); };
-    auto errs_of = [&](uint32_t s) { return lay.cnt16 ? v.hi(CW + s) : v.w(CW + S + s); };
-    for (uint32_t i = t0; i < 2u * S; i += ts) {
-      const unsigned long long x = i < S ? calls_of(i) : errs_of(i - S);
-      if (x) atomicAdd(st + ISIM_ST_SITES + i, x);
-    }
-    if (tab) {
-      for (uint32_t s = t0; s < S; s += ts) {
-        const uint32_t w = slot_tbkt[s], bk = w >> 24;
-        const unsigned long long calls = calls_of(s), errs = errs_of(s);
-        if (calls == 0 && errs == 0) continue;
-        // code-200 events = calls - 500s, in u64 wrap-around arithmetic: with the
-        // guarded 16-bit fields the two remainders are independent (the moved
-        // 2^15 steps already counted their share), so it may be "negative"
-        const unsigned long long ok = calls - errs;
-        unsigned long long *row = tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS;
-        if (bk != kTreeDynBucket) {
-          if (ok) atomicAdd(row + bk, ok);
-          if (errs) atomicAdd(row + ISIM_N_PROM + bk, errs);
-        }
-        if (w & kTreeLeafSlot) {  // a leaf callee lasts its latency every time
-          const unsigned long long tc = kp.slot_tc[s];
-          if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
-          if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
-        }
-      }
-      for (uint32_t r = t0; r < lay.n_sum; r += ts) {
-        const unsigned long long x = lay.compact ? v.w(SW + r) : v.q(SW + 2u * r);
-        if (x) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, x);
-      }
-    }
-  } else {  // a wide tree: the hot sites' LDS counters (the cold ones counted in HBM as they came)
-    for (uint32_t i = t0; i < kp.n_lds_slots; i += ts) {
-      const unsigned long long calls = v.lo(CW + i), errs = v.hi(CW + i);
-      if (!calls && !errs) continue;
-      const uint32_t s = kp.lds_slot[i];
-      if (calls) atomicAdd(st + ISIM_ST_SITES + s, calls);
-      if (errs) atomicAdd(st + ISIM_ST_SITES + S + s, errs);
-      const uint32_t w = slot_tbkt[s];
-      if (!tab || !(w & kTreeLeafSlot)) continue;  // (a calling callee's durations came per response)
-      // code-200 events = calls - 500s, in u64 wrap-around arithmetic (the guarded fields, as above)
-      const unsigned long long ok = calls - errs;
-      unsigned long long *row = tab + (uint64_t)wide_row(w) * ISIM_SVC_DUR_WORDS;
-      const uint32_t bk = w >> 24;
-      const unsigned long long tc = kp.slot_tc[s];
-      if (ok) atomicAdd(row + bk, ok);
-      if (errs) atomicAdd(row + ISIM_N_PROM + bk, errs);
-      if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
-      if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
-    }
-    for (uint32_t r = t0; r < lay.n_sum && tab; r += ts) {  // the hot rows' code-200 sums
-      const unsigned long long x = v.q(SW + 2u * r);
-      if (x) atomicAdd(tab + (uint64_t)wide_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, x);
-    }
-  }
-  if (tab) {
-    // the varying LDS rows' bucket tables: one item per (row, word)
-    for (uint32_t i = t0; i < kp.dyn_words; i += ts) {
-      // the table holding word i: the last entry whose header is at or before it
-      uint32_t lo = 0, hi = kp.n_dyn;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (kp.tree_dyn[mid].off <= i) lo = mid;
-        else hi = mid;
-      }
-      const TreeDynRow d = kp.tree_dyn[lo];
-      if (i == d.off) continue;  // the header
-      unsigned long long *row = tab + (uint64_t)(WIDE ? wide_row(d.row) : dur_row(d.row)) * ISIM_SVC_DUR_WORDS;
-      if (lay.compact) {  // code-200 u16 pairs
-        const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
-        const unsigned long long x0 = v.lo(DW + i), x1 = v.hi(DW + i);
-        if (x0) atomicAdd(row + b, x0);
-        if (x1) atomicAdd(row + b + 1u, x1);
-      } else {
-        const unsigned long long x = v.w(DW + i);
-        if (!x) continue;
-        if (WIDE) {  // [width] u32, code 200 (a wide tree's 500s went to HBM)
-          atomicAdd(row + d.b_lo + (i - d.off - 1u), x);
-        } else {  // [code][width] u32
-          const uint32_t j = i - d.off - 1, code = j >= d.width ? 1u : 0u, b = d.b_lo + j - code * d.width;
-          atomicAdd(row + code * ISIM_N_PROM + b, x);
-        }
-      }
-    }
-    // the entry's row: its invocations are the traces (end-to-end histogram and sums)
-    unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;
-    for (uint32_t i = t0; i < 2u * ISIM_N_PROM; i += ts) {
-      const unsigned long long x = v.w(HW + i);
-      if (x) atomicAdd(root + i, x);
-    }
-  }
-  if (!lead) return;
-  const unsigned long long ntr = v.q(A_NTR);
-  if (!ntr) return;
-  const unsigned long long lat = v.q(A_LAT), s5 = v.q(A_LAT500), s2 = lat - s5;
-  if (tab) {
-    unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;
-    if (s2) atomicAdd(root + 2 * ISIM_N_PROM, s2);
-    if (s5) atomicAdd(root + 2 * ISIM_N_PROM + 1, s5);
-  }
-  atomicAdd(st + ISIM_ST_N_TRACES, ntr);
-  atomicAdd(st + ISIM_ST_SUM_LATENCY, lat);
-  atomicAdd(st + ISIM_ST_SUM_HOPS, v.q(A_HOPS));
-  atomicAdd(st + ISIM_ST_SUM_ERR_HOPS, v.q(A_ERR));
-  atomicAdd(st + ISIM_ST_N_500, v.q(A_N500));
-  atomicMax(st + ISIM_ST_NOT_MIN_LATENCY, v.mx(A_NOTMIN));
-  atomicMax(st + ISIM_ST_MAX_LATENCY, v.mx(A_MAX));
-}
-
 // WPE: waves per SIMD the register allocation must allow — 6 (80 VGPRs: two
 // 768-thread workgroups per CU) when the LDS layout fits half the CU, else 4
 // (one 1024-thread workgroup per CU: up to 128 VGPRs, no spills).
@@ -727,67 +542,119 @@ __global__ void __launch_bounds__(kWgThreads, WPE)
     }
   }
   __syncthreads();
-  // ---- the workgroup's accumulators: as raw words into the launch's
-  // partials (isim_tree_fold adds them up and flushes ONCE per launch), or
-  // flushed here by global atomics (a launch captured into a HIP graph)
-  if (kp.part) {
-    uint32_t *dst = kp.part + (size_t)blockIdx.x * kp.part_words;
-    if ((kp.part_words & 1u) == 0) {  // 8-byte words (ds_read_b64, global_store_dwordx2)
-      const lds_u64 *src = (const lds_u64 *)lds;
-      for (uint32_t i = threadIdx.x; i < kp.part_words / 2u; i += blockDim.x)
-        reinterpret_cast<unsigned long long *>(dst)[i] = src[i];
-    } else {
-      const __attribute__((address_space(3))) uint32_t *src = (const __attribute__((address_space(3))) uint32_t *)lds;
-      for (uint32_t i = threadIdx.x; i < kp.part_words; i += blockDim.x) dst[i] = src[i];
-    }
-    return;
+  // ---- flush the workgroup's accumulators (coalesced over slots / rows)
+  unsigned long long *st = reinterpret_cast<unsigned long long *>(gstats);
+  for (uint32_t i = threadIdx.x; i < kHistWords; i += blockDim.x)
+    if (c.hist[i]) atomicAdd(st + ISIM_ST_PROM + i, (unsigned long long)c.hist[i]);
+  // per-slot calls and 500s (their guarded 16-bit fields or the two u32 tables)
+  if constexpr (!WIDE) {
+  auto calls_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] & 0xFFFFu) : c.cnt[s]; };
+  auto errs_of = [&](uint32_t s) -> uint32_t { return lay.cnt16 ? (c.cnt[s] >> 16) : c.cnt[S + s]; };
+  for (uint32_t i = threadIdx.x; i < 2u * S; i += blockDim.x) {
+    const uint32_t v = i < S ? calls_of(i) : errs_of(i - S);
+    if (v) atomicAdd(st + ISIM_ST_SITES + i, (unsigned long long)v);
   }
-  tree_flush<WIDE>(LdsVal{reinterpret_cast<const uint32_t *>(lds)}, threadIdx.x, blockDim.x, threadIdx.x == 0, gstats,
-                   slot_tbkt, kp);
-}
-
-// The launch's fold, in two kernels: the workgroups' partial words summed per
-// slice of kTreeFoldSlice workgroups (one thread per (word, slice): its loads
-// all in flight), then the same flush over the slices' sums — one atomic per
-// nonzero statistic per LAUNCH instead of per workgroup (c3p's 256
-// workgroups each flushed ~50k counters: 1.1 GB of WRITE per 2^22 launch
-// against 67 MB of records)
-template <int = 0>  // (a template: one definition across the four objects of this file)
-__global__ void __launch_bounds__(256) isim_tree_fold_sum(const uint32_t *__restrict__ part, uint32_t pw,
-                                                          uint32_t groups, uint2 *__restrict__ img) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, k = blockIdx.y;
-  if (i >= pw) return;
-  const uint32_t g0 = k * kTreeFoldSlice, g1 = g0 + kTreeFoldSlice < groups ? g0 + kTreeFoldSlice : groups;
-  uint2 *out = img + (size_t)k * pw;
-  if (i >= kAccMaxLo && i < kAccMaxHi) {  // the WgAcc maxima (u64 word pairs): the slice's max
-    if (i & 1u) return;
-    unsigned long long m = 0;
-    for (uint32_t g = g0; g < g1; ++g) {
+  if (c.svc_tab) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
+      const uint32_t w = slot_tbkt[s], bk = w >> 24;
+      const uint32_t calls = calls_of(s), errs = errs_of(s);
+      if (calls == 0 && errs == 0) continue;
+      // code-200 events = calls - 500s, in u64 wrap-around arithmetic: with the
+      // guarded 16-bit fields the two remainders are independent (the moved
+      // 2^15 steps already counted their share), so it may be "negative"
+      const unsigned long long ok = (unsigned long long)calls - (unsigned long long)errs;
+      unsigned long long *row = tab + (uint64_t)dur_row(w) * ISIM_SVC_DUR_WORDS;
+      if (bk != kTreeDynBucket) {
+        if (ok) atomicAdd(row + bk, ok);
+        if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
+      }
+      if (w & kTreeLeafSlot) {  // a leaf callee lasts its latency every time
+        const unsigned long long tc = kp.slot_tc[s];
+        if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
+        if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
+      }
+    }
+    for (uint32_t r = threadIdx.x; r < lay.n_sum; r += blockDim.x) {
       const unsigned long long v =
-          (unsigned long long)part[(size_t)g * pw + i] | (unsigned long long)part[(size_t)g * pw + i + 1] << 32;
-      m = v > m ? v : m;
-    }
-    out[i] = make_uint2((uint32_t)m, 0u);
-    out[i + 1] = make_uint2((uint32_t)(m >> 32), 0u);
-    return;
-  }
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kTreeFoldSlice; ++j) {
-    if (g0 + j < g1) {
-      const uint32_t v = part[(size_t)(g0 + j) * pw + i];
-      lo += v & 0xFFFFu;
-      hi += v >> 16;
+          lay.compact ? (unsigned long long)((uint32_t *)sum200)[r] : ((unsigned long long *)sum200)[r];
+      if (v) atomicAdd(tab + (uint64_t)dur_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
     }
   }
-  out[i] = make_uint2(lo, hi);
-}
-template <bool WIDE>
-__global__ void __launch_bounds__(256) isim_tree_fold(uint64_t *__restrict__ gstats,
-                                                      const uint32_t *__restrict__ slot_tbkt, KParams kp,
-                                                      const uint2 *__restrict__ img, uint32_t slices) {
-  tree_flush<WIDE>(ImgVal{img, kp.part_words, slices}, blockIdx.x * blockDim.x + threadIdx.x,
-                   gridDim.x * blockDim.x, blockIdx.x == 0 && threadIdx.x == 0, gstats, slot_tbkt, kp);
+  } else {  // a wide tree: the hot sites' LDS counters (the cold ones counted in HBM as they came)
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
+    for (uint32_t i = threadIdx.x; i < kp.n_lds_slots; i += blockDim.x) {
+      const uint32_t v = c.cnt[i], calls = v & 0xFFFFu, errs = v >> 16;
+      if (!v) continue;
+      const uint32_t s = kp.lds_slot[i];
+      if (calls) atomicAdd(st + ISIM_ST_SITES + s, (unsigned long long)calls);
+      if (errs) atomicAdd(st + ISIM_ST_SITES + S + s, (unsigned long long)errs);
+      const uint32_t w = slot_tbkt[s];
+      if (!tab || !(w & kTreeLeafSlot)) continue;  // (a calling callee's durations came per response)
+      // code-200 events = calls - 500s, in u64 wrap-around arithmetic (the guarded fields, as above)
+      const unsigned long long ok = (unsigned long long)calls - (unsigned long long)errs;
+      unsigned long long *row = tab + (uint64_t)wide_row(w) * ISIM_SVC_DUR_WORDS;
+      const uint32_t bk = w >> 24;
+      const unsigned long long tc = kp.slot_tc[s];
+      if (ok) atomicAdd(row + bk, ok);
+      if (errs) atomicAdd(row + ISIM_N_PROM + bk, (unsigned long long)errs);
+      if (ok && tc) atomicAdd(row + 2 * ISIM_N_PROM, tc * ok);
+      if (errs && tc) atomicAdd(row + 2 * ISIM_N_PROM + 1, tc * errs);
+    }
+    for (uint32_t r = threadIdx.x; r < lay.n_sum && tab; r += blockDim.x) {  // the hot rows' code-200 sums
+      const unsigned long long v = ((unsigned long long *)sum200)[r];
+      if (v) atomicAdd(tab + (uint64_t)wide_row(kp.sum_row[r]) * ISIM_SVC_DUR_WORDS + 2 * ISIM_N_PROM, v);
+    }
+  }  // !WIDE
+  if (c.svc_tab) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
+    // the varying LDS rows' bucket tables: one thread per (row, word)
+    for (uint32_t i = threadIdx.x; i < kp.dyn_words; i += blockDim.x) {
+      const uint32_t v = dyn[i];
+      if (!v) continue;
+      // the table holding word i: the last entry whose header is at or before it
+      uint32_t lo = 0, hi = kp.n_dyn;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (kp.tree_dyn[mid].off <= i) lo = mid;
+        else hi = mid;
+      }
+      const TreeDynRow d = kp.tree_dyn[lo];
+      if (i == d.off) continue;  // the header
+      unsigned long long *row = tab + (uint64_t)(WIDE ? wide_row(d.row) : dur_row(d.row)) * ISIM_SVC_DUR_WORDS;
+      if (lay.compact) {  // code-200 u16 pairs
+        const uint32_t b = d.b_lo + 2u * (i - d.off - 1u);
+        if (v & 0xFFFFu) atomicAdd(row + b, (unsigned long long)(v & 0xFFFFu));
+        if (v >> 16) atomicAdd(row + b + 1u, (unsigned long long)(v >> 16));
+      } else if (WIDE) {  // [width] u32, code 200 (a wide tree's 500s went to HBM)
+        atomicAdd(row + d.b_lo + (i - d.off - 1u), (unsigned long long)v);
+      } else {  // [code][width] u32
+        const uint32_t j = i - d.off - 1, code = j >= d.width ? 1u : 0u, b = d.b_lo + j - code * d.width;
+        atomicAdd(row + code * ISIM_N_PROM + b, (unsigned long long)v);
+      }
+    }
+  }
+  if (c.svc_tab) {
+    unsigned long long *tab = reinterpret_cast<unsigned long long *>(c.svc_tab);
+    // the entry's row: its invocations are the traces (end-to-end histogram and sums)
+    unsigned long long *root = tab + (uint64_t)(kp.root_dur & kDurRowMask) * ISIM_SVC_DUR_WORDS;
+    for (uint32_t i = threadIdx.x; i < 2u * ISIM_N_PROM; i += blockDim.x)
+      if (c.hist[i]) atomicAdd(root + i, (unsigned long long)c.hist[i]);
+    if (threadIdx.x == 0 && c.acc->ntr) {
+      const unsigned long long s5 = c.acc->sum_latency500, s2 = c.acc->sum_latency - s5;
+      if (s2) atomicAdd(root + 2 * ISIM_N_PROM, s2);
+      if (s5) atomicAdd(root + 2 * ISIM_N_PROM + 1, s5);
+    }
+  }
+  if (threadIdx.x == 0 && c.acc->ntr) {
+    atomicAdd(st + ISIM_ST_N_TRACES, c.acc->ntr);
+    atomicAdd(st + ISIM_ST_SUM_LATENCY, c.acc->sum_latency);
+    atomicAdd(st + ISIM_ST_SUM_HOPS, c.acc->sum_hops);
+    atomicAdd(st + ISIM_ST_SUM_ERR_HOPS, c.acc->sum_err);
+    atomicAdd(st + ISIM_ST_N_500, c.acc->n500);
+    atomicMax(st + ISIM_ST_NOT_MIN_LATENCY, c.acc->notmin);
+    atomicMax(st + ISIM_ST_MAX_LATENCY, c.acc->max);
+  }
 }
 
 }  // namespace dev
@@ -843,13 +710,6 @@ static void *tree_pick(uint32_t frames, bool spill, bool occ2, bool t64, bool wi
   if (frames <= 12) return (void *)&isim_tree<M, 12, false, NLDS, C, DRAW, 4>;
   return (void *)&isim_tree<M, 16, false, NLDS, C, DRAW, 4>;
 }
-
-#if TREE_MODEB == 0 && TREE_CONC == 0  // (one definition: this object)
-void *tree_fold_kernel(bool wide) {
-  return wide ? (void *)&dev::isim_tree_fold<true> : (void *)&dev::isim_tree_fold<false>;
-}
-void *tree_fold_sum_kernel() { return (void *)&dev::isim_tree_fold_sum<>; }
-#endif
 
 #define TREE_CAT2(a, b, c) a##b##c
 #define TREE_CAT(a, b, c) TREE_CAT2(a, b, c)
