@@ -666,10 +666,11 @@ __device__ __forceinline__ uint64_t tie_key(const K &k, uint32_t i) {
   return ((uint64_t)k.itr[i] << 32) | k.ihop[i];
 }
 // runs of equal keys in a sorted round, re-ordered by (trace, hop): the run's
-// first thread sorts it — insertion sort for short runs (the common case:
-// runs are rare and short), heapsort past kTieInsert so that one lane's work
-// stays O(r log r) when many items meet one service at one instant (a wide
-// fan-out to one replica, near-zero gaps).  Tie keys are unique
+// first thread sorts it — insertion sort (runs are mostly short, or long
+// and already in order), bounded on runs past kTieInsert by 8 moves per item,
+// then heapsort, so that one lane's work stays O(r log r) when many items
+// meet one service at one instant out of order (a wide fan-out to one
+// replica, near-zero gaps).  Tie keys are unique
 // (one item per (trace, hop)), so the order is the same either way.  LIST:
 // the values are list indices into ids (k_qkey1), else item ids (k_qkey2)
 constexpr uint64_t kTieInsert = 32;
@@ -682,19 +683,25 @@ __global__ void __launch_bounds__(kT) k_tiefix(K k, const uint64_t *key, uint32_
     if (key[j + 1] != kj || (j > 0 && key[j - 1] == kj)) continue;  // the first of a run of ties only
     uint64_t e = j + 2;
     while (e < m && key[e] == kj) ++e;
-    if (e - j <= kTieInsert) {
-      for (uint64_t x = j + 1; x < e; ++x) {
-        const uint32_t v = val[x];
-        const uint64_t t = tk(v);
-        uint64_t y = x;
-        while (y > j && tk(val[y - 1]) > t) {
-          val[y] = val[y - 1];
-          --y;
-        }
-        val[y] = v;
+    // insertion sort: the stable radix sort leaves a run in its list order,
+    // usually (trace, hop) order already, so this is O(run) — with a budget
+    // of moves on a long run; past it (a wide fan-out meeting one service at
+    // one instant) a heapsort, O(run log run).  (Heapsort alone
+    // on every run past 32 items made c5p 26x slower: its long runs are
+    // already in order.)
+    const uint64_t budget = e - j <= kTieInsert ? ~0ull : 8u * (e - j);
+    uint64_t moves = 0;
+    for (uint64_t x = j + 1; x < e && moves <= budget; ++x) {
+      const uint32_t v = val[x];
+      const uint64_t t = tk(v);
+      uint64_t y = x;
+      while (y > j && tk(val[y - 1]) > t && ++moves <= budget) {
+        val[y] = val[y - 1];
+        --y;
       }
-      continue;
+      val[y] = v;  // (the run stays a permutation when the budget runs out)
     }
+    if (moves <= budget) continue;
     // heapsort of val[j, e) by tie key (a max-heap, then the max moved to the end)
     uint32_t *a = val + j;
     const uint64_t r = e - j;
