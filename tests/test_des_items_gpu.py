@@ -139,6 +139,16 @@ def test_items_mode_b(gpu, name, mean):
     c.compare((1 << 32) - 500, 1001)
 
 
+def test_items_tie_runs_out_of_order(gpu):
+    # arrivals 1 ns apart on average: many traces start at the same instant, so
+    # z's sorted round holds runs of equal keys from many traces in the
+    # round's position-major list order — far from (trace, hop) order, past
+    # k_tiefix's insertion-sort budget: its heapsort
+    c = DesCase(CASES["fanout_ties"](), 1)
+    c.compare(0, 3000)
+    c.compare((1 << 32) - 500, 1001)
+
+
 @pytest.mark.parametrize("n", [1, 2, 63, 257])
 def test_items_ragged(gpu, n):
     DesCase(CASES["real300p60"](), 1_000_000).compare(55, n)
